@@ -1,0 +1,252 @@
+/*
+ * oracle/ref/ref_driver.c -- TEST INFRASTRUCTURE ONLY (this container).
+ *
+ * Links the reference's own FEC scheme pluglets, compiled in place from
+ * /root/reference/plugins/fec/fec_scheme_protoops/*.c by oracle/ref/Makefile, into
+ * oracle/_ref/libfecref.so, and drives them the way plugin_run_protoop_internal
+ * (picoquic/plugin.c:1279-1450) does: inputs through get_cnx(cnx, AK_CNX_INPUT, i),
+ * outputs through set_cnx(cnx, AK_CNX_OUTPUT, i, v) (picoquic/getset.c:137-142,370-379).
+ *
+ * Stubs for the six pluglet API symbols the scheme objects import:
+ *   get_cnx / set_cnx   -> global argument arrays
+ *   my_malloc           -> malloc of max(size, 2100): the plugin allocator hands out
+ *                          fixed 2100-B slots (picoquic/memory.c:72-95,181-191) and the
+ *                          RLC encoder relies on it (knowns[] is under-allocated,
+ *                          rlc_fec_scheme_generate_gf256.c:50)
+ *   my_free / my_memcpy / my_memset -> libc
+ * Recover runs in a fork()ed child because the reference decoder dereferences x[-1]
+ * on some erasure patterns (rlc_fec_scheme_gf256.c:74-77).
+ */
+#include <signal.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <stddef.h>
+#include "fec/fec.h"             /* resolved with -I$(REF)/plugins */
+#include "fec/prng/tinymt32.c"
+
+/* ---- pluglet API stubs ---- */
+static protoop_arg_t g_in[PROTOOPARGS_MAX];
+static protoop_arg_t g_out[PROTOOPARGS_MAX];
+
+protoop_arg_t get_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param) {
+    (void)cnx;
+    if (ak == AK_CNX_INPUT) return g_in[param];
+    if (ak == AK_CNX_OUTPUT) return g_out[param];
+    return 0;
+}
+void set_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, protoop_arg_t val) {
+    (void)cnx;
+    if (ak == AK_CNX_OUTPUT) g_out[param] = val;
+    else if (ak == AK_CNX_INPUT) g_in[param] = val;
+}
+void *my_malloc(picoquic_cnx_t *cnx, unsigned int size) {
+    (void)cnx;
+    return malloc(size < 2100 ? 2100 : size);
+}
+void my_free(picoquic_cnx_t *cnx, void *ptr) { (void)cnx; free(ptr); }
+void *my_memcpy(void *d, const void *s, size_t n) { return memcpy(d, s, n); }
+void *my_memset(void *d, int c, size_t n) { return memset(d, c, n); }
+
+/* ---- the reference pluglets, renamed per TU by the Makefile ---- */
+protoop_arg_t rlc_create(picoquic_cnx_t *cnx);
+protoop_arg_t rlc_encode(picoquic_cnx_t *cnx);
+protoop_arg_t rlc_decode(picoquic_cnx_t *cnx);
+protoop_arg_t xor_create(picoquic_cnx_t *cnx);
+protoop_arg_t xor_encode(picoquic_cnx_t *cnx);
+protoop_arg_t xor_decode(picoquic_cnx_t *cnx);
+
+typedef struct { uint8_t **table_mul; uint8_t *table_inv; } ref_rlc_scheme_t;
+static ref_rlc_scheme_t *g_scheme;
+
+static ref_rlc_scheme_t *scheme(void) {
+    if (!g_scheme) {
+        memset(g_out, 0, sizeof g_out);
+        if (rlc_create(NULL) == 0) g_scheme = (ref_rlc_scheme_t *)g_out[0];
+    }
+    return g_scheme;
+}
+
+int ref_gf_tables(uint8_t *mul, uint8_t *inv) {
+    ref_rlc_scheme_t *s = scheme();
+    if (!s) return -1;
+    for (int a = 0; a < 256; a++) memcpy(mul + 256 * a, s->table_mul[a], 256);
+    memcpy(inv, s->table_inv, 256);
+    return 0;
+}
+
+int ref_create_outputs(int xor_scheme, uint64_t *out0, uint64_t *out1) {
+    memset(g_out, 0, sizeof g_out);
+    int ret = (int)(xor_scheme ? xor_create(NULL) : rlc_create(NULL));
+    *out0 = g_out[0]; *out1 = g_out[1];
+    return ret;
+}
+
+void ref_tinymt32(uint32_t seed, int n, uint32_t *out) {
+    tinymt32_t t;
+    t.mat1 = 0x8f7011ee; t.mat2 = 0xfc78ff1f; t.tmat = 0x3793fdff;
+    tinymt32_init(&t, seed);
+    for (int i = 0; i < n; i++) out[i] = tinymt32_generate_uint32(&t);
+}
+
+static source_symbol_t *mk_source(uint32_t fbn, int j, const uint8_t *data, uint16_t len) {
+    source_symbol_t *s = my_malloc(NULL, sizeof *s);
+    memset(s, 0, sizeof *s);
+    s->fec_block_offset = (uint8_t)j;
+    s->fec_block_number = fbn;
+    s->data = my_malloc(NULL, len);
+    memcpy(s->data, data, len);
+    s->data_length = len;
+    return s;
+}
+
+/* Encode one block.  rep_out receives r * max_len bytes; meta_out per repair:
+ * [raw fpid u64, data_length].  Returns the pluglet's return code. */
+int ref_encode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
+               const uint16_t *src_len, int src_stride, uint8_t *rep_out, int rep_stride,
+               uint64_t *fpid_out, uint16_t *len_out) {
+    fec_block_t *fb = calloc(1, sizeof *fb);
+    fb->fec_block_number = fbn;
+    fb->total_source_symbols = (uint8_t)k;
+    fb->total_repair_symbols = (uint8_t)r;
+    for (int j = 0; j < k; j++)
+        fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+    fb->current_source_symbols = (uint8_t)k;
+    g_in[0] = (protoop_arg_t)fb;
+    g_in[1] = (protoop_arg_t)scheme();
+    int ret = (int)(xor_scheme ? xor_encode(NULL) : rlc_encode(NULL));
+    if (ret == 0) {
+        for (int i = 0; i < r; i++) {
+            repair_symbol_t *rs = fb->repair_symbols[i];
+            if (!rs) { len_out[i] = 0; fpid_out[i] = 0; continue; }
+            memcpy(rep_out + (size_t)i * rep_stride, rs->data, rs->data_length);
+            len_out[i] = rs->data_length;
+            fpid_out[i] = rs->repair_fec_payload_id.raw;
+        }
+    }
+    return ret;
+}
+
+/* Recover one block in a child process.
+ * src / rep: dense [k][stride] / [r][stride]; presence bytes per symbol.
+ * rep_fpid: raw repair FPIDs (the seed is its low 32 bits, rlc_fec_scheme_gf256.c:200).
+ * out: [k][out_stride]; recovered[j] = 1 when the pluglet inserted source j.
+ * Returns the pluglet's return code, or -1000 - signal when the child died. */
+int ref_decode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
+               const uint16_t *src_len, const uint8_t *src_present, int src_stride,
+               const uint8_t *rep, const uint16_t *rep_len, const uint8_t *rep_present,
+               const uint64_t *rep_fpid, int rep_stride, uint8_t *out, uint16_t *out_len,
+               uint8_t *recovered, int out_stride) {
+    size_t shm_len = (size_t)k * out_stride + (size_t)k * 3 + 64;
+    uint8_t *shm = mmap(NULL, shm_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (shm == MAP_FAILED) return -2000;
+    memset(shm, 0, shm_len);
+    pid_t pid = fork();
+    if (pid == 0) {
+        fec_block_t *fb = calloc(1, sizeof *fb);
+        fb->fec_block_number = fbn;
+        fb->total_source_symbols = (uint8_t)k;
+        fb->total_repair_symbols = (uint8_t)r;
+        for (int j = 0; j < k; j++)
+            if (src_present[j]) {
+                fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+                fb->current_source_symbols++;
+            }
+        for (int i = 0; i < r; i++)
+            if (rep_present[i]) {
+                repair_symbol_t *rs = my_malloc(NULL, sizeof *rs);
+                memset(rs, 0, sizeof *rs);
+                rs->repair_fec_payload_id.raw = rep_fpid[i];
+                rs->data = my_malloc(NULL, rep_len[i]);
+                memcpy(rs->data, rep + (size_t)i * rep_stride, rep_len[i]);
+                rs->data_length = rep_len[i];
+                fb->repair_symbols[i] = rs;
+                fb->current_repair_symbols++;
+            }
+        source_symbol_t *before[MAX_SYMBOLS_PER_FEC_BLOCK];
+        memcpy(before, fb->source_symbols, sizeof before);
+        g_in[0] = (protoop_arg_t)fb;
+        g_in[1] = (protoop_arg_t)scheme();
+        int ret = (int)(xor_scheme ? xor_decode(NULL) : rlc_decode(NULL));
+        int32_t *hdr = (int32_t *)shm;
+        hdr[0] = ret;
+        uint8_t *rec = shm + 64, *lens = rec + k, *data = lens + 2 * (size_t)k;
+        for (int j = 0; j < k; j++) {
+            source_symbol_t *ss = fb->source_symbols[j];
+            if (ss && ss != before[j]) {
+                rec[j] = 1;
+                uint16_t L = ss->data_length;
+                memcpy(lens + 2 * j, &L, 2);
+                memcpy(data + (size_t)j * out_stride, ss->data, L > out_stride ? out_stride : L);
+            }
+        }
+        _exit(0);
+    }
+    int status = 0;
+    waitpid(pid, &status, 0);
+    int ret;
+    if (WIFEXITED(status) && WEXITSTATUS(status) == 0) {
+        ret = ((int32_t *)shm)[0];
+        uint8_t *rec = shm + 64, *lens = rec + k, *data = lens + 2 * (size_t)k;
+        for (int j = 0; j < k; j++) {
+            recovered[j] = rec[j];
+            memcpy(&out_len[j], lens + 2 * j, 2);
+            if (rec[j]) memcpy(out + (size_t)j * out_stride, data + (size_t)j * out_stride, out_len[j]);
+        }
+    } else {
+        ret = WIFSIGNALED(status) ? -1000 - WTERMSIG(status) : -1000;
+        memset(recovered, 0, (size_t)k);
+    }
+    munmap(shm, shm_len);
+    return ret;
+}
+
+/* Batched encode for the calibration leg (no fork): same layout as the device engine. */
+int ref_rlc_encode_batch(const uint8_t *src, uint8_t *rep, uint64_t nblocks, int k, int r,
+                         int L, uint32_t fbn_base) {
+    uint16_t lens[256], rl[256];
+    uint64_t fp[256];
+    for (int j = 0; j < k; j++) lens[j] = (uint16_t)L;
+    for (uint64_t b = 0; b < nblocks; b++) {
+        fec_block_t fb;
+        memset(&fb, 0, sizeof fb);
+        fb.fec_block_number = (uint32_t)((fbn_base + b) & 0xffffff);
+        fb.total_source_symbols = (uint8_t)k;
+        fb.total_repair_symbols = (uint8_t)r;
+        fb.current_source_symbols = (uint8_t)k;
+        source_symbol_t ss[256];
+        for (int j = 0; j < k; j++) {
+            memset(&ss[j], 0, sizeof ss[j]);
+            ss[j].data = (uint8_t *)src + (b * k + j) * L;
+            ss[j].data_length = (uint16_t)L;
+            fb.source_symbols[j] = &ss[j];
+        }
+        g_in[0] = (protoop_arg_t)&fb;
+        g_in[1] = (protoop_arg_t)scheme();
+        if (rlc_encode(NULL) != 0) return -1;
+        for (int i = 0; i < r; i++) {
+            memcpy(rep + (b * r + i) * L, fb.repair_symbols[i]->data, L);
+            my_free(NULL, fb.repair_symbols[i]->data);
+            my_free(NULL, fb.repair_symbols[i]);
+        }
+    }
+    (void)lens; (void)rl; (void)fp;
+    return 0;
+}
+
+/* Layout facts the product's layout-compatible header must match (fec.h:44-130). */
+int ref_layout(uint64_t *out) {
+    out[0] = sizeof(fec_block_t);
+    out[1] = sizeof(source_symbol_t);
+    out[2] = sizeof(repair_symbol_t);
+    out[3] = offsetof(fec_block_t, source_symbols);
+    out[4] = offsetof(fec_block_t, repair_symbols);
+    out[5] = offsetof(source_symbol_t, data);
+    out[6] = offsetof(repair_symbol_t, data);
+    out[7] = sizeof(repair_fpid_t);
+    return 8;
+}
