@@ -1,0 +1,246 @@
+"""bench.py -- FEC encode+decode throughput of the MI355X engine (device-resident).
+
+Workload per GPU (BASELINE.json configs[1] + configs[2]): 2^20 independent FEC blocks of
+k = 16 source symbols x 1200 B; one step = RLC encode of r = 4 repairs for every block,
+then RLC decode of every block with 4 random source erasures (all 4 repairs received),
+recovered in place.  Inputs are synthetic (SplitMix64 bytes) and resident in HBM before the
+timed region.  value = source payload (k * L * blocks, all ranks) / step time, in GiB/s:
+each payload byte is both encoded and decoded inside one step.
+
+Multi-GPU (torchrun, one process per GPU): blocks are partitioned, each rank owns its own
+2^20 blocks (fbn offset by rank), there is no data-path collective (a FEC block never spans
+GPUs); barrier + max-over-ranks timing only.  scaling = weak.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E 8.0 TB/s)
+METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--blocks", type=int, default=1 << 20, help="FEC blocks per GPU")
+    p.add_argument("--k", type=int, default=16)
+    p.add_argument("--r", type=int, default=4)
+    p.add_argument("--erasures", type=int, default=4)
+    p.add_argument("--symbol", type=int, default=1200)
+    p.add_argument("--no-legs", action="store_true", help="skip the k=32 r=8 encode leg")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def load_traffic(kernel_tag: str):
+    """HBM bytes per launch from the committed PMC profile (profiles/*_pmc.json), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        v = d.get(kernel_tag, {}).get("hbm_bytes_per_launch_corrected")
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def make_erasures(torch, nb, k, e, seed, dev):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    keys = torch.rand((nb, k), generator=g)
+    miss = keys.argsort(dim=1)[:, :e]
+    pres = torch.ones((nb, k), dtype=torch.bool)
+    pres.scatter_(1, miss, False)
+    w = 1 << torch.arange(min(k, 63), dtype=torch.int64)
+    sp = torch.zeros((nb, 2), dtype=torch.int64)
+    sp[:, 0] = (pres[:, : min(k, 63)].to(torch.int64) * w).sum(1)
+    if k > 63:
+        raise SystemExit("bench erasure masks support k <= 63")
+    return sp.to(dev), miss
+
+
+def cpu_baseline(args, nthreads):
+    """The oracle (CPU restatement, bit-exact with the reference; kind "port") on a bounded
+    sample of the same workload, all threads of this process's CPU share."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle_py import Oracle, synth_bytes
+    o = Oracle()
+    k, r, L, e = args.k, args.r, args.symbol, args.erasures
+
+    def run(nb):
+        src = synth_bytes(nb * k * L, 0x5EEDF3C0).reshape(nb, k, L)
+        rng = np.random.default_rng(1)
+        sp = np.zeros((nb, 2), np.uint64)
+        rp = np.zeros((nb, 2), np.uint64)
+        full = (1 << k) - 1
+        for b in range(nb):
+            m = full
+            for j in rng.choice(k, e, replace=False):
+                m &= ~(1 << int(j))
+            sp[b, 0] = m
+            rp[b, 0] = (1 << r) - 1
+        t0 = time.perf_counter()
+        rep = o.rlc_encode_batch(src, r, 0, nthreads)
+        o.rlc_decode_batch(src, rep, sp, rp, 0, nthreads)
+        return time.perf_counter() - t0
+
+    nb = 2048
+    t = run(nb)
+    nb2 = int(min(max(nb * args.cpu_seconds / max(t, 1e-3), nb), 1 << 17))
+    t2 = run(nb2)
+    gib = nb2 * k * L / 2**30
+    return {"value": gib / t2, "unit": "GiB/s", "cores": nthreads, "kind": "port",
+            "sample": f"{nb2} blocks k={k} r={r} L={L}: RLC encode + decode with {e} erasures, "
+                      f"oracle/fec_oracle.c -O2, {nthreads} pthreads, {t2:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    from pquic_amd import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    eng = Engine(local)
+
+    nb, k, r, L, e = args.blocks, args.k, args.r, args.symbol, args.erasures
+    fbn_base = (rank * nb) & 0xFFFFFF
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
+    eng.synth_fill(src, src.numel(), 0x5EEDF3C0, rank * src.numel())
+    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
+    work = torch.empty_like(src)
+    sp, miss = make_erasures(torch, nb, k, e, 11 + rank, dev)
+    rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
+    rp[:, 0] = (1 << r) - 1
+    status = torch.empty(nb, dtype=torch.uint8, device=dev)
+    recovered = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+    ws = eng.alloc_workspace(nb, k, r)
+    # decode input: the received block (erased slots hold stale bytes); copied once, and the
+    # recovered symbols are rewritten in place by every decode pass
+    work.copy_(src)
+    idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
+    work.view(nb * k, L)[idx] = 0xA5
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        eng.rlc_encode(src, rep, k, r, L, fbn_base=fbn_base)
+        if ev:
+            ev[1].record(stream)
+        eng.rlc_decode(work, rep, sp, rp, status, recovered, k, r, L, fbn_base=fbn_base, workspace=ws)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate on the benchmarked data: every recovered block equals the original
+    ok = status == 0
+    assert bool((work[ok] == src[ok]).all()), "decode did not restore the sources"
+    n_ub = int((status == 2).sum())
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(evs[s])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    enc_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / args.steps
+    dec_ms = sum(ev[1].elapsed_time(ev[2]) for ev in evs) / args.steps
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    payload = nb * k * L  # per GPU per step
+    value = world * payload * args.steps / elapsed / 2**30
+    enc_bytes = (k + r) * L * nb
+    dec_bytes = (k + e) * L * nb
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
+
+    legs = {
+        "rlc_encode_k16_r4": {"ms": round(enc_ms, 3), "payload_GiB_s": round(payload / (enc_ms * 1e-3) / 2**30, 2),
+                              "algorithmic_GB_s": round(enc_gbs, 1), "hbm_frac": round(enc_gbs / HBM_PEAK_GBS, 4)},
+        "rlc_decode_k16_e4": {"ms": round(dec_ms, 3), "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
+                              "algorithmic_GB_s": round(dec_gbs, 1), "hbm_frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                              "ref_ub_blocks": n_ub},
+    }
+    del work, ws
+    if not args.no_legs and world == 1:
+        # north-star leg: k = 32, r = 8 encode, 2^21 blocks (one GPU's share of config 4)
+        nb2, k2, r2 = 1 << 21, 32, 8
+        del src, rep
+        torch.cuda.empty_cache()
+        s2 = torch.empty((nb2, k2, L), dtype=torch.uint8, device=dev)
+        eng.synth_fill(s2, s2.numel(), 0x5EEDF3C0, 0)
+        r2t = torch.empty((nb2, r2, L), dtype=torch.uint8, device=dev)
+        for _ in range(2):
+            eng.rlc_encode(s2, r2t, k2, r2, L)
+        a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(5):
+            eng.rlc_encode(s2, r2t, k2, r2, L)
+        b_.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b_) / 5
+        gbs = (k2 + r2) * L * nb2 / (ms * 1e-3) / 1e9
+        legs["rlc_encode_k32_r8"] = {"ms": round(ms, 3), "blocks": nb2,
+                                     "payload_GiB_s": round(nb2 * k2 * L / (ms * 1e-3) / 2**30, 2),
+                                     "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                                     "traffic": load_traffic("rlc_encode_k32_r8")}
+        del s2, r2t
+
+    if rank == 0:
+        dom = "rlc_encode_k16_r4" if enc_ms >= dec_ms else "rlc_decode_k16_e4"
+        ach = enc_gbs if dom == "rlc_encode_k16_r4" else dec_gbs
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom),
+                "bytes_per_launch": enc_bytes if dom.startswith("rlc_encode") else dec_bytes}
+        cpu = None
+        if not args.no_cpu and world == 1:
+            nthreads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+            cpu = cpu_baseline(args, nthreads)
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "config": {"workload": "RLC-GF(256) encode k=16 r=4 + decode 4 erasures, 1200B symbols",
+                          "k": k, "r": r, "erasures": e, "symbol_bytes": L, "blocks_per_gpu": nb,
+                          "parallelism": f"independent FEC blocks, {world} GPU(s), no collective"},
+               "roofline": roof, "cpu_baseline": cpu, "legs": legs}
+        print(json.dumps(out))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

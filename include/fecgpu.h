@@ -1,0 +1,104 @@
+/*
+ * include/fecgpu.h -- C ABI of the MI355X FEC engine (libpquic_fec.so).
+ *
+ * Batched, device-resident replacement for the arithmetic inside PQUIC's FEC scheme
+ * pluglets (plugins/fec/fec_scheme_protoops/):
+ *   fecgpu_rlc_encode  <- fec_generate_repair_symbols, RLC-GF(256)
+ *                         (rlc_fec_scheme_generate_gf256.c:24-77)
+ *   fecgpu_rlc_decode  <- fec_recover, RLC-GF(256) Gaussian elimination
+ *                         (rlc_fec_scheme_gf256.c:134-251)
+ *   fecgpu_xor_encode  <- fec_generate_repair_symbols, XOR (xor_fec_scheme_generate.c:41-78)
+ *   fecgpu_xor_decode  <- fec_recover, XOR (xor_fec_scheme.c:41-74)
+ * The per-block protoop adapters that keep the reference's hook surface are declared in
+ * include/pquic_fec_protoops.h and call these entry points.
+ *
+ * Layout (all device pointers, HBM-resident, 4-byte aligned):
+ *   src  [nblocks][k][symbol_size]   source symbols of consecutive FEC blocks
+ *   rep  [nblocks][r][symbol_size]   repair symbols
+ * Equal-length symbols; symbol_size % 4 == 0 (callers with ragged payloads zero-pad to a
+ * common length, which is what the reference does internally: every symbol of a block is
+ * treated as zero-padded to max(data_length)).
+ * FEC block number of block b: fbn[b] if fbn != NULL, else (fbn_base + b) mod 2^24.
+ * RLC coefficients of repair i of block fbn come from TinyMT32 seeded with
+ * (fbn << 8) | i, exactly as the reference (fec.h:44-75).
+ *
+ * `stream` is a hipStream_t (NULL = the null stream).  Every call is asynchronous and
+ * graph-capturable: no allocation, no synchronisation inside.
+ */
+#ifndef PQUIC_FECGPU_H
+#define PQUIC_FECGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Call status. */
+#define FECGPU_OK              0
+#define FECGPU_ERR_INVALID    -1   /* argument out of range / NULL / misaligned          */
+#define FECGPU_ERR_HIP        -2   /* a HIP runtime call failed: fecgpu_last_error()     */
+#define FECGPU_ERR_NO_DEVICE  -3   /* no gfx950 device visible                           */
+#define FECGPU_ERR_NOMEM      -4   /* workspace too small / allocation failed            */
+
+/* Per-block decode outcome written to status[b]. */
+#define FECGPU_BLOCK_RECOVERED 0   /* recovery ran (reference fec_recover returned 0 after
+                                      solving); recovered[] lists the inserted sources     */
+#define FECGPU_BLOCK_NOTHING   1   /* a precondition failed; nothing to recover          */
+#define FECGPU_BLOCK_REF_UB    2   /* erasure pattern on which the reference dereferences
+                                      x[-1] (rlc_fec_scheme_gf256.c:74-77) or a NULL repair
+                                      (xor_fec_scheme.c:50-51): no output, flagged          */
+
+#define FECGPU_MAX_K 128           /* presence masks are 2 x u64 per block               */
+#define FECGPU_MAX_R 128
+
+/* Engine version / device check.  Returns FECGPU_OK when a gfx950 device is usable. */
+int fecgpu_init(int device);
+const char *fecgpu_version(void);
+const char *fecgpu_last_error(void);
+
+/* RLC-GF(256) encode: rep[b][i] = sum_j coef(fbn_b, i)[j] * src[b][j] over GF(2^8)/0x11D. */
+int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
+                      void *stream);
+
+/* XOR encode (r == 1): rep[b][0] = XOR_j src[b][j]. */
+int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k,
+                      uint32_t symbol_size, void *stream);
+
+/* RLC decode.  Presence masks: bit j of src_present[2*b + j/64] set <=> source j of
+ * block b was received; same for rep_present.  Recovered sources are written IN PLACE
+ * into src[b][j]; bit j of recovered[2*b + j/64] is set for every source the reference
+ * would insert (determined and non-zero, rlc_fec_scheme_gf256.c:218-236).  Bytes of a
+ * missing slot whose bit stays clear are unspecified.  `workspace` must hold
+ * fecgpu_rlc_decode_workspace(nblocks, k, r) bytes of device memory. */
+size_t fecgpu_rlc_decode_workspace(uint64_t nblocks, uint32_t k, uint32_t r);
+int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
+                      const uint64_t *src_present, const uint64_t *rep_present,
+                      uint8_t *status, uint64_t *recovered, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
+/* XOR decode (r == 1), same conventions. */
+int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
+                      uint32_t symbol_size, const uint64_t *src_present,
+                      const uint64_t *rep_present, uint8_t *status, uint64_t *recovered,
+                      void *stream);
+
+/* Synthetic payload generator (bench/tests): byte o of dst = byte (o mod 8) of
+ * splitmix64(seed + (o/8 + 1) * 0x9e3779b97f4a7c15), o counted from `offset`. */
+int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream);
+
+/* Per-process counters, the analogue of the reference's per-pluglet count/time
+ * (picoquic/ubpf.c:302-319 under DEBUG_PLUGIN_EXECUTION_TIME). */
+typedef struct {
+    uint64_t encode_calls, encode_blocks;
+    uint64_t decode_calls, decode_blocks;
+} fecgpu_stats_t;
+void fecgpu_get_stats(fecgpu_stats_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,749 @@
+// pquic_amd/csrc/fec_engine.hip -- MI355X (gfx950) FEC engine: kernels + C ABI (include/fecgpu.h).
+//
+// Data path (HBM-bound byte arithmetic, no MFMA):
+//   k_rlc_encode   one wavefront per (FEC block, column chunk).  Lanes own 4-byte words
+//                  of the symbol row; every source word is loaded once (coalesced 256-B
+//                  rows per load instruction) and multiply-accumulated into R_TILE repair
+//                  accumulators held in VGPRs.  Coefficients come from TinyMT32 run in
+//                  lanes 0..R_TILE-1 (seed (fbn << 8) | i), their v_perm product tables
+//                  are staged in LDS and read as wave-uniform broadcasts.
+//   k_rlc_plan     one wavefront per block: replays the reference's fec_recover on the
+//                  coefficients only (repair selection, sort_system, elimination without
+//                  re-pivoting, back substitution) and emits the e x k matrix that maps the
+//                  k received symbols to the e unknowns, plus the dependency pattern used by
+//                  the data-dependent "all-zero unknown" rule.
+//   k_rlc_recover  same shape as encode: e outputs from k gathered inputs, in place.
+//   k_rlc_finalize per block: applies the reference's zero/undetermined propagation.
+//   k_xor_*        XOR scheme, streaming 16-B lanes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <atomic>
+
+#include "fec_device.h"
+#include "../../include/fecgpu.h"
+
+using namespace fecdev;
+
+#define FECGPU_VERSION "pquic_amd fecgpu 0.1 (gfx950, v_perm GF(256) data path)"
+
+static thread_local char g_err[256];
+static std::atomic<uint64_t> g_stats[4];
+
+static int set_err(int code, const char *fmt, const char *what) {
+  snprintf(g_err, sizeof g_err, fmt, what);
+  return code;
+}
+
+#define HIPCHK(call)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess) return set_err(FECGPU_ERR_HIP, "HIP: %s", hipGetErrorString(e_)); \
+  } while (0)
+
+// =============================================================================================
+// Workspace layout of the decode plan (bytes per block).
+// =============================================================================================
+struct WsLayout {
+  uint32_t em;      // e_max = min(k, r)
+  uint32_t off_unk, off_sel, off_slot, off_nz, off_D, off_dep, stride;
+};
+
+__host__ __device__ static inline uint32_t pad16(uint32_t x) { return (x + 15u) & ~15u; }
+
+__host__ __device__ static inline WsLayout ws_layout(uint32_t k, uint32_t r) {
+  WsLayout w;
+  w.em = k < r ? k : r;
+  uint32_t o = 16;  // header: status, e
+  w.off_unk = o;  o += pad16(w.em);
+  w.off_sel = o;  o += pad16(w.em);
+  w.off_slot = o; o += pad16(k);
+  w.off_nz = o;   o += pad16(w.em);
+  w.off_D = o;    o += pad16(w.em * k);
+  w.off_dep = o;  o += pad16(w.em * w.em);
+  w.stride = o;
+  return w;
+}
+
+__device__ __forceinline__ uint32_t block_fbn(uint64_t b, uint32_t fbn_base, const uint32_t *fbn) {
+  return fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
+}
+
+constexpr int KT = 16;  // sources per LDS table stage
+
+// LDS carve for the data kernels: coefficient bytes [RT][kpad] then tables [KT][RT].
+template <int RT>
+struct DataLds {
+  static __device__ __forceinline__ uint8_t *coef(uint8_t *lds) { return lds; }
+  static __device__ __forceinline__ uint4 *t01(uint8_t *lds, int kpad) {
+    return reinterpret_cast<uint4 *>(lds + pad16(RT * kpad));
+  }
+  static __device__ __forceinline__ uint32_t *t2(uint8_t *lds, int kpad) {
+    return reinterpret_cast<uint32_t *>(lds + pad16(RT * kpad) + KT * RT * 16);
+  }
+  static __host__ __device__ size_t bytes(int k) {
+    int kpad = (int)pad16((uint32_t)k);
+    return pad16(RT * kpad) + KT * RT * 20;
+  }
+};
+
+// Build perm tables for sources [jt, jt+KT) from the coefficient bytes in LDS.
+template <int RT>
+__device__ __forceinline__ void stage_tables(uint8_t *lds, int kpad, int k, int jt, int lane) {
+  uint8_t *coef = DataLds<RT>::coef(lds);
+  uint4 *t01 = DataLds<RT>::t01(lds, kpad);
+  uint32_t *t2 = DataLds<RT>::t2(lds, kpad);
+  for (int e = lane; e < KT * RT; e += 64) {
+    int jj = e / RT, i = e % RT;
+    int j = jt + jj;
+    uint32_t c = j < k ? coef[i * kpad + j] : 0u;
+    PermTab t = perm_table(c);
+    t01[e] = t.t01;
+    t2[e] = t.t2;
+  }
+}
+
+// The multiply-accumulate sweep shared by encode and recover: acc[i][w] += coef(i, j) * in_j.
+// in_ptr(j) returns the dword row of input j (already offset to this chunk).
+template <int RT, int W, typename InPtr>
+__device__ __forceinline__ void mac_sweep(uint8_t *lds, int kpad, int k, int rt, int cn, int lane,
+                                          InPtr in_ptr, uint32_t (&acc)[RT][W]) {
+  uint4 *t01 = DataLds<RT>::t01(lds, kpad);
+  uint32_t *t2 = DataLds<RT>::t2(lds, kpad);
+  uint32_t nxt[W];
+  {
+    const uint32_t *p = in_ptr(0);
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      int idx = lane + 64 * w;
+      nxt[w] = idx < cn ? __builtin_nontemporal_load(p + idx) : 0u;
+    }
+  }
+  for (int jt = 0; jt < k; jt += KT) {
+    __syncthreads();
+    stage_tables<RT>(lds, kpad, k, jt, lane);
+    __syncthreads();
+    int jn = k - jt < KT ? k - jt : KT;
+    for (int jj = 0; jj < jn; jj++) {
+      int j = jt + jj;
+      Sel sel[W];
+#pragma unroll
+      for (int w = 0; w < W; w++) sel[w] = perm_selectors(nxt[w]);
+      if (j + 1 < k) {
+        const uint32_t *p = in_ptr(j + 1);
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          int idx = lane + 64 * w;
+          nxt[w] = idx < cn ? __builtin_nontemporal_load(p + idx) : 0u;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RT; i++) {
+        if (i < rt) {
+          uint4 ta = t01[jj * RT + i];
+          uint32_t tb = t2[jj * RT + i];
+#pragma unroll
+          for (int w = 0; w < W; w++) acc[i][w] = gf_mac(acc[i][w], sel[w], ta, tb);
+        }
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// RLC encode
+// =============================================================================================
+template <int RT, int W>
+__global__ __launch_bounds__(64) void k_rlc_encode(const uint32_t *__restrict__ src,
+                                                   uint32_t *__restrict__ rep, uint64_t nblocks,
+                                                   int k, int r, int Ldw, int nchunks, int chunk_dw,
+                                                   uint32_t fbn_base, const uint32_t *fbn, int r0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const int kpad = (int)pad16((uint32_t)k);
+  const int rt = r - r0 < RT ? r - r0 : RT;
+  const uint64_t units = nblocks * (uint64_t)nchunks;
+  for (uint64_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const uint64_t b = unit / (uint64_t)nchunks;
+    const int ch = (int)(unit - b * (uint64_t)nchunks);
+    const uint32_t f = block_fbn(b, fbn_base, fbn);
+    __syncthreads();
+    if (lane < rt) {
+      Tmt t;
+      tmt_init(t, rlc_seed(f, (uint32_t)(r0 + lane)));
+      uint8_t *coef = DataLds<RT>::coef(lds) + lane * kpad;
+      for (int j = 0; j < k; j++) coef[j] = tmt_coef(t);
+    }
+    const int c0 = ch * chunk_dw;
+    const int cn = Ldw - c0 < chunk_dw ? Ldw - c0 : chunk_dw;
+    uint32_t acc[RT][W];
+#pragma unroll
+    for (int i = 0; i < RT; i++)
+#pragma unroll
+      for (int w = 0; w < W; w++) acc[i][w] = 0;
+    const uint32_t *sb = src + (b * (uint64_t)k) * (uint64_t)Ldw + c0;
+    auto in_ptr = [&](int j) { return sb + (uint64_t)j * Ldw; };
+    mac_sweep<RT, W>(lds, kpad, k, rt, cn, lane, in_ptr, acc);
+    uint32_t *rb = rep + (b * (uint64_t)r + r0) * (uint64_t)Ldw + c0;
+#pragma unroll
+    for (int i = 0; i < RT; i++) {
+      if (i < rt) {
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          int idx = lane + 64 * w;
+          if (idx < cn) __builtin_nontemporal_store(acc[i][w], rb + (uint64_t)i * Ldw + idx);
+        }
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// RLC decode: plan (coefficients only), recover (data), finalize (zero propagation)
+// =============================================================================================
+// One wave per block.  LDS: rows[em][kpad] (full coefficient rows of the selected repairs),
+// A[em][empad] (system over unknowns), V[em][kpad] (input combinations), X[em][kpad]
+// (solution), then unk[128], sel[128], perm[128] ints and a flag word.
+struct PlanLds {
+  uint8_t *rows, *A, *V, *X;
+  int *unk, *sel, *perm, *flag;
+};
+
+__host__ __device__ static inline size_t plan_lds_bytes(uint32_t k, uint32_t r) {
+  const WsLayout L = ws_layout(k, r);
+  const size_t kpad = pad16(k), empad = pad16(L.em);
+  return pad16((uint32_t)(L.em * kpad * 3 + L.em * empad)) + 4 * (128 * 3 + 4);
+}
+
+__device__ __forceinline__ PlanLds plan_carve(uint8_t *lds, int em, int kpad, int empad) {
+  PlanLds p;
+  p.rows = lds;
+  p.A = p.rows + em * kpad;
+  p.V = p.A + em * empad;
+  p.X = p.V + em * kpad;
+  int *ints = reinterpret_cast<int *>(lds + pad16((uint32_t)(em * kpad * 3 + em * empad)));
+  p.unk = ints;
+  p.sel = ints + 128;
+  p.perm = ints + 256;
+  p.flag = ints + 384;
+  return p;
+}
+
+__device__ __forceinline__ bool bit128(uint64_t m0, uint64_t m1, int j) {
+  return j < 64 ? ((m0 >> j) & 1) : ((m1 >> (j - 64)) & 1);
+}
+__device__ __forceinline__ int rank128(uint64_t m0, uint64_t m1, int j) {  // set bits below j
+  return j < 64 ? __popcll(m0 & ((1ull << j) - 1)) : __popcll(m0) + __popcll(m1 & ((1ull << (j - 64)) - 1));
+}
+__device__ __forceinline__ void clip128(uint64_t &m0, uint64_t &m1, int n) {
+  if (n < 64) { m0 &= (1ull << n) - 1; m1 = 0; }
+  else if (n < 128) m1 &= (1ull << (n - 64)) - 1;
+}
+
+__global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                 const uint32_t *fbn, const uint64_t *sp,
+                                                 const uint64_t *rp, uint8_t *ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  const int em = (int)L.em;
+  const int kpad = (int)pad16((uint32_t)k);
+  const int empad = (int)pad16((uint32_t)em);
+  const PlanLds P = plan_carve(lds, em, kpad, empad);
+  uint8_t *rows = P.rows, *A = P.A, *V = P.V, *X = P.X;
+  int *unk = P.unk, *sel = P.sel, *perm = P.perm;
+
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    uint8_t *h = ws + b * (uint64_t)L.stride;
+    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
+    clip128(s0, s1, k);
+    clip128(q0, q1, r);
+    const int cur_ss = __popcll(s0) + __popcll(s1);
+    const int cur_rs = __popcll(q0) + __popcll(q1);
+    __syncthreads();
+    // rlc_fec_scheme_gf256.c:140-144
+    if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {
+      if (lane == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
+      continue;
+    }
+    const int n = k - cur_ss;  // unknowns == equations (n_eq = min(n_unk, cur_rs) = n_unk)
+    uint64_t m0 = ~s0, m1 = ~s1;
+    clip128(m0, m1, k);
+    // unknown u -> u-th missing source; equation e -> e-th present repair (:194-212)
+    for (int j = lane; j < k; j += 64)
+      if (bit128(m0, m1, j)) unk[rank128(m0, m1, j)] = j;
+    for (int i = lane; i < r; i += 64)
+      if (bit128(q0, q1, i)) {
+        int e = rank128(q0, q1, i);
+        if (e < n) sel[e] = i;
+      }
+    __syncthreads();
+    const uint32_t f = block_fbn(b, fbn_base, fbn);
+    for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
+      Tmt t;
+      tmt_init(t, rlc_seed(f, (uint32_t)sel[e]));
+      for (int j = 0; j < k; j++) rows[e * kpad + j] = tmt_coef(t);
+    }
+    __syncthreads();
+    // A[e][u] = rows[e][unk[u]];  V[e][j] = present j ? rows[e][j] : (j == unk[e])
+    for (int e = 0; e < n; e++) {
+      for (int u = lane; u < n; u += 64) A[e * empad + u] = rows[e * kpad + unk[u]];
+      for (int j = lane; j < k; j += 64)
+        V[e * kpad + j] = bit128(m0, m1, j) ? (uint8_t)(unk[e] == j) : rows[e * kpad + j];
+    }
+    for (int i = lane; i < n; i += 64) perm[i] = i;
+    __syncthreads();
+    // sort_system (:28-40): position i takes the first row with the largest A[.][i]
+    if (lane == 0) {
+      for (int i = 0; i < n; i++) {
+        int mx = i;
+        for (int j = i + 1; j < n; j++)
+          if (A[perm[mx] * empad + i] < A[perm[j] * empad + i]) mx = j;
+        int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t;
+      }
+    }
+    __syncthreads();
+    // forward elimination without re-pivoting (:54-70); inv(0) = 0 makes term 0
+    for (int i = 0; i < n - 1; i++) {
+      const int pi = perm[i];
+      const uint32_t ipiv = gf_inv(A[pi * empad + i]);
+      for (int kk = i + 1; kk < n; kk++) {
+        const int pk = perm[kk];
+        const uint32_t term = gf_mul(A[pk * empad + i], ipiv);
+        __syncthreads();
+        if (term) {
+          for (int u = lane; u < n; u += 64) A[pk * empad + u] ^= (uint8_t)gf_mul(term, A[pi * empad + u]);
+          for (int j = lane; j < k; j += 64) V[pk * kpad + j] ^= (uint8_t)gf_mul(term, V[pi * kpad + j]);
+        }
+        __syncthreads();
+      }
+    }
+    // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
+    if (lane == 0) {
+      int ub = 0;
+      for (int i = 0; i < n; i++) ub |= A[perm[i] * empad + i] == 0;
+      *P.flag = ub;
+    }
+    __syncthreads();
+    if (*P.flag) {
+      if (lane == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
+      continue;
+    }
+    // back substitution (:71-114) on the input-combination vectors
+    for (int i = n - 1; i >= 0; i--) {
+      const int pi = perm[i];
+      const uint32_t ip = gf_inv(A[pi * empad + i]);
+      for (int j = lane; j < k; j += 64) {
+        uint32_t v = V[pi * kpad + j];
+        for (int u = i + 1; u < n; u++) {
+          uint32_t a = A[pi * empad + u];
+          if (a) v ^= gf_mul(a, X[u * kpad + j]);
+        }
+        X[i * kpad + j] = (uint8_t)gf_mul(v, ip);
+      }
+      for (int u = lane; u < n; u += 64) h[L.off_dep + i * em + u] = (u > i) && A[pi * empad + u] != 0;
+    }
+    for (int i = 0; i < n; i++)
+      for (int j = lane; j < k; j += 64) h[L.off_D + i * k + j] = X[i * kpad + j];
+    for (int u = lane; u < n; u += 64) {
+      h[L.off_nz + u] = 0;
+      h[L.off_unk + u] = (uint8_t)unk[u];
+      h[L.off_sel + u] = (uint8_t)sel[u];
+    }
+    // slot map: input j = source j if present, else the repair selected for its unknown
+    for (int j = lane; j < k; j += 64)
+      h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | sel[rank128(m0, m1, j)]) : (uint8_t)j;
+    if (lane == 0) { h[0] = FECGPU_BLOCK_RECOVERED; h[1] = (uint8_t)n; }
+  }
+}
+
+template <int RT, int W>
+__global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
+                                                    const uint32_t *__restrict__ rep, uint64_t nblocks,
+                                                    int k, int r, int Ldw, int nchunks, int chunk_dw,
+                                                    uint8_t *ws, int r0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  const int kpad = (int)pad16((uint32_t)k);
+  const uint64_t units = nblocks * (uint64_t)nchunks;
+  for (uint64_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const uint64_t b = unit / (uint64_t)nchunks;
+    const int ch = (int)(unit - b * (uint64_t)nchunks);
+    uint8_t *h = ws + b * (uint64_t)L.stride;
+    const int status = h[0], e = h[1];
+    if (status != FECGPU_BLOCK_RECOVERED || e <= r0) continue;  // uniform per wave
+    const int rt = e - r0 < RT ? e - r0 : RT;
+    __syncthreads();
+    for (int x = lane; x < RT * kpad; x += 64) {
+      int i = x / kpad, j = x - i * kpad;
+      DataLds<RT>::coef(lds)[x] = (i < rt && j < k) ? h[L.off_D + (r0 + i) * k + j] : 0;
+    }
+    const int c0 = ch * chunk_dw;
+    const int cn = Ldw - c0 < chunk_dw ? Ldw - c0 : chunk_dw;
+    uint32_t acc[RT][W];
+#pragma unroll
+    for (int i = 0; i < RT; i++)
+#pragma unroll
+      for (int w = 0; w < W; w++) acc[i][w] = 0;
+    const uint8_t *slot = h + L.off_slot;
+    auto in_ptr = [&](int j) {
+      uint32_t s = slot[j];
+      const uint32_t *base = (s & 0x80) ? rep + (b * (uint64_t)r + (s & 0x7f)) * (uint64_t)Ldw
+                                        : src + (b * (uint64_t)k + s) * (uint64_t)Ldw;
+      return base + c0;
+    };
+    mac_sweep<RT, W>(lds, kpad, k, rt, cn, lane, in_ptr, acc);
+#pragma unroll
+    for (int i = 0; i < RT; i++) {
+      if (i < rt) {
+        uint32_t *ob = src + (b * (uint64_t)k + h[L.off_unk + r0 + i]) * (uint64_t)Ldw + c0;
+        uint32_t any = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          int idx = lane + 64 * w;
+          if (idx < cn) { ob[idx] = acc[i][w]; any |= acc[i][w]; }
+        }
+        if (__any(any != 0) && lane == 0) h[L.off_nz + r0 + i] = 1;  // idempotent across chunks
+      }
+    }
+  }
+}
+
+__global__ void k_rlc_finalize(uint64_t nblocks, int k, int r, const uint8_t *ws, uint8_t *status,
+                               uint64_t *recovered) {
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nblocks;
+       b += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t *h = ws + b * (uint64_t)L.stride;
+    uint64_t m0 = 0, m1 = 0;
+    const int st = h[0];
+    if (st == FECGPU_BLOCK_RECOVERED) {
+      const int n = h[1];
+      uint64_t det0 = 0, det1 = 0;  // determined unknowns, indexed by u
+      for (int u = n - 1; u >= 0; u--) {
+        bool ok = h[L.off_nz + u] != 0;  // symbol_is_zero -> undetermined (:98-101)
+        for (int v = u + 1; v < n && ok; v++)
+          if (h[L.off_dep + u * L.em + v]) ok = v < 64 ? ((det0 >> v) & 1) : ((det1 >> (v - 64)) & 1);
+        if (ok) {
+          if (u < 64) det0 |= 1ull << u; else det1 |= 1ull << (u - 64);
+          int j = h[L.off_unk + u];
+          if (j < 64) m0 |= 1ull << j; else m1 |= 1ull << (j - 64);
+        }
+      }
+    }
+    status[b] = (uint8_t)st;
+    recovered[2 * b] = m0;
+    recovered[2 * b + 1] = m1;
+  }
+}
+
+// =============================================================================================
+// XOR scheme
+// =============================================================================================
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ V vxor(V a, V b) { return a ^ b; }
+
+template <typename V>
+__global__ __launch_bounds__(256) void k_xor_encode(const V *__restrict__ src, V *__restrict__ rep,
+                                                    uint64_t nblocks, int k, int Lv) {
+  const uint64_t total = nblocks * (uint64_t)Lv;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = t / (uint64_t)Lv, c = t - b * (uint64_t)Lv;
+    const V *p = src + b * (uint64_t)k * Lv + c;
+    V a = __builtin_nontemporal_load(p);
+    for (int j = 1; j < k; j++) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
+    __builtin_nontemporal_store(a, rep + b * (uint64_t)Lv + c);
+  }
+}
+
+// xor_fec_scheme.c:41-74.  status: RECOVERED when exactly the preconditions hold and the
+// repair is present; REF_UB when they hold with the repair absent (NULL dereference).
+template <typename V>
+__global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V *__restrict__ rep,
+                                                    uint64_t nblocks, int k, int Lv,
+                                                    const uint64_t *sp, const uint64_t *rp,
+                                                    uint8_t *status, uint64_t *recovered) {
+  const uint64_t total = nblocks * (uint64_t)Lv;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = t / (uint64_t)Lv, c = t - b * (uint64_t)Lv;
+    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1];
+    if (k < 64) { s0 &= (1ull << k) - 1; s1 = 0; } else if (k < 128) s1 &= (1ull << (k - 64)) - 1;
+    const int cur_ss = __popcll(s0) + __popcll(s1);
+    const int cur_rs = (int)(rp[2 * b] & 1);
+    int st = FECGPU_BLOCK_NOTHING, miss = -1;
+    if (cur_ss + cur_rs == k) {
+      if (!cur_rs) st = FECGPU_BLOCK_REF_UB;
+      else {
+        st = FECGPU_BLOCK_RECOVERED;
+        uint64_t m0 = ~s0, m1 = ~s1;
+        if (k < 64) { m0 &= (1ull << k) - 1; m1 = 0; } else if (k < 128) m1 &= (1ull << (k - 64)) - 1;
+        miss = m1 ? 127 - __clzll(m1) : 63 - __clzll(m0);  // LAST missing index (:54-58)
+      }
+    }
+    if (st == FECGPU_BLOCK_RECOVERED) {
+      V a = rep[b * (uint64_t)Lv + c];
+      const V *p = src + b * (uint64_t)k * Lv + c;
+      for (int j = 0; j < k; j++)
+        if (j != miss) a = vxor(a, p[(uint64_t)j * Lv]);
+      src[(b * (uint64_t)k + miss) * Lv + c] = a;
+    }
+    if (c == 0) {
+      status[b] = (uint8_t)st;
+      recovered[2 * b] = (st == FECGPU_BLOCK_RECOVERED && miss < 64) ? 1ull << miss : 0;
+      recovered[2 * b + 1] = (st == FECGPU_BLOCK_RECOVERED && miss >= 64) ? 1ull << (miss - 64) : 0;
+    }
+  }
+}
+
+__global__ void k_synth_fill(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t offset) {
+  // one 8-byte word of the stream per thread; unaligned head/tail handled bytewise
+  const uint64_t first = offset >> 3, last = (offset + nbytes + 7) >> 3;
+  for (uint64_t w = first + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < last;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (w + 1) * 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z ^= z >> 31;
+    const uint64_t o0 = w << 3;
+    if (o0 >= offset && o0 + 8 <= offset + nbytes && ((o0 - offset) & 7) == 0 &&
+        (((uintptr_t)(dst + (o0 - offset))) & 7) == 0) {
+      *reinterpret_cast<uint64_t *>(dst + (o0 - offset)) = z;
+    } else {
+      for (int i = 0; i < 8; i++) {
+        uint64_t o = o0 + i;
+        if (o >= offset && o < offset + nbytes) dst[o - offset] = (uint8_t)(z >> (8 * i));
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// Launch configuration
+// =============================================================================================
+struct DataCfg { int W, nchunks, chunk_dw; };
+
+// Choose lane words W (1..8) and the column chunking that wastes the fewest lane slots.
+static DataCfg pick_data_cfg(int Ldw) {
+  DataCfg best{1, 1, 64};
+  double best_eff = -1;
+  for (int W = 8; W >= 1; W--) {
+    int nch = (Ldw + 64 * W - 1) / (64 * W);
+    int chunk = (Ldw + nch - 1) / nch;
+    int wneed = (chunk + 63) / 64;
+    double eff = (double)Ldw / ((double)nch * 64.0 * wneed);
+    // prefer fewer chunks (fewer coefficient regenerations) at equal efficiency
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = DataCfg{wneed, nch, chunk}; }
+  }
+  return best;
+}
+
+static int pick_rt(uint32_t r) { return r >= 16 ? 16 : r >= 8 ? 8 : r >= 4 ? 4 : r >= 2 ? 2 : 1; }
+
+static uint32_t grid_for(uint64_t units) {
+  const uint64_t cap = 1u << 22;
+  return (uint32_t)(units < cap ? (units ? units : 1) : cap);
+}
+
+template <int RT, int W>
+static void launch_encode(const uint32_t *src, uint32_t *rep, uint64_t nb, int k, int r, int Ldw,
+                          const DataCfg &c, uint32_t fbn_base, const uint32_t *fbn, int r0,
+                          hipStream_t s) {
+  size_t lds = DataLds<RT>::bytes(k);
+  hipLaunchKernelGGL((k_rlc_encode<RT, W>), dim3(grid_for(nb * c.nchunks)), dim3(64), lds, s, src, rep,
+                     nb, k, r, Ldw, c.nchunks, c.chunk_dw, fbn_base, fbn, r0);
+}
+
+template <int RT, int W>
+static void launch_recover(uint32_t *src, const uint32_t *rep, uint64_t nb, int k, int r, int Ldw,
+                           const DataCfg &c, uint8_t *ws, int r0, hipStream_t s) {
+  size_t lds = DataLds<RT>::bytes(k);
+  hipLaunchKernelGGL((k_rlc_recover<RT, W>), dim3(grid_for(nb * c.nchunks)), dim3(64), lds, s, src,
+                     rep, nb, k, r, Ldw, c.nchunks, c.chunk_dw, ws, r0);
+}
+
+#define FEC_DISPATCH_W(FN, RT, ...)                       \
+  switch (cfg.W) {                                        \
+    case 1: FN<RT, 1>(__VA_ARGS__); break;                \
+    case 2: FN<RT, 2>(__VA_ARGS__); break;                \
+    case 3: FN<RT, 3>(__VA_ARGS__); break;                \
+    case 4: FN<RT, 4>(__VA_ARGS__); break;                \
+    case 5: FN<RT, 5>(__VA_ARGS__); break;                \
+    case 6: FN<RT, 6>(__VA_ARGS__); break;                \
+    case 7: FN<RT, 7>(__VA_ARGS__); break;                \
+    default: FN<RT, 8>(__VA_ARGS__); break;               \
+  }
+
+#define FEC_DISPATCH_RT(FN, ...)                          \
+  switch (rt) {                                           \
+    case 1: FEC_DISPATCH_W(FN, 1, __VA_ARGS__) break;     \
+    case 2: FEC_DISPATCH_W(FN, 2, __VA_ARGS__) break;     \
+    case 4: FEC_DISPATCH_W(FN, 4, __VA_ARGS__) break;     \
+    case 8: FEC_DISPATCH_W(FN, 8, __VA_ARGS__) break;     \
+    default: FEC_DISPATCH_W(FN, 16, __VA_ARGS__) break;   \
+  }
+
+static int check_common(const void *a, const void *b, uint64_t nblocks, uint32_t k, uint32_t r,
+                        uint32_t L) {
+  if (nblocks == 0) return FECGPU_OK;
+  if (!a || !b) return set_err(FECGPU_ERR_INVALID, "%s", "NULL symbol buffer");
+  if (k < 1 || k > FECGPU_MAX_K) return set_err(FECGPU_ERR_INVALID, "%s", "k out of range [1,128]");
+  if (r > FECGPU_MAX_R) return set_err(FECGPU_ERR_INVALID, "%s", "r out of range [0,128]");
+  if (L == 0 || (L & 3) || L > 65532) return set_err(FECGPU_ERR_INVALID, "%s", "symbol_size must be a positive multiple of 4 (<= 65532)");
+  if (((uintptr_t)a & 3) || ((uintptr_t)b & 3)) return set_err(FECGPU_ERR_INVALID, "%s", "buffers must be 4-byte aligned");
+  return FECGPU_OK;
+}
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+const char *fecgpu_version(void) { return FECGPU_VERSION; }
+const char *fecgpu_last_error(void) { return g_err; }
+
+int fecgpu_init(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device)
+    return set_err(FECGPU_ERR_NO_DEVICE, "%s", "no HIP device");
+  hipDeviceProp_t p;
+  HIPCHK(hipGetDeviceProperties(&p, device));
+  if (strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    return set_err(FECGPU_ERR_NO_DEVICE, "device is %s, engine is built for gfx950", p.gcnArchName);
+  return FECGPU_OK;
+}
+
+void fecgpu_get_stats(fecgpu_stats_t *out) {
+  out->encode_calls = g_stats[0].load();
+  out->encode_blocks = g_stats[1].load();
+  out->decode_calls = g_stats[2].load();
+  out->decode_blocks = g_stats[3].load();
+}
+
+int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn, void *stream) {
+  int rc = check_common(src, rep, nblocks, k, r, symbol_size);
+  if (rc || nblocks == 0 || r == 0) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int Ldw = (int)(symbol_size / 4);
+  const DataCfg cfg = pick_data_cfg(Ldw);
+  const int rt = pick_rt(r);
+  for (int r0 = 0; r0 < (int)r; r0 += rt) {
+    FEC_DISPATCH_RT(launch_encode, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
+                    cfg, fbn_base, fbn, r0, s)
+  }
+  HIPCHK(hipGetLastError());
+  g_stats[0]++;
+  g_stats[1] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,
+                      void *stream) {
+  int rc = check_common(src, rep, nblocks, k, 1, symbol_size);
+  if (rc || nblocks == 0) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0;
+  const int Lv = (int)(v4 ? symbol_size / 16 : symbol_size / 4);
+  const uint64_t total = nblocks * (uint64_t)Lv;
+  const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
+  if (v4)
+    hipLaunchKernelGGL(k_xor_encode<u32x4>, dim3(grid), dim3(256), 0, s, (const u32x4 *)src, (u32x4 *)rep,
+                       nblocks, (int)k, Lv);
+  else
+    hipLaunchKernelGGL(k_xor_encode<uint32_t>, dim3(grid), dim3(256), 0, s, (const uint32_t *)src,
+                       (uint32_t *)rep, nblocks, (int)k, Lv);
+  HIPCHK(hipGetLastError());
+  g_stats[0]++;
+  g_stats[1] += nblocks;
+  return FECGPU_OK;
+}
+
+size_t fecgpu_rlc_decode_workspace(uint64_t nblocks, uint32_t k, uint32_t r) {
+  return (size_t)nblocks * ws_layout(k, r).stride;
+}
+
+int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
+                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                      uint64_t *recovered, void *workspace, size_t workspace_bytes, void *stream) {
+  int rc = check_common(src, rep, nblocks, k, r, symbol_size);
+  if (rc || nblocks == 0) return rc;
+  if (!src_present || !rep_present || !status || !recovered || !workspace)
+    return set_err(FECGPU_ERR_INVALID, "%s", "NULL mask/status/workspace");
+  if (workspace_bytes < fecgpu_rlc_decode_workspace(nblocks, k, r))
+    return set_err(FECGPU_ERR_NOMEM, "%s", "decode workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t *ws = (uint8_t *)workspace;
+  const WsLayout L = ws_layout(k, r);
+  const size_t plan_lds = plan_lds_bytes(k, r);
+  if (plan_lds > 65536) {
+    static bool raised = false;
+    if (!raised) {
+      HIPCHK(hipFuncSetAttribute((const void *)k_rlc_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plan_lds));
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
+                     fbn_base, fbn, src_present, rep_present, ws);
+  HIPCHK(hipGetLastError());
+  if (r > 0) {
+    const int Ldw = (int)(symbol_size / 4);
+    const DataCfg cfg = pick_data_cfg(Ldw);
+    const int rt = pick_rt(L.em);
+    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+      FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
+                      cfg, ws, r0, s)
+    }
+    HIPCHK(hipGetLastError());
+  }
+  const uint32_t fgrid = (uint32_t)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
+  hipLaunchKernelGGL(k_rlc_finalize, dim3(fgrid), dim3(256), 0, s, nblocks, (int)k, (int)r, ws, status,
+                     recovered);
+  HIPCHK(hipGetLastError());
+  g_stats[2]++;
+  g_stats[3] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,
+                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                      uint64_t *recovered, void *stream) {
+  int rc = check_common(src, rep, nblocks, k, 1, symbol_size);
+  if (rc || nblocks == 0) return rc;
+  if (!src_present || !rep_present || !status || !recovered)
+    return set_err(FECGPU_ERR_INVALID, "%s", "NULL mask/status");
+  hipStream_t s = (hipStream_t)stream;
+  const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0;
+  const int Lv = (int)(v4 ? symbol_size / 16 : symbol_size / 4);
+  const uint64_t total = nblocks * (uint64_t)Lv;
+  const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
+  if (v4)
+    hipLaunchKernelGGL(k_xor_decode<u32x4>, dim3(grid), dim3(256), 0, s, (u32x4 *)src, (const u32x4 *)rep,
+                       nblocks, (int)k, Lv, src_present, rep_present, status, recovered);
+  else
+    hipLaunchKernelGGL(k_xor_decode<uint32_t>, dim3(grid), dim3(256), 0, s, (uint32_t *)src,
+                       (const uint32_t *)rep, nblocks, (int)k, Lv, src_present, rep_present, status,
+                       recovered);
+  HIPCHK(hipGetLastError());
+  g_stats[2]++;
+  g_stats[3] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream) {
+  if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL dst");
+  if (!nbytes) return FECGPU_OK;
+  const uint64_t words = ((offset + nbytes + 7) >> 3) - (offset >> 3) + 1;
+  const uint32_t grid = (uint32_t)((words + 255) / 256 < (1u << 20) ? (words + 255) / 256 : (1u << 20));
+  hipLaunchKernelGGL(k_synth_fill, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint8_t *)dst, nbytes,
+                     seed, offset);
+  HIPCHK(hipGetLastError());
+  return FECGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+"""ctypes mirror of include/fecgpu.h (batched device-resident FEC engine).
+
+Buffers are torch CUDA tensors (HBM allocations) or raw device addresses; kernels run on
+the given HIP stream (default: torch's current stream), so torch.cuda.Event timing
+brackets exactly the engine's launches.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "lib", "libpquic_fec.so")
+
+OK, ERR_INVALID, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
+BLOCK_RECOVERED, BLOCK_NOTHING, BLOCK_REF_UB = 0, 1, 2
+
+_lib = None
+
+
+class FecGpuError(RuntimeError):
+    pass
+
+
+class FecGpuStats(C.Structure):
+    _fields_ = [("encode_calls", C.c_uint64), ("encode_blocks", C.c_uint64),
+                ("decode_calls", C.c_uint64), ("decode_blocks", C.c_uint64)]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libpquic_fec.so.  Raises if it is missing -- never falls back to CPU."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FecGpuError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(path)
+    v, u64, u32, sz = C.c_void_p, C.c_uint64, C.c_uint32, C.c_size_t
+    L.fecgpu_init.argtypes = [C.c_int]
+    L.fecgpu_version.restype = C.c_char_p
+    L.fecgpu_last_error.restype = C.c_char_p
+    L.fecgpu_rlc_encode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v]
+    L.fecgpu_xor_encode.argtypes = [v, v, u64, u32, u32, v]
+    L.fecgpu_rlc_decode_workspace.argtypes = [u64, u32, u32]
+    L.fecgpu_rlc_decode_workspace.restype = sz
+    L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
+    L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
+    L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
+    L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
+    _lib = L
+    return L
+
+
+def _addr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+class Engine:
+    """Batched FEC engine on one device.  Mirrors fecgpu_* one to one."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        self.torch = torch
+        self.lib = load_library()
+        self.device = device
+        rc = self.lib.fecgpu_init(device)
+        if rc != OK:
+            raise FecGpuError(f"fecgpu_init({device}) = {rc}: {self.err()}")
+
+    # ------------------------------------------------------------------ helpers
+    def err(self) -> str:
+        return self.lib.fecgpu_last_error().decode()
+
+    def version(self) -> str:
+        return self.lib.fecgpu_version().decode()
+
+    def _stream(self, stream):
+        if stream is None:
+            stream = self.torch.cuda.current_stream(self.device)
+        return C.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+    def _check(self, rc, what):
+        if rc != OK:
+            raise FecGpuError(f"{what} failed ({rc}): {self.err()}")
+
+    def stats(self) -> dict:
+        s = FecGpuStats()
+        self.lib.fecgpu_get_stats(C.byref(s))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    # ------------------------------------------------------------------ encode
+    def rlc_encode(self, src, rep, k: int, r: int, L: int, nblocks: int | None = None,
+                   fbn_base: int = 0, fbn=None, stream=None):
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        self._check(self.lib.fecgpu_rlc_encode(_addr(src), _addr(rep), nb, k, r, L, fbn_base,
+                                               _addr(fbn), self._stream(stream)), "fecgpu_rlc_encode")
+        return rep
+
+    def xor_encode(self, src, rep, k: int, L: int, nblocks: int | None = None, stream=None):
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        self._check(self.lib.fecgpu_xor_encode(_addr(src), _addr(rep), nb, k, L, self._stream(stream)),
+                    "fecgpu_xor_encode")
+        return rep
+
+    # ------------------------------------------------------------------ decode
+    def decode_workspace_bytes(self, nblocks: int, k: int, r: int) -> int:
+        return int(self.lib.fecgpu_rlc_decode_workspace(nblocks, k, r))
+
+    def alloc_workspace(self, nblocks: int, k: int, r: int):
+        n = self.decode_workspace_bytes(nblocks, k, r)
+        return self.torch.empty(max(n, 16), dtype=self.torch.uint8, device=f"cuda:{self.device}")
+
+    def rlc_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, r: int,
+                   L: int, nblocks: int | None = None, fbn_base: int = 0, fbn=None,
+                   workspace=None, stream=None):
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        if workspace is None:
+            workspace = self.alloc_workspace(nb, k, r)
+        self._check(self.lib.fecgpu_rlc_decode(
+            _addr(src), _addr(rep), nb, k, r, L, fbn_base, _addr(fbn), _addr(src_present),
+            _addr(rep_present), _addr(status), _addr(recovered), _addr(workspace),
+            workspace.numel(), self._stream(stream)), "fecgpu_rlc_decode")
+        return status, recovered
+
+    def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,
+                   nblocks: int | None = None, stream=None):
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        self._check(self.lib.fecgpu_xor_decode(_addr(src), _addr(rep), nb, k, L, _addr(src_present),
+                                               _addr(rep_present), _addr(status), _addr(recovered),
+                                               self._stream(stream)), "fecgpu_xor_decode")
+        return status, recovered
+
+    def synth_fill(self, dst, nbytes: int, seed: int, offset: int = 0, stream=None):
+        self._check(self.lib.fecgpu_synth_fill(_addr(dst), nbytes, seed, offset, self._stream(stream)),
+                    "fecgpu_synth_fill")
+        return dst
