@@ -79,7 +79,7 @@ def cpu_baseline(args, nthreads):
     o = Oracle()
     k, r, L, e = args.k, args.r, args.symbol, args.erasures
 
-    def run(nb):
+    def make(nb):
         src = synth_bytes(nb * k * L, 0x5EEDF3C0).reshape(nb, k, L)
         rng = np.random.default_rng(1)
         sp = np.zeros((nb, 2), np.uint64)
@@ -91,19 +91,35 @@ def cpu_baseline(args, nthreads):
                 m &= ~(1 << int(j))
             sp[b, 0] = m
             rp[b, 0] = (1 << r) - 1
+        return src, sp, rp
+
+    def run(src, sp, rp):
+        work = src.copy()
         t0 = time.perf_counter()
-        rep = o.rlc_encode_batch(src, r, 0, nthreads)
-        o.rlc_decode_batch(src, rep, sp, rp, 0, nthreads)
+        rep = o.rlc_encode_batch(work, r, 0, nthreads)
+        o.rlc_decode_batch(work, rep, sp, rp, 0, nthreads)
         return time.perf_counter() - t0
 
-    nb = 2048
-    t = run(nb)
-    nb2 = int(min(max(nb * args.cpu_seconds / max(t, 1e-3), nb), 1 << 17))
-    t2 = run(nb2)
-    gib = nb2 * k * L / 2**30
-    return {"value": gib / t2, "unit": "GiB/s", "cores": nthreads, "kind": "port",
-            "sample": f"{nb2} blocks k={k} r={r} L={L}: RLC encode + decode with {e} erasures, "
-                      f"oracle/fec_oracle.c -O2, {nthreads} pthreads, {t2:.1f} s"}
+    # bounded sample: 2^14 blocks (300 MiB of payload), re-run until ~cpu_seconds of CPU work
+    nb = 1 << 14
+    src, sp, rp = make(nb)
+    passes, t_total = 0, 0.0
+    while t_total < args.cpu_seconds and passes < 1000:
+        t_total += run(src, sp, rp)
+        passes += 1
+    gib = passes * nb * k * L / 2**30
+    out = {"value": gib / t_total, "unit": "GiB/s", "cores": nthreads, "kind": "port",
+           "sample": f"{passes} passes x {nb} blocks, k={k} r={r} L={L}: RLC encode + decode with {e} "
+                     f"erasures, oracle/fec_oracle.c -O2, {nthreads} pthreads, {t_total:.1f} s"}
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
+    if os.path.exists(ref_path):  # the reference's own encode pluglet, 1 core (calibration)
+        from oracle_py import Reference
+        R = Reference(ref_path)
+        s1 = src[:1024].copy()
+        t0 = time.perf_counter()
+        R.rlc_encode_batch(s1, r, 0)
+        out["reference_encode_1core_GiB_s"] = round(1024 * k * L / 2**30 / (time.perf_counter() - t0), 4)
+    return out
 
 
 def main():

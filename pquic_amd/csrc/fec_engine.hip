@@ -358,6 +358,156 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lane-per-block plan (small systems): one lane replays fec_recover's coefficient work for one
+// block.  GF(2^8) products through log/exp tables in LDS; each lane's working set (A: em x em,
+// V: em x k, lists) lives in LDS byte-interleaved across the wave (element e of lane l at
+// e * 64 + l), so a wave-uniform step touches 64 consecutive bytes.
+// ---------------------------------------------------------------------------------------------
+struct GfLogExp { uint8_t exp[512]; uint8_t log[256]; };
+
+constexpr GfLogExp make_logexp() {
+  GfLogExp t{};
+  uint32_t x = 1;
+  for (int i = 0; i < 255; i++) {
+    t.exp[i] = (uint8_t)x;
+    t.exp[i + 255] = (uint8_t)x;
+    t.log[x] = (uint8_t)i;
+    x = ((x << 1) ^ ((x & 0x80u) ? 0x11du : 0u)) & 0xffu;
+  }
+  t.exp[510] = t.exp[0];
+  t.exp[511] = t.exp[1];
+  t.log[0] = 0;
+  return t;
+}
+
+__constant__ GfLogExp kLogExp = make_logexp();
+
+__host__ __device__ static inline uint32_t lane_arena_bytes(uint32_t k, uint32_t r) {
+  const uint32_t em = k < r ? k : r;
+  return em * em + em * k + 3 * em;
+}
+
+__global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                      const uint32_t *fbn, const uint64_t *sp,
+                                                      const uint64_t *rp, uint8_t *ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  const int em = (int)L.em;
+  uint8_t *EXP = lds, *LOG = lds + 512;
+  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  __syncthreads();
+  uint8_t *my = lds + 768 + lane;
+  const int oA = 0, oV = em * em, oP = oV + em * k, oU = oP + em, oS = oU + em;
+#define AR(e) my[(e) * 64]
+  for (uint64_t base = (uint64_t)blockIdx.x * 64; base < nblocks; base += (uint64_t)gridDim.x * 64) {
+    const uint64_t b = base + lane;
+    if (b >= nblocks) continue;
+    uint8_t *h = ws + b * (uint64_t)L.stride;
+    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
+    clip128(s0, s1, k);
+    clip128(q0, q1, r);
+    const int cur_ss = __popcll(s0) + __popcll(s1);
+    const int cur_rs = __popcll(q0) + __popcll(q1);
+    if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
+      h[0] = FECGPU_BLOCK_NOTHING;
+      h[1] = 0;
+      continue;
+    }
+    const int n = k - cur_ss;
+    uint64_t m0 = ~s0, m1 = ~s1;
+    clip128(m0, m1, k);
+    {
+      int u = 0;
+      for (int j = 0; j < k; j++)
+        if (bit128(m0, m1, j)) AR(oU + u++) = (uint8_t)j;
+      int e = 0;
+      for (int i = 0; i < r && e < n; i++)
+        if (bit128(q0, q1, i)) AR(oS + e++) = (uint8_t)i;
+    }
+    const uint32_t f = block_fbn(b, fbn_base, fbn);
+    for (int e = 0; e < n; e++) {  // system rows, :194-212
+      Tmt t;
+      tmt_init(t, rlc_seed(f, AR(oS + e)));
+      int u = 0;
+      for (int j = 0; j < k; j++) {
+        uint8_t c = tmt_coef(t);
+        if (bit128(m0, m1, j)) {
+          AR(oA + e * em + u) = c;
+          AR(oV + e * k + j) = (uint8_t)(u == e);
+          u++;
+        } else {
+          AR(oV + e * k + j) = c;
+        }
+      }
+      AR(oP + e) = (uint8_t)e;
+    }
+    for (int i = 0; i < n; i++) {  // sort_system :28-40
+      int mx = i;
+      for (int j = i + 1; j < n; j++)
+        if (AR(oA + AR(oP + mx) * em + i) < AR(oA + AR(oP + j) * em + i)) mx = j;
+      uint8_t t = AR(oP + i); AR(oP + i) = AR(oP + mx); AR(oP + mx) = t;
+    }
+    for (int i = 0; i < n - 1; i++) {  // elimination :54-70
+      const int pi = AR(oP + i);
+      const uint32_t piv = AR(oA + pi * em + i);
+      if (!piv) continue;  // inv(0) = 0: every term is 0, nothing changes
+      const uint32_t lip = 255u - LOG[piv];
+      for (int kk = i + 1; kk < n; kk++) {
+        const int pk = AR(oP + kk);
+        const uint32_t a = AR(oA + pk * em + i);
+        if (!a) continue;
+        const uint32_t lt = LOG[EXP[LOG[a] + lip]];
+        for (int u = 0; u < n; u++) {
+          uint32_t x = AR(oA + pi * em + u);
+          if (x) AR(oA + pk * em + u) ^= EXP[lt + LOG[x]];
+        }
+        for (int j = 0; j < k; j++) {
+          uint32_t x = AR(oV + pi * k + j);
+          if (x) AR(oV + pk * k + j) ^= EXP[lt + LOG[x]];
+        }
+      }
+    }
+    bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
+    for (int i = 0; i < n; i++) ub |= AR(oA + AR(oP + i) * em + i) == 0;
+    if (ub) {
+      h[0] = FECGPU_BLOCK_REF_UB;
+      h[1] = 0;
+      continue;
+    }
+    for (int i = n - 1; i >= 0; i--) {  // back substitution :71-114; X_i stored over V[P[i]]
+      const int pi = AR(oP + i);
+      const uint32_t li = 255u - LOG[AR(oA + pi * em + i)];
+      for (int j = 0; j < k; j++) {
+        uint32_t v = AR(oV + pi * k + j);
+        for (int u = i + 1; u < n; u++) {
+          uint32_t a = AR(oA + pi * em + u);
+          uint32_t x = AR(oV + AR(oP + u) * k + j);
+          if (a && x) v ^= EXP[LOG[a] + LOG[x]];
+        }
+        AR(oV + pi * k + j) = v ? EXP[LOG[v] + li] : 0;
+      }
+      for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && AR(oA + pi * em + u) != 0;
+    }
+    for (int i = 0; i < n; i++) {
+      const int pi = AR(oP + i);
+      for (int j = 0; j < k; j++) h[L.off_D + i * k + j] = AR(oV + pi * k + j);
+      h[L.off_nz + i] = 0;
+      h[L.off_unk + i] = AR(oU + i);
+      h[L.off_sel + i] = AR(oS + i);
+    }
+    {
+      int u = 0;
+      for (int j = 0; j < k; j++)
+        h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | AR(oS + u++)) : (uint8_t)j;
+    }
+    h[0] = FECGPU_BLOCK_RECOVERED;
+    h[1] = (uint8_t)n;
+  }
+#undef AR
+}
+
 template <int RT, int W>
 __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
                                                     const uint32_t *__restrict__ rep, uint64_t nblocks,
@@ -680,16 +830,23 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const WsLayout L = ws_layout(k, r);
-  const size_t plan_lds = plan_lds_bytes(k, r);
-  if (plan_lds > 65536) {
-    static bool raised = false;
-    if (!raised) {
-      HIPCHK(hipFuncSetAttribute((const void *)k_rlc_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plan_lds));
-      raised = true;
+  const size_t lane_lds = 768 + 64 * (size_t)lane_arena_bytes(k, r);
+  if (lane_lds <= 48 * 1024) {
+    const uint64_t groups = (nblocks + 63) / 64;
+    hipLaunchKernelGGL(k_rlc_plan_lane, dim3(grid_for(groups)), dim3(64), lane_lds, s, nblocks, (int)k,
+                       (int)r, fbn_base, fbn, src_present, rep_present, ws);
+  } else {
+    const size_t plan_lds = plan_lds_bytes(k, r);
+    if (plan_lds > 65536) {
+      static bool raised = false;
+      if (!raised) {
+        HIPCHK(hipFuncSetAttribute((const void *)k_rlc_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plan_lds));
+        raised = true;
+      }
     }
+    hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
+                       fbn_base, fbn, src_present, rep_present, ws);
   }
-  hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
-                     fbn_base, fbn, src_present, rep_present, ws);
   HIPCHK(hipGetLastError());
   if (r > 0) {
     const int Ldw = (int)(symbol_size / 4);
