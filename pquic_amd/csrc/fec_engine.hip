@@ -20,8 +20,10 @@
 #include <stdio.h>
 #include <string.h>
 #include <atomic>
+#include <stdlib.h>
 
 #include "fec_device.h"
+#include "bitslice_gen.h"
 #include "../../include/fecgpu.h"
 
 using namespace fecdev;
@@ -69,6 +71,8 @@ __host__ __device__ static inline WsLayout ws_layout(uint32_t k, uint32_t r) {
 __device__ __forceinline__ uint32_t block_fbn(uint64_t b, uint32_t fbn_base, const uint32_t *fbn) {
   return fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
 }
+
+static uint32_t grid_for(uint64_t units);
 
 constexpr int KT = 16;  // sources per LDS table stage
 
@@ -590,6 +594,240 @@ __global__ void k_rlc_finalize(uint64_t nblocks, int k, int r, const uint8_t *ws
 }
 
 // =============================================================================================
+// Bitsliced data path (default): one wave per (block, column chunk of <= 2 KiB); each lane owns
+// 32 bytes of the chunk as NP = 32 / VEC pieces (piece p of the chunk at byte VEC * p; lane l
+// holds pieces l, l + A, ..., A = active lanes).  The multiply-accumulate runs in the generated
+// inline-assembly bodies of bitslice_gen.h; this wrapper stages coefficients and addresses in LDS.
+// =============================================================================================
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+struct BsCfg { int vec, nchunks, chunk_bytes; };
+
+template <int VEC>
+struct BsLanes {
+  static constexpr int NP = 32 / VEC;
+  uint32_t off[NP];
+  uint64_t vm[NP];
+  int active;
+  __device__ __forceinline__ BsLanes(int lane, int cb) {
+    const int npieces = cb / VEC;
+    active = (npieces + NP - 1) / NP;
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+      const int piece = lane + active * q;
+      const bool ok = lane < active && piece < npieces;
+      off[q] = ok ? (uint32_t)(piece * VEC) : 0u;
+      vm[q] = __ballot(ok);
+    }
+  }
+};
+
+#define BS_CALL_ENC(RT)                                                                             \
+  do {                                                                                              \
+    if constexpr (VEC == 16)                                                                        \
+      bs_enc_r##RT##_v16(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.vm[0], ln.vm[1]); \
+    else if constexpr (VEC == 8)                                                                    \
+      bs_enc_r##RT##_v8(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], \
+                        ln.vm[0], ln.vm[1], ln.vm[2], ln.vm[3]);                                    \
+    else                                                                                            \
+      bs_enc_r##RT##_v4(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], \
+                        ln.off[4], ln.off[5], ln.off[6], ln.off[7], ln.vm[0], ln.vm[1], ln.vm[2],   \
+                        ln.vm[3], ln.vm[4], ln.vm[5], ln.vm[6], ln.vm[7]);                          \
+  } while (0)
+
+#define BS_CALL_DEC(RT)                                                                             \
+  do {                                                                                              \
+    if constexpr (VEC == 16)                                                                        \
+      bs_dec_r##RT##_v16(ia, oa, nsrc, k, ca, ln.off[0], ln.off[1], ln.vm[0], ln.vm[1]);            \
+    else if constexpr (VEC == 8)                                                                    \
+      bs_dec_r##RT##_v8(ia, oa, nsrc, k, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], ln.vm[0],  \
+                        ln.vm[1], ln.vm[2], ln.vm[3]);                                              \
+    else                                                                                            \
+      bs_dec_r##RT##_v4(ia, oa, nsrc, k, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], ln.off[4], \
+                        ln.off[5], ln.off[6], ln.off[7], ln.vm[0], ln.vm[1], ln.vm[2], ln.vm[3],    \
+                        ln.vm[4], ln.vm[5], ln.vm[6], ln.vm[7]);                                    \
+  } while (0)
+
+template <int RT, int VEC>
+__device__ __forceinline__ void bs_enc_call(uint64_t sp, uint64_t rpp, uint32_t L, uint32_t rstride, uint32_t nsrc,
+                                            uint32_t k, uint32_t rt, uint32_t ca, const BsLanes<VEC> &ln) {
+  if constexpr (RT == 1) BS_CALL_ENC(1);
+  else if constexpr (RT == 2) BS_CALL_ENC(2);
+  else if constexpr (RT == 4) BS_CALL_ENC(4);
+  else if constexpr (RT == 8) BS_CALL_ENC(8);
+  else BS_CALL_ENC(16);
+}
+
+template <int RT, int VEC>
+__device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t nsrc, uint32_t k, uint32_t ca,
+                                            const BsLanes<VEC> &ln) {
+  if constexpr (RT == 1) BS_CALL_DEC(1);
+  else if constexpr (RT == 2) BS_CALL_DEC(2);
+  else if constexpr (RT == 4) BS_CALL_DEC(4);
+  else if constexpr (RT == 8) BS_CALL_DEC(8);
+  else BS_CALL_DEC(16);
+}
+
+// blocks per group: 64 / RT coefficient lanes per block, bounded by the LDS budget
+__host__ __device__ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes) {
+  int g = 64 / RT;
+  while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
+  return g;
+}
+
+constexpr int kDecRec = 144;  // per-block record: 16 output addresses, nz base, rt (see gen_bitslice.py)
+
+template <int RT, int VEC>
+__global__ __launch_bounds__(64) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                      uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                      int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
+                                                      int r0, int G) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const int rt = r - r0 < RT ? r - r0 : RT;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
+    __syncthreads();
+    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g0 + lane / RT, repair r0 + lane % RT)
+      const int g = lane / RT, i = lane % RT;
+      const uint64_t b = g0 + g;
+      uint8_t *row = lds + (size_t)g * k * 16 + i;
+      if (b < nblocks && i < rt) {
+        Tmt t;
+        tmt_init(t, rlc_seed(block_fbn(b, fbn_base, fbn), (uint32_t)(r0 + i)));
+        for (int j = 0; j < k; j++) row[j * 16] = tmt_coef(t);
+      } else {
+        for (int j = 0; j < k; j++) row[j * 16] = 0;
+      }
+    }
+    __syncthreads();
+    const uint64_t ng = nblocks - g0 < (uint64_t)G ? nblocks - g0 : (uint64_t)G;
+    for (int ch = 0; ch < nchunks; ch++) {
+      const int c0 = ch * chunk_bytes;
+      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+      BsLanes<VEC> ln(lane, cb);
+      const uint64_t sp = (uint64_t)(uintptr_t)(src + (g0 * (uint64_t)k) * (uint64_t)L + c0);
+      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (g0 * (uint64_t)r + r0) * (uint64_t)L + c0);
+      if (lane < ln.active)
+        bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, (uint32_t)(r * L), (uint32_t)(ng * k), (uint32_t)k,
+                             (uint32_t)rt, lds_addr(lds), ln);
+    }
+  }
+}
+
+template <int RT, int VEC>
+__global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                       int chunk_bytes, uint8_t *ws, int r0, int G) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  // LDS: coef rows [G][k][16] | input addresses [G][k] x 8 B | records [G] x kDecRec
+  uint8_t *coef = lds;
+  uint64_t *intab = reinterpret_cast<uint64_t *>(lds + (size_t)G * k * 16);
+  uint8_t *rec = lds + (size_t)G * k * 24;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
+    bool act = false;
+    if (lane < G && g0 + lane < nblocks) {
+      const uint8_t *h = ws + (g0 + lane) * (uint64_t)WL.stride;
+      act = h[0] == FECGPU_BLOCK_RECOVERED && h[1] > r0;
+    }
+    const uint64_t am = __ballot(act);
+    const int nact = __popcll(am);
+    __syncthreads();
+    for (uint64_t m = am; m; m &= m - 1) {  // compacted slot t <- block g0 + g
+      const int g = __ffsll((long long)m) - 1;
+      const int t = __popcll(am & ((1ull << g) - 1));
+      const uint64_t b = g0 + g;
+      uint8_t *h = ws + b * (uint64_t)WL.stride;
+      const int e = h[1];
+      const int rt = e - r0 < RT ? e - r0 : RT;
+      for (int x = lane; x < k * 16; x += 64) {
+        const int j = x >> 4, u = x & 15;
+        coef[(size_t)t * k * 16 + x] = u < rt ? h[WL.off_D + (r0 + u) * k + j] : 0;
+      }
+      for (int j = lane; j < k; j += 64) {
+        const uint32_t sl = h[WL.off_slot + j];
+        const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
+                                       : src + (b * (uint64_t)k + sl) * (uint64_t)L;
+        intab[(size_t)t * k + j] = (uint64_t)(uintptr_t)p;
+      }
+      uint8_t *rc = rec + (size_t)t * kDecRec;
+      if (lane < rt)
+        reinterpret_cast<uint64_t *>(rc)[lane] =
+            (uint64_t)(uintptr_t)(src + (b * (uint64_t)k + h[WL.off_unk + r0 + lane]) * (uint64_t)L);
+      if (lane == 0) {
+        reinterpret_cast<uint64_t *>(rc)[16] = (uint64_t)(uintptr_t)(h + WL.off_nz + r0);
+        reinterpret_cast<uint32_t *>(rc)[34] = (uint32_t)rt;
+      }
+    }
+    __syncthreads();
+    if (!nact) continue;
+    for (int ch = 0; ch < nchunks; ch++) {
+      const int c0 = ch * chunk_bytes;
+      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+      BsLanes<VEC> ln(lane, cb);
+#pragma unroll
+      for (int q = 0; q < BsLanes<VEC>::NP; q++) ln.off[q] += (uint32_t)c0;  // chunk offset
+      if (lane < ln.active)
+        bs_dec_call<RT, VEC>(lds_addr(intab), lds_addr(rec), (uint32_t)(nact * k), (uint32_t)k, lds_addr(coef), ln);
+    }
+  }
+}
+
+static BsCfg pick_bs_cfg(int L) {
+  BsCfg c;
+  c.vec = (L % 16 == 0) ? 16 : (L % 8 == 0) ? 8 : 4;
+  c.nchunks = (L + 2047) / 2048;
+  int cb = (L + c.nchunks - 1) / c.nchunks;
+  cb = (cb + c.vec - 1) / c.vec * c.vec;
+  c.chunk_bytes = cb;
+  return c;
+}
+
+template <int RT, int VEC>
+static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
+                             uint32_t fbn_base, const uint32_t *fbn, int r0, hipStream_t s) {
+  const int G = bs_group(RT, k, 16, 0);
+  const size_t lds = (size_t)G * k * 16;
+  const uint64_t groups = (nb + G - 1) / G;
+  hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
+                     L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G);
+}
+
+template <int RT, int VEC>
+static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
+                              uint8_t *ws, int r0, hipStream_t s) {
+  const int G = bs_group(RT, k, 24, kDecRec);
+  const size_t lds = (size_t)G * ((size_t)k * 24 + kDecRec);
+  const uint64_t groups = (nb + G - 1) / G;
+  hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G);
+}
+
+#define FEC_BS_DISPATCH(FN, ...)                                                   \
+  switch (rt * 100 + cfg.vec) {                                                    \
+    case 116: FN<1, 16>(__VA_ARGS__); break;  case 108: FN<1, 8>(__VA_ARGS__); break;   \
+    case 104: FN<1, 4>(__VA_ARGS__); break;   case 216: FN<2, 16>(__VA_ARGS__); break;  \
+    case 208: FN<2, 8>(__VA_ARGS__); break;   case 204: FN<2, 4>(__VA_ARGS__); break;   \
+    case 416: FN<4, 16>(__VA_ARGS__); break;  case 408: FN<4, 8>(__VA_ARGS__); break;   \
+    case 404: FN<4, 4>(__VA_ARGS__); break;   case 816: FN<8, 16>(__VA_ARGS__); break;  \
+    case 808: FN<8, 8>(__VA_ARGS__); break;   case 804: FN<8, 4>(__VA_ARGS__); break;   \
+    case 1616: FN<16, 16>(__VA_ARGS__); break; case 1608: FN<16, 8>(__VA_ARGS__); break; \
+    default: FN<16, 4>(__VA_ARGS__); break;                                        \
+  }
+
+static bool use_perm_path() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("FECGPU_DATAPATH");
+    v = (e && strcmp(e, "perm") == 0) ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// =============================================================================================
 // XOR scheme
 // =============================================================================================
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -779,12 +1017,20 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   int rc = check_common(src, rep, nblocks, k, r, symbol_size);
   if (rc || nblocks == 0 || r == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
-  const int Ldw = (int)(symbol_size / 4);
-  const DataCfg cfg = pick_data_cfg(Ldw);
   const int rt = pick_rt(r);
-  for (int r0 = 0; r0 < (int)r; r0 += rt) {
-    FEC_DISPATCH_RT(launch_encode, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                    cfg, fbn_base, fbn, r0, s)
+  if (use_perm_path()) {
+    const int Ldw = (int)(symbol_size / 4);
+    const DataCfg cfg = pick_data_cfg(Ldw);
+    for (int r0 = 0; r0 < (int)r; r0 += rt) {
+      FEC_DISPATCH_RT(launch_encode, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
+                      cfg, fbn_base, fbn, r0, s)
+    }
+  } else {
+    const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+    for (int r0 = 0; r0 < (int)r; r0 += rt) {
+      FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
+                      (int)symbol_size, cfg, fbn_base, fbn, r0, s)
+    }
   }
   HIPCHK(hipGetLastError());
   g_stats[0]++;
@@ -849,12 +1095,20 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   }
   HIPCHK(hipGetLastError());
   if (r > 0) {
-    const int Ldw = (int)(symbol_size / 4);
-    const DataCfg cfg = pick_data_cfg(Ldw);
     const int rt = pick_rt(L.em);
-    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-      FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                      cfg, ws, r0, s)
+    if (use_perm_path()) {
+      const int Ldw = (int)(symbol_size / 4);
+      const DataCfg cfg = pick_data_cfg(Ldw);
+      for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+        FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
+                        cfg, ws, r0, s)
+      }
+    } else {
+      const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+      for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+        FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+                        (int)symbol_size, cfg, ws, r0, s)
+      }
     }
     HIPCHK(hipGetLastError());
   }

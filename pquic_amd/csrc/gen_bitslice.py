@@ -1,0 +1,455 @@
+#!/usr/bin/env python3
+"""Generate pquic_amd/csrc/bitslice_gen.h -- the bitsliced GF(2^8) multiply-accumulate
+engine of the RLC data path (gfx950 inline assembly).
+
+How a lane computes  acc_i += c_ij * S_j  over GF(2^8)/0x11D for 32 bytes at a time
+---------------------------------------------------------------------------------------
+* Bit slicing.  The lane's 32 bytes of S_j (8 dwords w0..w7) are transposed with three
+  rounds of masked shift-exchange (v_lshlrev/v_lshrrev + v_bitop3 mux) into 8 bit planes
+  x_0..x_7: plane p holds bit p of all 32 bytes.  Multiplying every byte by a constant c
+  is then a GF(2)-linear map on planes:  out_o = XOR_p M_c[o][p] x_p,  with column p of
+  M_c = c * alpha^p.
+* Four Russians.  Per source the lane builds TL[n] = XOR_{p<4, n_p} x_p and
+  TH[n] = XOR_{p<4, n_p} x_{p+4} (n = 1..15, 22 XORs), so each output plane is ONE
+  v_bitop3_b32 (3-input XOR):  acc_o ^= TL[row_o & 15] ^ TH[row_o >> 4].
+  A coefficient therefore costs at most 8 full-rate VALU ops per 32 bytes.
+* Dispatch.  The 8 register indices depend on the wave-uniform coefficient c, so the code
+  is selected per coefficient: a shared table of 256 cases (72 bytes each, 32 KiB-aligned)
+  is entered with s_swappc_b64 and left with s_setpc_b64.  The case code names the
+  accumulator planes as v0..v7; s_set_gpr_idx_on(SRC0,DST) relocates them to repair i's
+  accumulators (ACC_BASE + 8 i), while the table operands (SRC1/SRC2) stay absolute.
+* Output.  The same three exchange rounds are an involution, so applying them to the
+  accumulator planes yields the repair bytes in the original word order.
+
+The generator self-checks the plane algebra and the transpose against a byte-level GF
+model before writing the header.
+"""
+from __future__ import annotations
+
+import os
+import random
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "bitslice_gen.h")
+
+# ----------------------------------------------------------------------------- register map
+T_BASE = 32
+TL = {n: T_BASE + n - 1 for n in range(1, 16)}          # v32..v46
+TH = {n: T_BASE + 15 + n - 1 for n in range(1, 16)}     # v47..v61
+TMP = [62, 63, 64, 65]
+CO = [66, 67, 68, 69]
+COPTR = 70
+INPTR = 71
+OUTPTR = 72  # decode only; decode data buffers start one register later
+DATA_BASE = 72
+CASE_BYTES = 72
+# stage-0 destinations (scratch, overwritten by the combos), stage-2 destinations (planes)
+XS = [TL[3], TL[5], TL[6], TL[7], TH[3], TH[5], TH[6], TH[7]]
+PL = [TL[1], TL[2], TL[4], TL[8], TH[1], TH[2], TH[4], TH[8]]
+# SGPRs owned by the asm bodies
+S_TAB, S_TGT, S_RET, S_T, S_J = 60, 62, 64, 66, 67
+S_C = [68, 69, 70, 71]
+S_MASK = [72, 73, 74]
+S_T2 = 75
+S_CUR = 76
+S_SAVEM0 = 78
+S_SAVEEX = 80
+S_OUT = 82
+S_T3 = 84
+S_EPI = 86
+S_S = 88
+S_O2 = 90
+S_RT = 92
+S_NZ = 94
+SGPR_CLOBBER = list(range(60, 96))
+MASKS = [0x55555555, 0x33333333, 0x0F0F0F0F]
+STAGES = [  # (shift, mask index, pairs)
+    (1, 0, [(0, 1), (2, 3), (4, 5), (6, 7)]),
+    (2, 1, [(0, 2), (1, 3), (4, 6), (5, 7)]),
+    (4, 2, [(0, 4), (1, 5), (2, 6), (3, 7)]),
+]
+
+
+# ----------------------------------------------------------------------------- GF model
+def gf_mul(a: int, b: int) -> int:
+    p = 0
+    for _ in range(8):
+        if b & 1:
+            p ^= a
+        b >>= 1
+        carry = a & 0x80
+        a = (a << 1) & 0xFF
+        if carry:
+            a ^= 0x1D
+    return p
+
+
+def case_rows(c: int):
+    """(nl, nh) per output plane o for coefficient c."""
+    col = [gf_mul(c, 1 << p) for p in range(8)]  # column p = c * alpha^p
+    rows = []
+    for o in range(8):
+        bits = [(col[p] >> o) & 1 for p in range(8)]
+        nl = sum(bits[p] << p for p in range(4))
+        nh = sum(bits[p + 4] << p for p in range(4))
+        rows.append((nl, nh))
+    return rows
+
+
+def selfcheck():
+    # plane algebra: out byte = c * x for every c, x
+    for c in range(256):
+        rows = case_rows(c)
+        for x in range(256):
+            xp = [(x >> p) & 1 for p in range(8)]
+            tl = lambda n: sum(xp[p] for p in range(4) if (n >> p) & 1) & 1  # noqa: E731
+            th = lambda n: sum(xp[p + 4] for p in range(4) if (n >> p) & 1) & 1  # noqa: E731
+            out = 0
+            for o, (nl, nh) in enumerate(rows):
+                out |= (tl(nl) ^ th(nh)) << o
+            assert out == gf_mul(c, x), (c, x)
+    # transpose: plane p = bit p of all 32 bytes; involution
+    rnd = random.Random(1)
+    for _ in range(200):
+        w = [rnd.getrandbits(32) for _ in range(8)]
+        t = transpose_model(w)
+        for p in range(8):
+            for byte in range(4):
+                for b in range(8):
+                    orig = (w[b] >> (8 * byte + p)) & 1
+                    assert ((t[p] >> (8 * byte + b)) & 1) == orig
+        assert transpose_model(t) == w
+
+
+def transpose_model(w):
+    w = list(w)
+    for sh, mi, pairs in STAGES:
+        m = MASKS[mi]
+        for a, b in pairs:
+            t0 = (w[b] << sh) & 0xFFFFFFFF
+            t1 = w[a] >> sh
+            na = (m & w[a]) | (~m & t0 & 0xFFFFFFFF)
+            nb = (m & t1) | (~m & w[b] & 0xFFFFFFFF)
+            w[a], w[b] = na, nb
+    return w
+
+
+# ----------------------------------------------------------------------------- code emitters
+def v(n):
+    return f"v{n}"
+
+
+def emit_table():
+    lines = ['  .text', '  .p2align 15', '  .globl fec_bs_case_table', '  .hidden fec_bs_case_table', 'fec_bs_case_table:']
+    for c in range(256):
+        body = []
+        for o, (nl, nh) in enumerate(case_rows(c)):
+            if nl and nh:
+                body.append(f"v_bitop3_b32 v{o}, v{o}, {v(TL[nl])}, {v(TH[nh])} bitop3:0x96")
+            elif nl:
+                body.append(f"v_xor_b32 v{o}, v{o}, {v(TL[nl])}")
+            elif nh:
+                body.append(f"v_xor_b32 v{o}, v{o}, {v(TH[nh])}")
+        body.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+        lines += ["  " + b for b in body]
+        lines.append(f"  .org fec_bs_case_table + {CASE_BYTES * (c + 1)}")
+    return lines
+
+
+def transpose_fwd(src_words):
+    """src_words: 8 VGPR numbers (read only). Writes planes into PL via scratch XS."""
+    out = []
+    cur = list(src_words)
+    for si, (sh, mi, pairs) in enumerate(STAGES):
+        dst = list(cur)
+        for pi, (a, b) in enumerate(pairs):
+            if si == 0:
+                da, db = XS[a], XS[b]
+            elif si == 2:
+                da, db = PL[a], PL[b]
+            else:
+                da, db = cur[a], cur[b]
+            t0, t1 = (TMP[0], TMP[1]) if pi % 2 == 0 else (TMP[2], TMP[3])
+            out += [f"v_lshlrev_b32 v{t0}, {sh}, v{cur[b]}",
+                    f"v_lshrrev_b32 v{t1}, {sh}, v{cur[a]}",
+                    f"v_bitop3_b32 v{da}, s{S_MASK[mi]}, v{cur[a]}, v{t0} bitop3:0xca",
+                    f"v_bitop3_b32 v{db}, s{S_MASK[mi]}, v{t1}, v{cur[b]} bitop3:0xca"]
+            dst[a], dst[b] = da, db
+        cur = dst
+    return out
+
+
+def transpose_inplace(regs):
+    out = []
+    for sh, mi, pairs in STAGES:
+        for pi, (a, b) in enumerate(pairs):
+            t0, t1 = (TMP[0], TMP[1]) if pi % 2 == 0 else (TMP[2], TMP[3])
+            out += [f"v_lshlrev_b32 v{t0}, {sh}, v{regs[b]}",
+                    f"v_lshrrev_b32 v{t1}, {sh}, v{regs[a]}",
+                    f"v_bitop3_b32 v{regs[a]}, s{S_MASK[mi]}, v{regs[a]}, v{t0} bitop3:0xca",
+                    f"v_bitop3_b32 v{regs[b]}, s{S_MASK[mi]}, v{t1}, v{regs[b]} bitop3:0xca"]
+    return out
+
+
+def combos():
+    out = []
+    for T, name in ((TL, "L"), (TH, "H")):
+        out += [f"v_xor_b32 v{T[3]}, v{T[1]}, v{T[2]}",
+                f"v_xor_b32 v{T[5]}, v{T[1]}, v{T[4]}",
+                f"v_xor_b32 v{T[6]}, v{T[2]}, v{T[4]}",
+                f"v_xor_b32 v{T[9]}, v{T[1]}, v{T[8]}",
+                f"v_xor_b32 v{T[10]}, v{T[2]}, v{T[8]}",
+                f"v_xor_b32 v{T[12]}, v{T[4]}, v{T[8]}",
+                f"v_bitop3_b32 v{T[7]}, v{T[1]}, v{T[2]}, v{T[4]} bitop3:0x96",
+                f"v_bitop3_b32 v{T[11]}, v{T[1]}, v{T[2]}, v{T[8]} bitop3:0x96",
+                f"v_bitop3_b32 v{T[13]}, v{T[1]}, v{T[4]}, v{T[8]} bitop3:0x96",
+                f"v_bitop3_b32 v{T[14]}, v{T[2]}, v{T[4]}, v{T[8]} bitop3:0x96",
+                f"v_bitop3_b32 v{T[15]}, v{T[3]}, v{T[4]}, v{T[8]} bitop3:0x96"]
+    return out
+
+
+LOADOP = {16: ("global_load_dwordx4", "global_store_dwordx4", 4),
+          8: ("global_load_dwordx2", "global_store_dwordx2", 2),
+          4: ("global_load_dword", "global_store_dword", 1)}
+
+
+def regrange(base, n):
+    return f"v{base}" if n == 1 else f"v[{base}:{base + n - 1}]"
+
+
+def body(mode: str, RT: int, VEC: int, P: int):
+    """Inline-asm text for one group of blocks x one column chunk.
+
+    The sources of all blocks of the group form ONE stream (flattened index s = g*k + j),
+    so the P-deep register prefetch runs across block boundaries; when j wraps, the
+    per-block epilogue subroutine (reached by s_swappc) transposes the accumulators back,
+    stores them and clears them.  mode 'enc' (addresses by stride) or 'dec' (addresses
+    from LDS tables written by the wrapper)."""
+    ld, st, nw = LOADOP[VEC]
+    NP = 32 // VEC
+    DATA_BASE = data_base(mode)
+    acc_base = DATA_BASE + 8 * P
+    assert acc_base + 8 * RT <= 256
+    L = []
+    a = L.append
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a(f"s_mov_b32 s{S_SAVEM0}, m0")
+    a(f"s_mov_b64 s[{S_SAVEEX}:{S_SAVEEX + 1}], exec")
+    for i, m in enumerate(MASKS):
+        a(f"s_mov_b32 s{S_MASK[i]}, 0x{m:08x}")
+    a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
+    a(f"s_add_u32 s{S_TAB}, s{S_TAB}, fec_bs_case_table@rel32@lo+4")
+    a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, fec_bs_case_table@rel32@hi+12")
+    a(f"s_getpc_b64 s[{S_EPI}:{S_EPI + 1}]")
+    a(".Lepipc_%=:")
+    a(f"s_add_u32 s{S_EPI}, s{S_EPI}, .Lepi_%= - .Lepipc_%=")
+    a(f"s_addc_u32 s{S_EPI + 1}, s{S_EPI + 1}, 0")
+    for r in range(acc_base, acc_base + 8 * RT):
+        a(f"v_mov_b32 v{r}, 0")
+    for r in range(DATA_BASE, DATA_BASE + 8 * P):
+        a(f"v_mov_b32 v{r}, 0")
+    a(f"v_mov_b32 v{COPTR}, %[coef]")
+    if mode == "enc":
+        a(f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], %[src]")
+        a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
+    else:
+        a(f"v_mov_b32 v{INPTR}, %[intab]")
+        a(f"v_mov_b32 v{OUTPTR}, %[outtab]")
+    a(f"s_mov_b32 s{S_S}, 0")
+    a(f"s_mov_b32 s{S_J}, 0")
+
+    def load_source(buf):
+        out = []
+        if mode == "dec":
+            out += [f"ds_read_b64 v[{TMP[0]}:{TMP[1]}], v{INPTR}",
+                    f"v_add_u32 v{INPTR}, 8, v{INPTR}",
+                    "s_waitcnt lgkmcnt(0)",
+                    f"v_readfirstlane_b32 s{S_CUR}, v{TMP[0]}",
+                    f"v_readfirstlane_b32 s{S_CUR + 1}, v{TMP[1]}"]
+        for q in range(NP):
+            out += [f"s_mov_b64 exec, %[vm{q}]",
+                    f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]"]
+        out.append(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+        if mode == "enc":
+            out += [f"s_add_u32 s{S_CUR}, s{S_CUR}, %[L]", f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, 0"]
+        return out
+
+    for q in range(P - 1):  # prologue: sources 0 .. P-2
+        a(f"s_cmp_lt_u32 {q}, %[nsrc]")
+        a(f"s_cbranch_scc0 .Lpro_done_%=")
+        L.extend(load_source(q))
+    a(".Lpro_done_%=:")
+    ncw = 1 if RT <= 4 else (2 if RT <= 8 else 4)
+    dsr = {1: "ds_read_b32", 2: "ds_read_b64", 4: "ds_read_b128"}[ncw]
+    for b in range(P):
+        nb = (b + P - 1) % P
+        a(f".Lbody{b}_%=:")
+        a(f"s_add_u32 s{S_T2}, s{S_S}, {P - 1}")
+        a(f"s_cmp_lt_u32 s{S_T2}, %[nsrc]")
+        a(f"s_cbranch_scc0 .Lnopf{b}_%=")
+        L.extend(load_source(nb))
+        a(f"s_waitcnt vmcnt({NP * (P - 1)})")
+        a(f"s_branch .Lpf{b}_%=")
+        a(f".Lnopf{b}_%=:")
+        a("s_waitcnt vmcnt(0)")
+        a(f".Lpf{b}_%=:")
+        a(f"{dsr} {regrange(CO[0], ncw)}, v{COPTR}")
+        a(f"v_add_u32 v{COPTR}, 16, v{COPTR}")
+        L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
+        L.extend(combos())
+        a("s_waitcnt lgkmcnt(0)")
+        for w in range(ncw):
+            a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+        for i in range(RT):
+            a(f"s_bfe_u32 s{S_T}, s{S_C[i // 4]}, 0x{(8 << 16) | (8 * (i % 4)):x}")
+            a(f"s_mul_i32 s{S_T}, s{S_T}, {CASE_BYTES}")
+            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
+            a(f"s_addc_u32 s{S_TGT + 1}, s{S_TAB + 1}, 0")
+            if i == 0:
+                a(f"s_set_gpr_idx_on {acc_base}, gpr_idx(SRC0,DST)")
+            else:
+                a(f"s_set_gpr_idx_idx {acc_base + 8 * i}")
+            a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+        a("s_set_gpr_idx_off")
+        a(f"s_add_u32 s{S_S}, s{S_S}, 1")
+        a(f"s_add_u32 s{S_J}, s{S_J}, 1")
+        a(f"s_cmp_eq_u32 s{S_J}, %[k]")
+        a(f"s_cbranch_scc0 .Lnoepi{b}_%=")
+        a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]")
+        a(f"s_mov_b32 s{S_J}, 0")
+        a(f".Lnoepi{b}_%=:")
+        a(f"s_cmp_lt_u32 s{S_S}, %[nsrc]")
+        a(f"s_cbranch_scc0 .Lexit_%=")
+    a(f"s_branch .Lbody0_%=")
+
+    # ---- per-block epilogue subroutine ----
+    a(".Lepi_%=:")
+    if mode == "enc":
+        a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
+        a(f"s_mov_b32 s{S_RT}, %[rt]")
+    else:
+        a(f"ds_read_b128 v[{TMP[0]}:{TMP[3]}], v{OUTPTR} offset:128")
+        a("s_waitcnt lgkmcnt(0)")
+        a(f"v_readfirstlane_b32 s{S_NZ}, v{TMP[0]}")
+        a(f"v_readfirstlane_b32 s{S_NZ + 1}, v{TMP[1]}")
+        a(f"v_readfirstlane_b32 s{S_RT}, v{TMP[2]}")
+    for i in range(RT):
+        accs = [acc_base + 8 * i + w for w in range(8)]
+        a(f"s_cmp_le_u32 s{S_RT}, {i}")
+        a(f"s_cbranch_scc1 .Lepi_done_%=")
+        L.extend(transpose_inplace(accs))
+        if mode == "dec":
+            a(f"ds_read_b64 v[{TMP[2]}:{TMP[3]}], v{OUTPTR} offset:{8 * i}")
+            a(f"v_or3_b32 v{TMP[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
+            a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[3]}, v{accs[4]}")
+            a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[5]}, v{accs[6]}")
+            a(f"v_or_b32 v{TMP[0]}, v{TMP[0]}, v{accs[7]}")
+            a(f"v_cmp_ne_u32 vcc, 0, v{TMP[0]}")
+            a(f"v_mov_b32 v{TMP[0]}, 0")
+            a(f"v_mov_b32 v{TMP[1]}, 1")
+            a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
+            a(f"global_store_byte v{TMP[0]}, v{TMP[1]}, s[{S_NZ}:{S_NZ + 1}] offset:{i}")
+            a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+            a("s_waitcnt lgkmcnt(0)")
+            a(f"v_readfirstlane_b32 s{S_O2}, v{TMP[2]}")
+            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{TMP[3]}")
+        for q in range(NP):
+            a(f"s_mov_b64 exec, %[vm{q}]")
+            a(f"{st} %[off{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]")
+        a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+        if mode == "enc":
+            a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
+            a(f"s_addc_u32 s{S_O2 + 1}, s{S_O2 + 1}, 0")
+    a(".Lepi_done_%=:")
+    for r in range(acc_base, acc_base + 8 * RT):
+        a(f"v_mov_b32 v{r}, 0")
+    if mode == "enc":
+        a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rstride]")
+        a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, 0")
+    else:
+        a(f"v_add_u32 v{OUTPTR}, {DEC_REC_BYTES}, v{OUTPTR}")
+    a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+    a(".Lexit_%=:")
+    a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+    a(f"s_mov_b32 m0, s{S_SAVEM0}")
+    return L, acc_base + 8 * RT
+
+
+def cstring(lines):
+    return "\n".join(f'      "{ln}\\n"' for ln in lines)
+
+
+def emit_function(mode, RT, VEC, P):
+    lines, top = body(mode, RT, VEC, P)
+    NP = 32 // VEC
+    name = f"bs_{mode}_r{RT}_v{VEC}"
+    offs = ", ".join(f"uint32_t off{q}" for q in range(NP))
+    vms = ", ".join(f"uint64_t vm{q}" for q in range(NP))
+    if mode == "enc":
+        sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rstride, "
+               f"uint32_t nsrc, uint32_t k, uint32_t rt, uint32_t coef, {offs}, {vms})")
+        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rstride] "s"(rstride)', '[rt] "s"(rt)']
+    else:
+        sig = (f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, uint32_t nsrc, "
+               f"uint32_t k, uint32_t coef, {offs}, {vms})")
+        ins = ['[intab] "v"(intab)', '[outtab] "v"(outtab)']
+    ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "v"(coef)']
+    ins += [f'[off{q}] "v"(off{q})' for q in range(NP)]
+    ins += [f'[vm{q}] "s"(vm{q})' for q in range(NP)]
+    clob = [f'"v{r}"' for r in range(T_BASE, top)] + [f'"s{r}"' for r in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
+    out = [sig + " {", "  asm volatile(", cstring(lines), "      :",
+           "      : " + ", ".join(ins), "      : " + ", ".join(clob) + ");", "}"]
+    return "\n".join(out), top
+
+
+DEC_REC_BYTES = 144  # per-block decode record in LDS: 16 x 8 B output addresses, nz base, rt
+
+
+def data_base(mode: str) -> int:
+    return DATA_BASE if mode == "enc" else DATA_BASE + 2  # tuples must start on an even VGPR
+
+
+def prefetch_depth(mode: str, RT: int) -> int:
+    """Deepest register prefetch that keeps 3 waves/SIMD (<= 168 VGPRs) where possible."""
+    for P in (8, 7, 6, 5, 4, 3, 2):
+        if data_base(mode) + 8 * P + 8 * RT <= 168:
+            return P
+    return 2
+
+
+CONFIGS = [(RT, VEC) for VEC in (16, 8, 4) for RT in (1, 2, 4, 8, 16)]
+
+
+def main():
+    selfcheck()
+    parts = ["// GENERATED by pquic_amd/csrc/gen_bitslice.py -- do not edit.",
+             "// Bitsliced GF(2^8) multiply-accumulate bodies for gfx950 (see the generator's docstring).",
+             "#pragma once",
+             "#include <hip/hip_runtime.h>",
+             "#include <stdint.h>",
+             "",
+             f"#define FEC_BS_CASE_BYTES {CASE_BYTES}",
+             "",
+             "// Shared 256-case table: case c applies  acc[v0..v7] ^= TL[.] ^ TH[.]  for coefficient c.",
+             "// It lives in the body of a never-launched kernel (HIP drops module-level asm in the",
+             "// device pass); the data-path bodies reach it through a PC-relative relocation.",
+             "__global__ void fec_bs_case_table_holder() {",
+             "  asm volatile(",
+             '    "s_endpgm\\n"']
+    parts += [f'    "{ln}\\n"' for ln in emit_table()]
+    parts += ['    "  s_endpgm\\n");', "}", ""]
+    tops = {}
+    for mode in ("enc", "dec"):
+        for RT, VEC in CONFIGS:
+            P = prefetch_depth(mode, RT)
+            fn, top = emit_function(mode, RT, VEC, P)
+            tops[(mode, RT, VEC, P)] = top
+            parts.append(fn)
+            parts.append("")
+    with open(OUT, "w") as f:
+        f.write("\n".join(parts))
+    print(f"wrote {OUT}: {len(CONFIGS) * 2} bodies, max VGPR {max(tops.values())}")
+
+
+if __name__ == "__main__":
+    main()
