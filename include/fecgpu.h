@@ -86,6 +86,29 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
                       const uint64_t *rep_present, uint8_t *status, uint64_t *recovered,
                       void *stream);
 
+/* ---- Host-resident path --------------------------------------------------------------------
+ * The same operations on HOST buffers (pageable or pinned): H2D copy, kernels, D2H copy,
+ * pipelined over sub-batches of about `chunk_bytes` of payload on `nstreams` HIP streams so
+ * that PCIe transfers overlap the kernels.  Synchronous: results are in host memory on
+ * return.  Used by the protoop adapters (one block per call) and by the PCIe-inclusive
+ * measurement.  Decode copies whole source rows both ways (received sources in, recovered
+ * sources back in place). */
+typedef struct fecgpu_host_ctx fecgpu_host_ctx_t;
+fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk_bytes);
+void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *ctx);
+int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *ctx, const void *src, void *rep, uint64_t nblocks,
+                           uint32_t k, uint32_t r, uint32_t symbol_size, uint32_t fbn_base,
+                           const uint32_t *fbn);
+int fecgpu_rlc_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,
+                           uint32_t k, uint32_t r, uint32_t symbol_size, uint32_t fbn_base,
+                           const uint32_t *fbn, const uint64_t *src_present,
+                           const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
+int fecgpu_xor_encode_host(fecgpu_host_ctx_t *ctx, const void *src, void *rep, uint64_t nblocks,
+                           uint32_t k, uint32_t symbol_size);
+int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,
+                           uint32_t k, uint32_t symbol_size, const uint64_t *src_present,
+                           const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
+
 /* Synthetic payload generator (bench/tests): byte o of dst = byte (o mod 8) of
  * splitmix64(seed + (o/8 + 1) * 0x9e3779b97f4a7c15), o counted from `offset`. */
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream);

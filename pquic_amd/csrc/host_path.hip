@@ -1,0 +1,202 @@
+// pquic_amd/csrc/host_path.hip -- host-resident entry points of include/fecgpu.h.
+//
+// The reference path starts and ends in host packet buffers (picoquic/packet.c:1468 on
+// receive, sender.c:1084 on send).  These entry points move a batch of FEC blocks through
+// the device: per sub-batch, H2D copy -> fecgpu_* kernels -> D2H copy on one of `nstreams`
+// streams, so the copies of one sub-batch overlap the kernels of the next.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+
+#include "../../include/fecgpu.h"
+
+namespace {
+constexpr int kMaxStreams = 4;
+
+struct Slot {
+  hipStream_t st = nullptr;
+  void *d_src = nullptr, *d_rep = nullptr, *d_aux = nullptr, *d_ws = nullptr;
+  size_t cap_src = 0, cap_rep = 0, cap_aux = 0, cap_ws = 0;
+};
+
+hipError_t grow(void **p, size_t *cap, size_t need) {
+  if (need <= *cap) return hipSuccess;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  hipError_t e = hipMalloc(p, need);
+  if (e == hipSuccess) *cap = need;
+  return e;
+}
+}  // namespace
+
+struct fecgpu_host_ctx {
+  int device = 0;
+  int ns = 1;
+  size_t chunk_bytes = 64u << 20;
+  Slot slot[kMaxStreams];
+  std::mutex mu;
+};
+
+#define HCHK(x)                        \
+  do {                                 \
+    hipError_t e_ = (x);               \
+    if (e_ != hipSuccess) return FECGPU_ERR_HIP; \
+  } while (0)
+
+extern "C" {
+
+fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk_bytes) {
+  if (fecgpu_init(device) != FECGPU_OK) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  auto *c = new fecgpu_host_ctx;
+  c->device = device;
+  c->ns = nstreams < 1 ? 1 : (nstreams > kMaxStreams ? kMaxStreams : nstreams);
+  c->chunk_bytes = chunk_bytes ? chunk_bytes : (64u << 20);
+  for (int i = 0; i < c->ns; i++) {
+    if (hipStreamCreateWithFlags(&c->slot[i].st, hipStreamNonBlocking) != hipSuccess) {
+      fecgpu_host_ctx_destroy(c);
+      return nullptr;
+    }
+  }
+  return c;
+}
+
+void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (int i = 0; i < kMaxStreams; i++) {
+    Slot &s = c->slot[i];
+    if (s.st) { (void)hipStreamSynchronize(s.st); (void)hipStreamDestroy(s.st); }
+    if (s.d_src) (void)hipFree(s.d_src);
+    if (s.d_rep) (void)hipFree(s.d_rep);
+    if (s.d_aux) (void)hipFree(s.d_aux);
+    if (s.d_ws) (void)hipFree(s.d_ws);
+  }
+  delete c;
+}
+
+static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t per_block) {
+  uint64_t n = c->chunk_bytes / (per_block ? per_block : 1);
+  if (n < 1) n = 1;
+  return n < nblocks ? n : nblocks;
+}
+
+static int finish(fecgpu_host_ctx_t *c) {
+  for (int i = 0; i < c->ns; i++) HCHK(hipStreamSynchronize(c->slot[i].st));
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn) {
+  if (!c || !src || !rep) return FECGPU_ERR_INVALID;
+  if (!nblocks || !r) return FECGPU_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  const size_t sb = (size_t)k * L, rb = (size_t)r * L;
+  const uint64_t n = sub_batch(c, nblocks, sb);
+  int si = 0;
+  for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
+    Slot &s = c->slot[si];
+    const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
+    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
+    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+    const uint32_t *df = nullptr;
+    if (fbn) {
+      HCHK(grow(&s.d_aux, &s.cap_aux, n * 4));
+      HCHK(hipMemcpyAsync(s.d_aux, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+      df = (const uint32_t *)s.d_aux;
+    }
+    HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+    int rc = fecgpu_rlc_encode(s.d_src, s.d_rep, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu), df, s.st);
+    if (rc) return rc;
+    HCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
+  }
+  return finish(c);
+}
+
+int fecgpu_xor_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uint64_t nblocks, uint32_t k,
+                           uint32_t L) {
+  if (!c || !src || !rep) return FECGPU_ERR_INVALID;
+  if (!nblocks) return FECGPU_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  const size_t sb = (size_t)k * L, rb = L;
+  const uint64_t n = sub_batch(c, nblocks, sb);
+  int si = 0;
+  for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
+    Slot &s = c->slot[si];
+    const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
+    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
+    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+    HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+    int rc = fecgpu_xor_encode(s.d_src, s.d_rep, m, k, L, s.st);
+    if (rc) return rc;
+    HCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
+  }
+  return finish(c);
+}
+
+// aux layout per sub-batch: fbn[n] (u32, padded to 16), src_present[n][2], rep_present[n][2],
+// recovered[n][2] (u64), status[n] (u8)
+static size_t aux_bytes(uint64_t n) { return ((n * 4 + 15) & ~(size_t)15) + n * 16 * 3 + n; }
+
+static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep, uint64_t nblocks, uint32_t k,
+                       uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn, const uint64_t *sp,
+                       const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
+  if (!c || !src || !rep || !sp || !rp || !status || !recovered) return FECGPU_ERR_INVALID;
+  if (!nblocks) return FECGPU_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  const size_t sb = (size_t)k * L, rb = (size_t)r * L;
+  const uint64_t n = sub_batch(c, nblocks, sb + rb);
+  int si = 0;
+  for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
+    Slot &s = c->slot[si];
+    const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
+    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
+    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+    HCHK(grow(&s.d_aux, &s.cap_aux, aux_bytes(n)));
+    uint8_t *aux = (uint8_t *)s.d_aux;
+    uint32_t *d_fbn = (uint32_t *)aux;
+    uint64_t *d_sp = (uint64_t *)(aux + ((n * 4 + 15) & ~(size_t)15));
+    uint64_t *d_rp = d_sp + 2 * n, *d_rec = d_rp + 2 * n;
+    uint8_t *d_st = (uint8_t *)(d_rec + 2 * n);
+    HCHK(hipMemcpyAsync(d_sp, sp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+    HCHK(hipMemcpyAsync(d_rp, rp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+    if (fbn) HCHK(hipMemcpyAsync(d_fbn, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+    HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+    HCHK(hipMemcpyAsync(s.d_rep, (const uint8_t *)rep + b0 * rb, m * rb, hipMemcpyHostToDevice, s.st));
+    int rc;
+    if (xr) {
+      rc = fecgpu_xor_decode(s.d_src, s.d_rep, m, k, L, d_sp, d_rp, d_st, d_rec, s.st);
+    } else {
+      const size_t wsb = fecgpu_rlc_decode_workspace(n, k, r);
+      HCHK(grow(&s.d_ws, &s.cap_ws, wsb));
+      rc = fecgpu_rlc_decode(s.d_src, s.d_rep, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu),
+                             fbn ? d_fbn : nullptr, d_sp, d_rp, d_st, d_rec, s.d_ws, s.cap_ws, s.st);
+    }
+    if (rc) return rc;
+    HCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
+    HCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
+    HCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
+  }
+  return finish(c);
+}
+
+int fecgpu_rlc_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn,
+                           const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
+  return decode_host(c, false, src, rep, nblocks, k, r, L, fbn_base, fbn, sp, rp, status, recovered);
+}
+
+int fecgpu_xor_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
+                           uint32_t L, const uint64_t *sp, const uint64_t *rp, uint8_t *status,
+                           uint64_t *recovered) {
+  return decode_host(c, true, src, rep, nblocks, k, 1, L, 0, nullptr, sp, rp, status, recovered);
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+/*
+ * tests/host/mini_host.c -- TEST INFRASTRUCTURE: a minimal stand-in for the picoquic plugin
+ * runtime, enough to drive the FEC scheme protocol operations the way the reference does.
+ *
+ *   - picoquic_cnx_t carries protoop_inputv / protoop_outputv like the real connection
+ *     (picoquic/picoquic_internal.h), read and written by get_cnx / set_cnx
+ *     (picoquic/getset.c:137-142, 370-379);
+ *   - my_malloc hands out fixed 2100-byte slots for requests <= 2092 bytes and falls back
+ *     to the heap above that, like a plugin with dynamic_memory (picoquic/memory.c:72-95,
+ *     181-191; plugin.c:409-424); live allocations are counted for leak checks;
+ *   - run_protoop mirrors plugin_run_protoop_internal's argument passing
+ *     (picoquic/plugin.c:1279-1450): set inputs, call the operation, collect outputs.
+ * Blocks are assembled as the block framework does (block_framework_sender.h:175-203,
+ * block_framework_receiver.h:29-80, fec.h:292-308).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pquic_fec_protoops.h"
+
+struct st_picoquic_cnx_t {
+    protoop_arg_t inputv[16];
+    protoop_arg_t outputv[16];
+    int inputc, outputc;
+};
+
+static long g_live;
+
+static protoop_arg_t mh_get_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param) {
+    if (ak == PQUIC_AK_CNX_INPUT) return param < cnx->inputc ? cnx->inputv[param] : 0;
+    if (ak == PQUIC_AK_CNX_OUTPUT) return cnx->outputv[param];
+    return 0;
+}
+
+static void mh_set_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, protoop_arg_t val) {
+    if (ak == PQUIC_AK_CNX_OUTPUT && param < 16) {
+        cnx->outputv[param] = val;
+        if (param + 1 > cnx->outputc) cnx->outputc = param + 1;
+    }
+}
+
+static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
+    (void)cnx;
+    void *p = malloc(size <= 2092 ? 2100 : size);
+    if (p) g_live++;
+    return p;
+}
+
+static void mh_free(picoquic_cnx_t *cnx, void *p) {
+    (void)cnx;
+    if (p) { g_live--; free(p); }
+}
+
+typedef protoop_arg_t (*op_t)(picoquic_cnx_t *);
+
+static protoop_arg_t run_protoop(picoquic_cnx_t *cnx, op_t op, int inputc, const protoop_arg_t *inputv,
+                                 protoop_arg_t *outputv) {
+    memset(cnx, 0, sizeof *cnx);
+    cnx->inputc = inputc;
+    for (int i = 0; i < inputc; i++) cnx->inputv[i] = inputv[i];
+    protoop_arg_t ret = op(cnx);
+    if (outputv)
+        for (int i = 0; i < cnx->outputc; i++) outputv[i] = cnx->outputv[i];
+    return ret;
+}
+
+int mh_bind(int device) {
+    pquic_fec_host_api_t api = {mh_get_cnx, mh_set_cnx, mh_malloc, mh_free};
+    return pquic_fec_bind_host(&api, device);
+}
+
+int mh_unbind(void) { return pquic_fec_bind_host(NULL, 0); }
+
+long mh_live_allocations(void) { return g_live; }
+
+static op_t op_create(int xor_scheme) {
+    return xor_scheme ? pquic_fec_xor_create_fec_schemes : pquic_fec_rlc_create_fec_schemes;
+}
+
+static pquic_source_symbol_t *mk_source(uint32_t fbn, int j, const uint8_t *data, uint16_t len) {
+    picoquic_cnx_t c;
+    pquic_source_symbol_t *s = mh_malloc(&c, sizeof *s);
+    memset(s, 0, sizeof *s);
+    s->fpid.raw = (fbn << 8) | (uint32_t)j;
+    s->data = mh_malloc(&c, len);
+    memcpy(s->data, data, len);
+    s->data_length = len;
+    return s;
+}
+
+static void free_block(pquic_fec_block_t *fb) {
+    picoquic_cnx_t c;
+    for (int j = 0; j < PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK; j++) {
+        if (fb->source_symbols[j]) { mh_free(&c, fb->source_symbols[j]->data); mh_free(&c, fb->source_symbols[j]); }
+        if (fb->repair_symbols[j]) { mh_free(&c, fb->repair_symbols[j]->data); mh_free(&c, fb->repair_symbols[j]); }
+    }
+    free(fb);
+}
+
+/* Sender side: k sources -> fec_generate_repair_symbols.  Returns the protoop's code;
+ * repairs copied to rep_out[i * stride], lengths / raw FPIDs per repair. */
+long mh_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
+                 int src_stride, uint8_t *rep_out, uint16_t *rep_len, uint64_t *rep_fpid, int rep_stride,
+                 uint64_t *scheme_out) {
+    picoquic_cnx_t cnx;
+    protoop_arg_t schemes[2] = {0, 0};
+    protoop_arg_t ret = run_protoop(&cnx, op_create(xor_scheme), 0, NULL, schemes);
+    if (ret) return (long)ret;
+    scheme_out[0] = schemes[0];
+    scheme_out[1] = schemes[1];
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    fb->fec_block_number = fbn;
+    for (int j = 0; j < k; j++) fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+    fb->current_source_symbols = (uint8_t)k;
+    fb->total_source_symbols = (uint8_t)k;      /* block_framework_sender.h:184-185 */
+    fb->total_repair_symbols = (uint8_t)r;
+    protoop_arg_t in[2] = {(protoop_arg_t)(uintptr_t)fb, schemes[1]};
+    ret = run_protoop(&cnx, xor_scheme ? pquic_fec_xor_generate_repair_symbols : pquic_fec_rlc_generate_repair_symbols,
+                      2, in, NULL);
+    for (int i = 0; i < r; i++) {
+        pquic_repair_symbol_t *rs = fb->repair_symbols[i];
+        rep_len[i] = rs ? rs->data_length : 0;
+        rep_fpid[i] = rs ? rs->fpid.raw : 0;
+        if (rs) memcpy(rep_out + (size_t)i * rep_stride, rs->data, rs->data_length);
+    }
+    if (schemes[1] && !xor_scheme) mh_free(&cnx, (void *)(uintptr_t)schemes[1]);
+    free_block(fb);
+    return (long)ret;
+}
+
+/* Receiver side: a block with the given sources / repairs present -> fec_recover.
+ * recovered[j] = 1 for every source inserted by the operation; its bytes and length in
+ * out[j * stride] / out_len[j]; *cur_ss = current_source_symbols afterwards. */
+long mh_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
+                const uint8_t *src_present, int src_stride, const uint8_t *rep, const uint16_t *rep_len,
+                const uint8_t *rep_present, const uint64_t *rep_fpid, int rep_stride, uint8_t *out,
+                uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss) {
+    picoquic_cnx_t cnx;
+    protoop_arg_t schemes[2] = {0, 0};
+    protoop_arg_t ret = run_protoop(&cnx, op_create(xor_scheme), 0, NULL, schemes);
+    if (ret) return (long)ret;
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    fb->fec_block_number = fbn;
+    fb->total_source_symbols = (uint8_t)k;       /* block_framework_receiver.h:42-43 */
+    fb->total_repair_symbols = (uint8_t)r;
+    for (int j = 0; j < k; j++)
+        if (src_present[j]) {
+            fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+            fb->current_source_symbols++;
+        }
+    for (int i = 0; i < r; i++)
+        if (rep_present[i]) {
+            pquic_repair_symbol_t *rs = mh_malloc(&cnx, sizeof *rs);
+            memset(rs, 0, sizeof *rs);
+            rs->fpid.raw = rep_fpid[i];
+            rs->data = mh_malloc(&cnx, rep_len[i]);
+            memcpy(rs->data, rep + (size_t)i * rep_stride, rep_len[i]);
+            rs->data_length = rep_len[i];
+            fb->repair_symbols[i] = rs;
+            fb->current_repair_symbols++;
+        }
+    pquic_source_symbol_t *before[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
+    memcpy(before, fb->source_symbols, sizeof before);
+    protoop_arg_t in[2] = {(protoop_arg_t)(uintptr_t)fb, schemes[0]};
+    ret = run_protoop(&cnx, xor_scheme ? pquic_fec_xor_recover : pquic_fec_rlc_recover, 2, in, NULL);
+    for (int j = 0; j < k; j++) {
+        pquic_source_symbol_t *ss = fb->source_symbols[j];
+        recovered[j] = ss && ss != before[j];
+        out_len[j] = recovered[j] ? ss->data_length : 0;
+        if (recovered[j]) memcpy(out + (size_t)j * out_stride, ss->data, ss->data_length);
+    }
+    *cur_ss = fb->current_source_symbols;
+    if (schemes[0] && !xor_scheme) mh_free(&cnx, (void *)(uintptr_t)schemes[0]);
+    free_block(fb);
+    return (long)ret;
+}

@@ -1,0 +1,93 @@
+"""C-ABI boundary checks that need no GPU: the engine library loads, exports every entry
+point declared in include/*.h, validates arguments without touching a device, matches the
+reference's fec_block_t layout, and refuses to compute when no gfx950 device is present
+(there is no CPU fallback in the product path)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from golden_io import load
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+LIB = os.path.join(ROOT, "pquic_amd", "lib", "libpquic_fec.so")
+MINIHOST = os.path.join(ROOT, "tests", "host", "libminihost.so")
+
+
+def declared_functions():
+    names = set()
+    for h in ("fecgpu.h", "pquic_fec_protoops.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b((?:fecgpu|pquic_fec)_\w+)\s*\(", text, re.M):
+            if not m.group(0).lstrip().startswith("typedef"):
+                names.add(m.group(1))
+    return sorted(names)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    return C.CDLL(LIB)
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_layout_matches_reference(lib):
+    lay = load("layout.json")
+    out = (C.c_uint64 * 8)()
+    assert lib.pquic_fec_layout(out) == 8
+    exp = [lay["sizeof_fec_block_t"], lay["sizeof_source_symbol_t"], lay["sizeof_repair_symbol_t"],
+           lay["off_source_symbols"], lay["off_repair_symbols"], lay["off_source_data"],
+           lay["off_repair_data"], lay["sizeof_repair_fpid_t"]]
+    assert list(out) == exp
+
+
+def test_argument_validation_without_device(lib):
+    lib.fecgpu_rlc_encode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_void_p, C.c_void_p]
+    assert lib.fecgpu_rlc_encode(None, None, 0, 4, 1, 1200, 0, None, None) == 0      # empty batch
+    assert lib.fecgpu_rlc_encode(None, None, 1, 4, 1, 1200, 0, None, None) == -1     # NULL buffers
+    assert lib.fecgpu_rlc_encode(16, 16, 1, 4, 1, 1201, 0, None, None) == -1         # L % 4
+    assert lib.fecgpu_rlc_encode(16, 16, 1, 0, 1, 1200, 0, None, None) == -1         # k = 0
+    assert lib.fecgpu_rlc_encode(16, 16, 1, 129, 1, 1200, 0, None, None) == -1       # k > 128
+    lib.fecgpu_rlc_decode_workspace.restype = C.c_size_t
+    lib.fecgpu_rlc_decode_workspace.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+    assert lib.fecgpu_rlc_decode_workspace(1000, 16, 4) >= 1000 * (16 * 4 + 16)
+    lib.fecgpu_version.restype = C.c_char_p
+    assert b"gfx950" in lib.fecgpu_version()
+
+
+def test_no_cpu_fallback(lib):
+    """Without a gfx950 device the engine reports NO_DEVICE and the protoop adapters fail
+    with an error code instead of computing on the CPU."""
+    if lib.fecgpu_init(0) == 0:
+        pytest.skip("a gfx950 device is present here")
+    assert lib.fecgpu_init(0) == -3
+    mh = C.CDLL(MINIHOST)
+    mh.mh_generate.restype = C.c_long
+    import numpy as np
+    k, r, L = 4, 2, 64
+    src = np.arange(k * L, dtype=np.uint8)
+    lens = np.full(k, L, np.uint16)
+    rep = np.zeros(r * L, np.uint8)
+    rl = np.zeros(r, np.uint16)
+    fp = np.zeros(r, np.uint64)
+    sch = np.zeros(2, np.uint64)
+    p = lambda a, t=C.c_uint8: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    # unbound: the documented error code
+    mh.mh_unbind()
+    assert mh.mh_generate(0, 7, k, r, p(src), p(lens, C.c_uint16), L, p(rep), p(rl, C.c_uint16),
+                          p(fp, C.c_uint64), L, p(sch, C.c_uint64)) == 0x41B
+    mh.mh_bind(0)
+    before = mh.mh_live_allocations()
+    ret = mh.mh_generate(0, 7, k, r, p(src), p(lens, C.c_uint16), L, p(rep), p(rl, C.c_uint16),
+                         p(fp, C.c_uint64), L, p(sch, C.c_uint64))
+    assert ret == 0x41B and not rep.any()
+    assert mh.mh_live_allocations() == before

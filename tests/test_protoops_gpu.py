@@ -1,0 +1,166 @@
+"""The drop-in protocol operations (include/pquic_fec_protoops.h), driven through a minimal
+picoquic stand-in (tests/host/mini_host.c) exactly as the block framework calls the
+reference pluglets, against fixtures produced by the reference pluglets themselves."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from golden_io import decode_sources, load, sha
+from oracle_py import Oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+MINIHOST = os.path.join(ROOT, "tests", "host", "libminihost.so")
+
+
+def _p(a, t=C.c_uint8):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Host:
+    def __init__(self):
+        self.lib = C.CDLL(MINIHOST)
+        self.lib.mh_generate.restype = C.c_long
+        self.lib.mh_recover.restype = C.c_long
+        self.lib.mh_live_allocations.restype = C.c_long
+        assert self.lib.mh_bind(0) == 0
+
+    def generate(self, xor, fbn, srcs, r):
+        k = len(srcs)
+        stride = max([len(s) for s in srcs] + [1])
+        buf = np.zeros((k, stride), np.uint8)
+        lens = np.zeros(k, np.uint16)
+        for j, s in enumerate(srcs):
+            buf[j, : len(s)] = s
+            lens[j] = len(s)
+        rep = np.zeros((max(r, 1), stride), np.uint8)
+        rl = np.zeros(max(r, 1), np.uint16)
+        fp = np.zeros(max(r, 1), np.uint64)
+        sch = np.zeros(2, np.uint64)
+        ret = self.lib.mh_generate(int(xor), fbn, k, r, _p(buf), _p(lens, C.c_uint16), stride, _p(rep),
+                                   _p(rl, C.c_uint16), _p(fp, C.c_uint64), stride, _p(sch, C.c_uint64))
+        return ret, [rep[i, : rl[i]].copy() for i in range(r)], [int(x) for x in fp[:r]], sch
+
+    def recover(self, xor, fbn, srcs, reps, fpids):
+        k, r = len(srcs), len(reps)
+        stride = max([len(s) for s in srcs + reps if s is not None] + [1])
+        sb = np.zeros((k, stride), np.uint8)
+        sl = np.zeros(k, np.uint16)
+        spres = np.zeros(k, np.uint8)
+        for j, s in enumerate(srcs):
+            if s is not None:
+                sb[j, : len(s)] = s
+                sl[j] = len(s)
+                spres[j] = 1
+        rb = np.zeros((max(r, 1), stride), np.uint8)
+        rl = np.zeros(max(r, 1), np.uint16)
+        rpres = np.zeros(max(r, 1), np.uint8)
+        for i, s in enumerate(reps):
+            if s is not None:
+                rb[i, : len(s)] = s
+                rl[i] = len(s)
+                rpres[i] = 1
+        fp = np.zeros(max(r, 1), np.uint64)
+        fp[:r] = fpids
+        out = np.zeros((k, stride), np.uint8)
+        ol = np.zeros(k, np.uint16)
+        rec = np.zeros(k, np.uint8)
+        cur = C.c_int(0)
+        ret = self.lib.mh_recover(int(xor), fbn, k, r, _p(sb), _p(sl, C.c_uint16), _p(spres), stride, _p(rb),
+                                  _p(rl, C.c_uint16), _p(rpres), _p(fp, C.c_uint64), stride, _p(out),
+                                  _p(ol, C.c_uint16), _p(rec), stride, C.byref(cur))
+        return ret, {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}, cur.value
+
+
+@pytest.fixture(scope="module")
+def host():
+    return Host()
+
+
+def test_generate_varlen_matches_reference(host):
+    e = load("encode_cases.json")
+    for case in e["varlen"]:
+        srcs = [np.frombuffer(bytes.fromhex(h), np.uint8) for h in case["src_hex"]]
+        ret, reps, fps, sch = host.generate(case["scheme"] == "xor", case["fbn"], srcs, case["r"])
+        assert ret == case["ret"]
+        assert [x.tobytes().hex() for x in reps] == case["rep_hex"]
+        assert fps == case["repair_fpid_raw"]
+        if case["scheme"] == "rlc":
+            assert sch[0] == sch[1] != 0   # one scheme object for both directions
+        else:
+            assert sch[0] == sch[1] == 0   # create_xor_fec_scheme.c:6-7
+
+
+def test_generate_fixed_cases_and_preconditions(host):
+    from golden_io import encode_inputs, load_npz
+    e = load("encode_cases.json")
+    full = load_npz("encode_full.npz")
+    for case in e["cases"]:
+        if case["k"] > 100 or case["r"] > 100:
+            continue
+        src = encode_inputs(case)
+        for b in range(case["nblocks"]):
+            fbn = (case["fbn_base"] + b) & 0xFFFFFF
+            ret, reps, fps, _ = host.generate(case["scheme"] == "xor", fbn, list(src[b]), case["r"])
+            assert ret == 0
+            assert sha(np.stack(reps).tobytes()) == case["block_sha256"][b], case["name"]
+            assert fps == case["repair_fpid_raw"][b]
+    for p in e["preconditions"]:
+        srcs = [np.arange(10, dtype=np.uint8) + j for j in range(p["k"])]
+        ret, _, _, _ = host.generate(p["scheme"] == "xor", 3, srcs, p["r"])
+        assert ret == p["ret"]
+
+
+def _decode_case(host, case):
+    srcs_full = decode_sources(case)
+    k, r, fbn = case["k"], case["r"], case["fbn"]
+    o = Oracle()
+    if case["scheme"] == "xor":
+        reps_full = [o.xor_encode_block(srcs_full)[1]]
+        fpids = [fbn << 8]
+    else:
+        reps_full = o.rlc_encode_block(fbn, srcs_full, r)[1]
+        fpids = [(fbn << 8) | i for i in range(r)]
+    srcs = [None if j in case["src_missing"] else srcs_full[j] for j in range(k)]
+    reps = [reps_full[i] if i in case["rep_present"] else None for i in range(r)]
+    return host.recover(case["scheme"] == "xor", fbn, srcs, reps, fpids), srcs
+
+
+def test_recover_matches_reference(host):
+    d = load("decode_cases.json")
+    n = 0
+    for case in d["cases"] + d["zero_cases"] + d["varlen_cases"]:
+        if case["crashed"] or case["k"] > 100:
+            continue
+        (ret, rec, cur), srcs = _decode_case(host, case)
+        assert ret == case["ret"], case["tag"]
+        got = {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())}
+        assert got == case["recovered"], case["tag"]
+        assert {str(j): len(v) for j, v in rec.items()} == case["recovered_len"]
+        present = sum(s is not None for s in srcs)
+        if case["scheme"] == "rlc":
+            assert cur == present + len(rec)   # rlc_fec_scheme_gf256.c:230
+        else:
+            assert cur == present              # xor_fec_scheme.c:72 does not count it
+        n += 1
+    assert n > 350
+
+
+def test_recover_reference_crash_patterns_do_not_crash(host):
+    d = load("decode_cases.json")
+    crashed = [c for c in d["cases"] if c["crashed"]]
+    assert crashed
+    for case in crashed:
+        (ret, rec, _), _ = _decode_case(host, case)
+        assert ret == 0 and rec == {}
+
+
+def test_no_leaks(host):
+    base = host.lib.mh_live_allocations()
+    d = load("decode_cases.json")
+    for case in d["cases"][:40]:
+        _decode_case(host, case)
+    assert host.lib.mh_live_allocations() == base
