@@ -6,8 +6,8 @@ it loads that library with ctypes and passes device pointers (torch CUDA tensors
 used only as HBM allocations and for the HIP stream).  There is no CPU fallback: if the
 library or a gfx950 device is missing, calls raise.
 """
-from .engine import Engine, FecGpuError, load_library, LIB_PATH  # noqa: F401
+from .engine import Engine, FecGpuError, HostPath, load_library, LIB_PATH  # noqa: F401
 from .engine import BLOCK_RECOVERED, BLOCK_NOTHING, BLOCK_REF_UB  # noqa: F401
 
-__all__ = ["Engine", "FecGpuError", "load_library", "LIB_PATH",
+__all__ = ["Engine", "FecGpuError", "HostPath", "load_library", "LIB_PATH",
            "BLOCK_RECOVERED", "BLOCK_NOTHING", "BLOCK_REF_UB"]

@@ -1063,19 +1063,25 @@ size_t fecgpu_rlc_decode_workspace(uint64_t nblocks, uint32_t k, uint32_t r) {
   return (size_t)nblocks * ws_layout(k, r).stride;
 }
 
-int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
-                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
-                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
-                      uint64_t *recovered, void *workspace, size_t workspace_bytes, void *stream) {
-  int rc = check_common(src, rep, nblocks, k, r, symbol_size);
-  if (rc || nblocks == 0) return rc;
-  if (!src_present || !rep_present || !status || !recovered || !workspace)
-    return set_err(FECGPU_ERR_INVALID, "%s", "NULL mask/status/workspace");
-  if (workspace_bytes < fecgpu_rlc_decode_workspace(nblocks, k, r))
+static int decode_args(const void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r, uint32_t L,
+                       const void *a, const void *b, const void *c, const void *d, void *ws, size_t wsb) {
+  int rc = check_common(src, rep, nblocks, k, r, L);
+  if (rc) return rc;
+  if (nblocks && (!a || !b || !c || !d || !ws)) return set_err(FECGPU_ERR_INVALID, "%s", "NULL mask/status/workspace");
+  if (nblocks && wsb < fecgpu_rlc_decode_workspace(nblocks, k, r))
     return set_err(FECGPU_ERR_NOMEM, "%s", "decode workspace too small");
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
+                           const uint64_t *src_present, const uint64_t *rep_present, void *workspace,
+                           size_t workspace_bytes, void *stream) {
+  static const uint32_t dummy = 0;
+  int rc = decode_args(&dummy, &dummy, nblocks, k, r, 4, src_present, rep_present, &dummy, &dummy, workspace,
+                       workspace_bytes);
+  if (rc || nblocks == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
-  const WsLayout L = ws_layout(k, r);
   const size_t lane_lds = 768 + 64 * (size_t)lane_arena_bytes(k, r);
   if (lane_lds <= 48 * 1024) {
     const uint64_t groups = (nblocks + 63) / 64;
@@ -1094,28 +1100,64 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
                        fbn_base, fbn, src_present, rep_present, ws);
   }
   HIPCHK(hipGetLastError());
-  if (r > 0) {
-    const int rt = pick_rt(L.em);
-    if (use_perm_path()) {
-      const int Ldw = (int)(symbol_size / 4);
-      const DataCfg cfg = pick_data_cfg(Ldw);
-      for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-        FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                        cfg, ws, r0, s)
-      }
-    } else {
-      const BsCfg cfg = pick_bs_cfg((int)symbol_size);
-      for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-        FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
-                        (int)symbol_size, cfg, ws, r0, s)
-      }
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                            uint32_t symbol_size, void *workspace, size_t workspace_bytes, void *stream) {
+  static const uint64_t dummy = 0;
+  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, &dummy, &dummy, &dummy, &dummy, workspace,
+                       workspace_bytes);
+  if (rc || nblocks == 0 || r == 0) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t *ws = (uint8_t *)workspace;
+  const WsLayout L = ws_layout(k, r);
+  const int rt = pick_rt(L.em);
+  if (use_perm_path()) {
+    const int Ldw = (int)(symbol_size / 4);
+    const DataCfg cfg = pick_data_cfg(Ldw);
+    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+      FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
+                      cfg, ws, r0, s)
     }
-    HIPCHK(hipGetLastError());
+  } else {
+    const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+      FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+                      (int)symbol_size, cfg, ws, r0, s)
+    }
   }
-  const uint32_t fgrid = (uint32_t)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
-  hipLaunchKernelGGL(k_rlc_finalize, dim3(fgrid), dim3(256), 0, s, nblocks, (int)k, (int)r, ws, status,
-                     recovered);
   HIPCHK(hipGetLastError());
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode_finish(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *status, uint64_t *recovered,
+                             const void *workspace, size_t workspace_bytes, void *stream) {
+  static const uint32_t dummy = 0;
+  int rc = decode_args(&dummy, &dummy, nblocks, k, r, 4, &dummy, &dummy, status, recovered, (void *)workspace,
+                       workspace_bytes);
+  if (rc || nblocks == 0) return rc;
+  const uint32_t fgrid = (uint32_t)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
+  hipLaunchKernelGGL(k_rlc_finalize, dim3(fgrid), dim3(256), 0, (hipStream_t)stream, nblocks, (int)k, (int)r,
+                     (const uint8_t *)workspace, status, recovered);
+  HIPCHK(hipGetLastError());
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                      uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
+                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                      uint64_t *recovered, void *workspace, size_t workspace_bytes, void *stream) {
+  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, src_present, rep_present, status, recovered,
+                       workspace, workspace_bytes);
+  if (rc || nblocks == 0) return rc;
+  if ((rc = fecgpu_rlc_decode_plan(nblocks, k, r, fbn_base, fbn, src_present, rep_present, workspace,
+                                   workspace_bytes, stream)))
+    return rc;
+  if ((rc = fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, workspace, workspace_bytes, stream)))
+    return rc;
+  if ((rc = fecgpu_rlc_decode_finish(nblocks, k, r, status, recovered, workspace, workspace_bytes, stream)))
+    return rc;
   g_stats[2]++;
   g_stats[3] += nblocks;
   return FECGPU_OK;

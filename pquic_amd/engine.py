@@ -45,8 +45,18 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_rlc_decode_workspace.restype = sz
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
+    L.fecgpu_rlc_decode_plan.argtypes = [u64, u32, u32, u32, v, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, sz, v]
+    L.fecgpu_rlc_decode_finish.argtypes = [u64, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
+    L.fecgpu_host_ctx_create.argtypes = [C.c_int, C.c_int, sz]
+    L.fecgpu_host_ctx_create.restype = v
+    L.fecgpu_host_ctx_destroy.argtypes = [v]
+    L.fecgpu_rlc_encode_host.argtypes = [v, v, v, u64, u32, u32, u32, u32, v]
+    L.fecgpu_rlc_decode_host.argtypes = [v, v, v, u64, u32, u32, u32, u32, v, v, v, v, v]
+    L.fecgpu_xor_encode_host.argtypes = [v, v, v, u64, u32, u32]
+    L.fecgpu_xor_decode_host.argtypes = [v, v, v, u64, u32, u32, v, v, v, v]
     _lib = L
     return L
 
@@ -56,7 +66,9 @@ def _addr(x):
         return None
     if isinstance(x, int):
         return x
-    return x.data_ptr()
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return x.ctypes.data  # numpy (host-resident path)
 
 
 class Engine:
@@ -126,6 +138,27 @@ class Engine:
             workspace.numel(), self._stream(stream)), "fecgpu_rlc_decode")
         return status, recovered
 
+    def rlc_decode_stages(self, src, rep, src_present, rep_present, status, recovered, k, r, L, nblocks,
+                          workspace, fbn_base=0, stream=None, events=None):
+        """fecgpu_rlc_decode as its three stages; events[i] (if given) recorded before stage i
+        and events[3] after the last, on the launch stream."""
+        st = self._stream(stream)
+        torch_stream = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        rec = (lambda i: events[i].record(torch_stream)) if events else (lambda i: None)
+        rec(0)
+        self._check(self.lib.fecgpu_rlc_decode_plan(nblocks, k, r, fbn_base, None, _addr(src_present),
+                                                    _addr(rep_present), _addr(workspace), workspace.numel(), st),
+                    "fecgpu_rlc_decode_plan")
+        rec(1)
+        self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(workspace),
+                                                     workspace.numel(), st), "fecgpu_rlc_decode_apply")
+        rec(2)
+        self._check(self.lib.fecgpu_rlc_decode_finish(nblocks, k, r, _addr(status), _addr(recovered),
+                                                      _addr(workspace), workspace.numel(), st),
+                    "fecgpu_rlc_decode_finish")
+        rec(3)
+        return status, recovered
+
     def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,
                    nblocks: int | None = None, stream=None):
         nb = nblocks if nblocks is not None else src.numel() // (k * L)
@@ -138,3 +171,38 @@ class Engine:
         self._check(self.lib.fecgpu_synth_fill(_addr(dst), nbytes, seed, offset, self._stream(stream)),
                     "fecgpu_synth_fill")
         return dst
+
+
+class HostPath:
+    """Host-resident entry points (include/fecgpu.h 'Host-resident path'): host buffers in,
+    host buffers out, H2D/D2H overlapped with the kernels on `nstreams` streams."""
+
+    def __init__(self, device: int = 0, nstreams: int = 3, chunk_bytes: int = 64 << 20):
+        self.lib = load_library()
+        self.ctx = self.lib.fecgpu_host_ctx_create(device, nstreams, chunk_bytes)
+        if not self.ctx:
+            raise FecGpuError(f"fecgpu_host_ctx_create({device}) failed: {self.lib.fecgpu_last_error().decode()}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.fecgpu_host_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != OK:
+            raise FecGpuError(f"{what} failed ({rc}): {self.lib.fecgpu_last_error().decode()}")
+
+    def rlc_encode(self, src, rep, nblocks, k, r, L, fbn_base=0):
+        self._chk(self.lib.fecgpu_rlc_encode_host(self.ctx, _addr(src), _addr(rep), nblocks, k, r, L, fbn_base,
+                                                  None), "fecgpu_rlc_encode_host")
+
+    def rlc_decode(self, src, rep, sp, rp, status, rec, nblocks, k, r, L, fbn_base=0):
+        self._chk(self.lib.fecgpu_rlc_decode_host(self.ctx, _addr(src), _addr(rep), nblocks, k, r, L, fbn_base,
+                                                  None, _addr(sp), _addr(rp), _addr(status), _addr(rec)),
+                  "fecgpu_rlc_decode_host")

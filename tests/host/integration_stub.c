@@ -1,0 +1,38 @@
+/*
+ * tests/host/integration_stub.c -- TEST INFRASTRUCTURE: the reference-side binding from
+ * INTEGRATION.md §2-§4, compiled against picoquic's real headers (survey container only),
+ * proving the adapter header is type-compatible with picoquic's plugin ABI.
+ */
+#include "picoquic.h"
+#include "picoquic_internal.h"
+#include "getset.h"
+#include "memory.h"
+#include "uthash.h"
+#include "pquic_fec_protoops.h"
+
+void pquic_fec_install(int hip_device) {
+    static const pquic_fec_host_api_t api = {get_cnx, set_cnx, my_malloc, my_free};
+    pquic_fec_bind_host(&api, hip_device);
+}
+
+static protoop_plugin_t *fec_plugin(picoquic_cnx_t *cnx) {
+    protoop_plugin_t *p = NULL;
+    HASH_FIND_STR(cnx->plugins, "be.michelfra.fecxor", p);
+    return p;
+}
+static void *fec_malloc(picoquic_cnx_t *cnx, unsigned int n) {
+    protoop_plugin_t *p = fec_plugin(cnx);
+    return p->memory_manager.my_malloc(p, n);
+}
+static void fec_free(picoquic_cnx_t *cnx, void *ptr) { my_free_in_core(fec_plugin(cnx), ptr); }
+
+void pquic_fec_install_native(picoquic_cnx_t *cnx) {
+    static const pquic_fec_host_api_t api = {get_cnx, set_cnx, fec_malloc, fec_free};
+    pquic_fec_bind_host(&api, 0);
+    static protoop_id_t pid_create = {.id = "create_fec_schemes"};
+    static protoop_id_t pid_gen = {.id = "fec_generate_repair_symbols"};
+    static protoop_id_t pid_rec = {.id = "fec_recover"};
+    register_noparam_protoop(cnx, &pid_create, pquic_fec_rlc_create_fec_schemes);
+    register_noparam_protoop(cnx, &pid_gen, pquic_fec_rlc_generate_repair_symbols);
+    register_noparam_protoop(cnx, &pid_rec, pquic_fec_rlc_recover);
+}

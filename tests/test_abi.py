@@ -91,3 +91,16 @@ def test_no_cpu_fallback(lib):
                          p(fp, C.c_uint64), L, p(sch, C.c_uint64))
     assert ret == 0x41B and not rep.any()
     assert mh.mh_live_allocations() == before
+
+
+def test_integration_stub_compiles_against_picoquic(tmp_path):
+    """INTEGRATION.md's binding (both options) compiles against picoquic's own headers
+    (survey container only; the reference tree is not on the GPU box)."""
+    import subprocess
+    pico = "/root/reference/picoquic"
+    if not os.path.isdir(pico):
+        pytest.skip("reference tree not present")
+    r = subprocess.run(["gcc", "-std=gnu11", "-c", "-Wall", "-Werror", f"-I{pico}",
+                        f"-I{os.path.join(ROOT, 'include')}", os.path.join(ROOT, "tests", "host", "integration_stub.c"),
+                        "-o", str(tmp_path / "stub.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
