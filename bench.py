@@ -36,7 +36,8 @@ def parse():
     p.add_argument("--r", type=int, default=4)
     p.add_argument("--erasures", type=int, default=4)
     p.add_argument("--symbol", type=int, default=1200)
-    p.add_argument("--no-legs", action="store_true", help="skip the k=32 r=8 encode leg")
+    p.add_argument("--no-legs", action="store_true", help="skip the PCIe and k=32 r=8 encode legs")
+    p.add_argument("--no-pcie", action="store_true", help="skip the PCIe end-to-end legs")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
@@ -213,7 +214,7 @@ def main():
     n_rec = int(ok.sum())
     n_ub = int((status == 2).sum())
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -225,9 +226,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    seg = [sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / args.steps for i in range(4)]
-    enc_ms, plan_ms, apply_ms, fin_ms = seg
-    dec_ms = plan_ms + apply_ms + fin_ms
+    seg = [sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / args.steps for i in range(3)]
+    enc_ms, plan_ms, apply_ms = seg  # apply includes the zero/undetermined rule (fused for e <= 16)
+    dec_ms = plan_ms + apply_ms
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -246,14 +247,13 @@ def main():
                               "algorithmic_GB_s": round(enc_gbs, 1), "hbm_frac": round(enc_gbs / HBM_PEAK_GBS, 4),
                               "bytes_per_launch": enc_bytes, "traffic": load_traffic("rlc_encode_k16_r4")},
         "rlc_decode_k16_e4": {"ms": round(dec_ms, 3), "plan_ms": round(plan_ms, 3), "apply_ms": round(apply_ms, 3),
-                              "finish_ms": round(fin_ms, 3),
                               "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
                               "apply_kernel": "k_rlc_recover_bs<4,16>", "apply_algorithmic_GB_s": round(app_gbs, 1),
                               "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
                               "ref_ub_blocks": n_ub, "traffic": load_traffic("rlc_decode_apply_k16_e4")},
     }
     del work, ws
-    if not args.no_legs and world == 1:
+    if not args.no_legs and not args.no_pcie and world == 1:
         legs.update(pcie_legs(torch, args, dev))
     if not args.no_legs and world == 1:
         # north-star leg: k = 32, r = 8 encode, 2^21 blocks (one GPU's share of config 4)

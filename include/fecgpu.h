@@ -80,20 +80,19 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
                       uint8_t *status, uint64_t *recovered, void *workspace,
                       size_t workspace_bytes, void *stream);
 
-/* The three stages fecgpu_rlc_decode runs, for callers that schedule or time them apart:
- * plan   -- coefficient-only replay of the reference elimination per block (workspace);
- * apply  -- the data pass: e recovered symbols from k received ones, written in place;
- * finish -- the reference's zero/undetermined rule, status[] and recovered[]. */
+/* The two stages fecgpu_rlc_decode runs, for callers that schedule or time them apart:
+ * plan  -- coefficient-only replay of the reference elimination per block (workspace);
+ * apply -- the data pass (e recovered symbols from k received ones, written in place) and the
+ *          reference's zero/undetermined rule, writing status[] and recovered[].  When
+ *          min(k, r) <= 16 the rule runs inside the data kernel; otherwise apply launches one
+ *          more small kernel after the data passes. */
 int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base,
                            const uint32_t *fbn, const uint64_t *src_present,
                            const uint64_t *rep_present, void *workspace, size_t workspace_bytes,
                            void *stream);
 int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
-                            uint32_t symbol_size, void *workspace, size_t workspace_bytes,
-                            void *stream);
-int fecgpu_rlc_decode_finish(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *status,
-                             uint64_t *recovered, const void *workspace, size_t workspace_bytes,
-                             void *stream);
+                            uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
+                            void *workspace, size_t workspace_bytes, void *stream);
 
 /* XOR decode (r == 1), same conventions. */
 int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,

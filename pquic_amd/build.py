@@ -51,10 +51,13 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in hip + c + hdr + [__file__])
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Build LIB (or, for A/B experiments, `out` with extra -D `defines`)."""
+    if out is None and not defines and not force and up_to_date():
         return LIB
+    target = out or LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     hip, c, _ = sources()
     hipcc = _hipcc()
     objs = []
@@ -65,16 +68,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
         objs.append(obj)
     for src in hip:
         obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + inc)
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + inc +
+             ["-D" + d for d in defines])
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, target)
     for o in objs:
         os.remove(o)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", target)
+    return target
 
 
 if __name__ == "__main__":

@@ -392,6 +392,15 @@ __host__ __device__ static inline uint32_t lane_arena_bytes(uint32_t k, uint32_t
   return em * em + em * k + 3 * em;
 }
 
+// Output records are assembled in LDS (row per lane, padded to an odd dword count so byte
+// writes from the 64 lanes spread over the banks) and leave as coalesced dword stores: the wave's
+// 64 workspace records are contiguous in HBM.
+__host__ __device__ static inline uint32_t plan_out_row(uint32_t stride) { return stride + 4; }
+
+__host__ __device__ static inline size_t plan_lane_lds(uint32_t k, uint32_t r) {
+  return 768 + 64 * (size_t)lane_arena_bytes(k, r) + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
+}
+
 __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, int r, uint32_t fbn_base,
                                                       const uint32_t *fbn, const uint64_t *sp,
                                                       const uint64_t *rp, uint8_t *ws) {
@@ -403,111 +412,124 @@ __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, i
   for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
   __syncthreads();
   uint8_t *my = lds + 768 + lane;
+  const uint32_t orow = plan_out_row(L.stride);
+  uint8_t *obase = lds + 768 + 64 * (size_t)lane_arena_bytes((uint32_t)k, (uint32_t)r);
+  uint8_t *h = obase + (size_t)lane * orow;  // this lane's workspace record (LDS copy)
   const int oA = 0, oV = em * em, oP = oV + em * k, oU = oP + em, oS = oU + em;
 #define AR(e) my[(e) * 64]
   for (uint64_t base = (uint64_t)blockIdx.x * 64; base < nblocks; base += (uint64_t)gridDim.x * 64) {
     const uint64_t b = base + lane;
-    if (b >= nblocks) continue;
-    uint8_t *h = ws + b * (uint64_t)L.stride;
-    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
-    clip128(s0, s1, k);
-    clip128(q0, q1, r);
-    const int cur_ss = __popcll(s0) + __popcll(s1);
-    const int cur_rs = __popcll(q0) + __popcll(q1);
-    if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
-      h[0] = FECGPU_BLOCK_NOTHING;
-      h[1] = 0;
-      continue;
-    }
-    const int n = k - cur_ss;
-    uint64_t m0 = ~s0, m1 = ~s1;
-    clip128(m0, m1, k);
-    {
-      int u = 0;
-      for (int j = 0; j < k; j++)
-        if (bit128(m0, m1, j)) AR(oU + u++) = (uint8_t)j;
-      int e = 0;
-      for (int i = 0; i < r && e < n; i++)
-        if (bit128(q0, q1, i)) AR(oS + e++) = (uint8_t)i;
-    }
-    const uint32_t f = block_fbn(b, fbn_base, fbn);
-    for (int e = 0; e < n; e++) {  // system rows, :194-212
-      Tmt t;
-      tmt_init(t, rlc_seed(f, AR(oS + e)));
-      int u = 0;
-      for (int j = 0; j < k; j++) {
-        uint8_t c = tmt_coef(t);
-        if (bit128(m0, m1, j)) {
-          AR(oA + e * em + u) = c;
-          AR(oV + e * k + j) = (uint8_t)(u == e);
-          u++;
-        } else {
-          AR(oV + e * k + j) = c;
-        }
+    if (b < nblocks) do {
+      uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
+      clip128(s0, s1, k);
+      clip128(q0, q1, r);
+      const int cur_ss = __popcll(s0) + __popcll(s1);
+      const int cur_rs = __popcll(q0) + __popcll(q1);
+      if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
+        h[0] = FECGPU_BLOCK_NOTHING;
+        h[1] = 0;
+        break;
       }
-      AR(oP + e) = (uint8_t)e;
-    }
-    for (int i = 0; i < n; i++) {  // sort_system :28-40
-      int mx = i;
-      for (int j = i + 1; j < n; j++)
-        if (AR(oA + AR(oP + mx) * em + i) < AR(oA + AR(oP + j) * em + i)) mx = j;
-      uint8_t t = AR(oP + i); AR(oP + i) = AR(oP + mx); AR(oP + mx) = t;
-    }
-    for (int i = 0; i < n - 1; i++) {  // elimination :54-70
-      const int pi = AR(oP + i);
-      const uint32_t piv = AR(oA + pi * em + i);
-      if (!piv) continue;  // inv(0) = 0: every term is 0, nothing changes
-      const uint32_t lip = 255u - LOG[piv];
-      for (int kk = i + 1; kk < n; kk++) {
-        const int pk = AR(oP + kk);
-        const uint32_t a = AR(oA + pk * em + i);
-        if (!a) continue;
-        const uint32_t lt = LOG[EXP[LOG[a] + lip]];
-        for (int u = 0; u < n; u++) {
-          uint32_t x = AR(oA + pi * em + u);
-          if (x) AR(oA + pk * em + u) ^= EXP[lt + LOG[x]];
-        }
+      const int n = k - cur_ss;
+      uint64_t m0 = ~s0, m1 = ~s1;
+      clip128(m0, m1, k);
+      {
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          if (bit128(m0, m1, j)) AR(oU + u++) = (uint8_t)j;
+        int e = 0;
+        for (int i = 0; i < r && e < n; i++)
+          if (bit128(q0, q1, i)) AR(oS + e++) = (uint8_t)i;
+      }
+      const uint32_t f = block_fbn(b, fbn_base, fbn);
+      for (int e = 0; e < n; e++) {  // system rows, :194-212
+        Tmt t;
+        tmt_init(t, rlc_seed(f, AR(oS + e)));
+        int u = 0;
         for (int j = 0; j < k; j++) {
-          uint32_t x = AR(oV + pi * k + j);
-          if (x) AR(oV + pk * k + j) ^= EXP[lt + LOG[x]];
+          uint8_t c = tmt_coef(t);
+          if (bit128(m0, m1, j)) {
+            AR(oA + e * em + u) = c;
+            AR(oV + e * k + j) = (uint8_t)(u == e);
+            u++;
+          } else {
+            AR(oV + e * k + j) = c;
+          }
+        }
+        AR(oP + e) = (uint8_t)e;
+      }
+      for (int i = 0; i < n; i++) {  // sort_system :28-40
+        int mx = i;
+        for (int j = i + 1; j < n; j++)
+          if (AR(oA + AR(oP + mx) * em + i) < AR(oA + AR(oP + j) * em + i)) mx = j;
+        uint8_t t = AR(oP + i); AR(oP + i) = AR(oP + mx); AR(oP + mx) = t;
+      }
+      for (int i = 0; i < n - 1; i++) {  // elimination :54-70
+        const int pi = AR(oP + i);
+        const uint32_t piv = AR(oA + pi * em + i);
+        if (!piv) continue;  // inv(0) = 0: every term is 0, nothing changes
+        const uint32_t lip = 255u - LOG[piv];
+        for (int kk = i + 1; kk < n; kk++) {
+          const int pk = AR(oP + kk);
+          const uint32_t a = AR(oA + pk * em + i);
+          if (!a) continue;
+          const uint32_t lt = LOG[EXP[LOG[a] + lip]];
+          for (int u = 0; u < n; u++) {
+            uint32_t x = AR(oA + pi * em + u);
+            if (x) AR(oA + pk * em + u) ^= EXP[lt + LOG[x]];
+          }
+          for (int j = 0; j < k; j++) {
+            uint32_t x = AR(oV + pi * k + j);
+            if (x) AR(oV + pk * k + j) ^= EXP[lt + LOG[x]];
+          }
         }
       }
-    }
-    bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
-    for (int i = 0; i < n; i++) ub |= AR(oA + AR(oP + i) * em + i) == 0;
-    if (ub) {
-      h[0] = FECGPU_BLOCK_REF_UB;
-      h[1] = 0;
-      continue;
-    }
-    for (int i = n - 1; i >= 0; i--) {  // back substitution :71-114; X_i stored over V[P[i]]
-      const int pi = AR(oP + i);
-      const uint32_t li = 255u - LOG[AR(oA + pi * em + i)];
-      for (int j = 0; j < k; j++) {
-        uint32_t v = AR(oV + pi * k + j);
-        for (int u = i + 1; u < n; u++) {
-          uint32_t a = AR(oA + pi * em + u);
-          uint32_t x = AR(oV + AR(oP + u) * k + j);
-          if (a && x) v ^= EXP[LOG[a] + LOG[x]];
-        }
-        AR(oV + pi * k + j) = v ? EXP[LOG[v] + li] : 0;
+      bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
+      for (int i = 0; i < n; i++) ub |= AR(oA + AR(oP + i) * em + i) == 0;
+      if (ub) {
+        h[0] = FECGPU_BLOCK_REF_UB;
+        h[1] = 0;
+        break;
       }
-      for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && AR(oA + pi * em + u) != 0;
+      for (int i = n - 1; i >= 0; i--) {  // back substitution :71-114; X_i stored over V[P[i]]
+        const int pi = AR(oP + i);
+        const uint32_t li = 255u - LOG[AR(oA + pi * em + i)];
+        for (int j = 0; j < k; j++) {
+          uint32_t v = AR(oV + pi * k + j);
+          for (int u = i + 1; u < n; u++) {
+            uint32_t a = AR(oA + pi * em + u);
+            uint32_t x = AR(oV + AR(oP + u) * k + j);
+            if (a && x) v ^= EXP[LOG[a] + LOG[x]];
+          }
+          AR(oV + pi * k + j) = v ? EXP[LOG[v] + li] : 0;
+        }
+        for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && AR(oA + pi * em + u) != 0;
+      }
+      for (int i = 0; i < n; i++) {
+        const int pi = AR(oP + i);
+        for (int j = 0; j < k; j++) h[L.off_D + i * k + j] = AR(oV + pi * k + j);
+        h[L.off_nz + i] = 0;
+        h[L.off_unk + i] = AR(oU + i);
+        h[L.off_sel + i] = AR(oS + i);
+      }
+      {
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | AR(oS + u++)) : (uint8_t)j;
+      }
+      h[0] = FECGPU_BLOCK_RECOVERED;
+      h[1] = (uint8_t)n;
+      } while (0);
+    __syncthreads();
+    const uint32_t nrows = nblocks - base < 64 ? (uint32_t)(nblocks - base) : 64u;
+    const uint32_t rdw = L.stride / 4, odw = orow / 4;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
+    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(obase);
+    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
+      const uint32_t row = x / rdw;
+      dst[x] = srcw[row * odw + (x - row * rdw)];
     }
-    for (int i = 0; i < n; i++) {
-      const int pi = AR(oP + i);
-      for (int j = 0; j < k; j++) h[L.off_D + i * k + j] = AR(oV + pi * k + j);
-      h[L.off_nz + i] = 0;
-      h[L.off_unk + i] = AR(oU + i);
-      h[L.off_sel + i] = AR(oS + i);
-    }
-    {
-      int u = 0;
-      for (int j = 0; j < k; j++)
-        h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | AR(oS + u++)) : (uint8_t)j;
-    }
-    h[0] = FECGPU_BLOCK_RECOVERED;
-    h[1] = (uint8_t)n;
+    __syncthreads();
   }
 #undef AR
 }
@@ -565,6 +587,30 @@ __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
   }
 }
 
+// per-block decode record in LDS (layout shared with gen_bitslice.py): 16 output addresses |
+// ws non-zero-flag address @128 | rt @136 | non-zero flags @144 (written by the asm body)
+constexpr int kDecRec = 160, kDecRecNzPtr = 16, kDecRecRt = 34, kDecRecNz = 144;
+
+// The reference's zero/undetermined rule (rlc_fec_scheme_gf256.c:98-101, 218-236) for one block,
+// given its non-zero flags: unknown u is inserted iff it is non-zero and every unknown its row
+// still references after elimination is itself determined.  Returns the recovered source masks.
+__device__ __forceinline__ void rlc_finalize_block(const uint8_t *h, const WsLayout &L, const uint8_t *nzf,
+                                                   uint64_t &m0, uint64_t &m1) {
+  m0 = m1 = 0;
+  const int n = h[1];
+  uint64_t det0 = 0, det1 = 0;  // determined unknowns, indexed by u
+  for (int u = n - 1; u >= 0; u--) {
+    bool ok = nzf[u] != 0;
+    for (int v = u + 1; v < n && ok; v++)
+      if (h[L.off_dep + u * L.em + v]) ok = v < 64 ? ((det0 >> v) & 1) : ((det1 >> (v - 64)) & 1);
+    if (ok) {
+      if (u < 64) det0 |= 1ull << u; else det1 |= 1ull << (u - 64);
+      const int j = h[L.off_unk + u];
+      if (j < 64) m0 |= 1ull << j; else m1 |= 1ull << (j - 64);
+    }
+  }
+}
+
 __global__ void k_rlc_finalize(uint64_t nblocks, int k, int r, const uint8_t *ws, uint8_t *status,
                                uint64_t *recovered) {
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
@@ -573,20 +619,7 @@ __global__ void k_rlc_finalize(uint64_t nblocks, int k, int r, const uint8_t *ws
     const uint8_t *h = ws + b * (uint64_t)L.stride;
     uint64_t m0 = 0, m1 = 0;
     const int st = h[0];
-    if (st == FECGPU_BLOCK_RECOVERED) {
-      const int n = h[1];
-      uint64_t det0 = 0, det1 = 0;  // determined unknowns, indexed by u
-      for (int u = n - 1; u >= 0; u--) {
-        bool ok = h[L.off_nz + u] != 0;  // symbol_is_zero -> undetermined (:98-101)
-        for (int v = u + 1; v < n && ok; v++)
-          if (h[L.off_dep + u * L.em + v]) ok = v < 64 ? ((det0 >> v) & 1) : ((det1 >> (v - 64)) & 1);
-        if (ok) {
-          if (u < 64) det0 |= 1ull << u; else det1 |= 1ull << (u - 64);
-          int j = h[L.off_unk + u];
-          if (j < 64) m0 |= 1ull << j; else m1 |= 1ull << (j - 64);
-        }
-      }
-    }
+    if (st == FECGPU_BLOCK_RECOVERED) rlc_finalize_block(h, L, h + L.off_nz, m0, m1);
     status[b] = (uint8_t)st;
     recovered[2 * b] = m0;
     recovered[2 * b + 1] = m1;
@@ -677,7 +710,6 @@ __host__ __device__ static inline int bs_group(int RT, int k, int per_j_bytes, i
   return g;
 }
 
-constexpr int kDecRec = 144;  // per-block record: 16 output addresses, nz base, rt (see gen_bitslice.py)
 
 template <int RT, int VEC>
 __global__ __launch_bounds__(64) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
@@ -716,62 +748,144 @@ __global__ __launch_bounds__(64) void k_rlc_encode_bs(const uint8_t *__restrict_
   }
 }
 
+// Setup reads the workspace for all of a group's blocks at once (lanes spread over (block, input)
+// pairs), so each group pays one HBM round trip before its data pass, not one per block.
+// status != nullptr: single pass (e <= RT for every block, r0 == 0) -- the zero/undetermined
+// rule runs here from LDS (non-zero flags from the asm body, dependency masks and unknown ids
+// staged during setup) and status[]/recovered[] are written for every block of the group.
+// Otherwise the flags are OR-ed into the workspace for k_rlc_finalize.
+struct RecoverLds {
+  uint8_t *coef;     // [G][k][16] coefficient rows (u fastest)
+  uint64_t *intab;   // [G][k] input symbol addresses
+  uint8_t *rec;      // [G] x kDecRec records read by the asm body
+  uint8_t *gid;      // [64] compacted slot -> block in group
+  uint8_t *ecnt;     // [64] unknowns of the block in this pass
+  uint8_t *unk;      // [G][16] unknown -> source index (fused finalize)
+  uint32_t *depm;    // [G][16] unknowns row u still references after elimination (fused finalize)
+  __host__ __device__ static size_t bytes(int G, int k) {
+    return (size_t)G * ((size_t)k * 24 + kDecRec + 16 + 64) + 128;
+  }
+  __device__ RecoverLds(uint8_t *l, int G, int k) {
+    coef = l;
+    intab = reinterpret_cast<uint64_t *>(l + (size_t)G * k * 16);
+    rec = l + (size_t)G * k * 24;
+    depm = reinterpret_cast<uint32_t *>(rec + (size_t)G * kDecRec);
+    unk = reinterpret_cast<uint8_t *>(depm + G * 16);
+    gid = unk + G * 16;
+    ecnt = gid + 64;
+  }
+};
+
 template <int RT, int VEC>
 __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
-                                                       int chunk_bytes, uint8_t *ws, int r0, int G) {
+                                                       int chunk_bytes, uint8_t *ws, int r0, int G,
+                                                       uint8_t *status, uint64_t *recovered) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
-  // LDS: coef rows [G][k][16] | input addresses [G][k] x 8 B | records [G] x kDecRec
-  uint8_t *coef = lds;
-  uint64_t *intab = reinterpret_cast<uint64_t *>(lds + (size_t)G * k * 16);
-  uint8_t *rec = lds + (size_t)G * k * 24;
+  RecoverLds S(lds, G, k);
   for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
     bool act = false;
+    int st = FECGPU_BLOCK_NOTHING, e = 0;
     if (lane < G && g0 + lane < nblocks) {
       const uint8_t *h = ws + (g0 + lane) * (uint64_t)WL.stride;
-      act = h[0] == FECGPU_BLOCK_RECOVERED && h[1] > r0;
+      st = h[0];
+      e = h[1];
+      act = st == FECGPU_BLOCK_RECOVERED && e > r0;
     }
     const uint64_t am = __ballot(act);
     const int nact = __popcll(am);
     __syncthreads();
-    for (uint64_t m = am; m; m &= m - 1) {  // compacted slot t <- block g0 + g
-      const int g = __ffsll((long long)m) - 1;
-      const int t = __popcll(am & ((1ull << g) - 1));
-      const uint64_t b = g0 + g;
-      uint8_t *h = ws + b * (uint64_t)WL.stride;
-      const int e = h[1];
-      const int rt = e - r0 < RT ? e - r0 : RT;
-      for (int x = lane; x < k * 16; x += 64) {
-        const int j = x >> 4, u = x & 15;
-        coef[(size_t)t * k * 16 + x] = u < rt ? h[WL.off_D + (r0 + u) * k + j] : 0;
+    if (act) {
+      const int t = __popcll(am & ((1ull << lane) - 1));
+      S.gid[t] = (uint8_t)lane;
+      S.ecnt[t] = (uint8_t)(e - r0 < RT ? e - r0 : RT);
+    }
+    __syncthreads();
+    // coefficient rows and input addresses, one (block, input j) pair per lane
+    for (int x = lane; x < nact * k; x += 64) {
+      const int t = x / k, j = x - t * k;
+      const uint64_t b = g0 + S.gid[t];
+      const int rt = S.ecnt[t];
+      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      uint8_t c[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) c[u] = (u < RT && u < rt) ? h[WL.off_D + (r0 + u) * k + j] : 0;
+      uint4 cv;
+      cv.x = c[0] | c[1] << 8 | c[2] << 16 | (uint32_t)c[3] << 24;
+      cv.y = c[4] | c[5] << 8 | c[6] << 16 | (uint32_t)c[7] << 24;
+      cv.z = c[8] | c[9] << 8 | c[10] << 16 | (uint32_t)c[11] << 24;
+      cv.w = c[12] | c[13] << 8 | c[14] << 16 | (uint32_t)c[15] << 24;
+      *reinterpret_cast<uint4 *>(S.coef + (size_t)x * 16) = cv;
+      const uint32_t sl = h[WL.off_slot + j];
+      const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
+                                     : src + (b * (uint64_t)k + sl) * (uint64_t)L;
+      S.intab[x] = (uint64_t)(uintptr_t)p;
+    }
+    // records: output addresses, rt, flags; for the fused finalize the dependency masks
+    for (int x = lane; x < nact * 16; x += 64) {
+      const int t = x >> 4, u = x & 15;
+      const uint64_t b = g0 + S.gid[t];
+      const int rt = S.ecnt[t];
+      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      uint8_t *rc = S.rec + (size_t)t * kDecRec;
+      rc[kDecRecNz + u] = 0;
+      if (u < rt) {
+        const int j = h[WL.off_unk + r0 + u];
+        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(src + (b * (uint64_t)k + j) * (uint64_t)L);
+        if (status) {
+          uint32_t m = 0;
+          for (int v = u + 1; v < rt; v++) m |= (uint32_t)(h[WL.off_dep + u * WL.em + v] != 0) << v;
+          S.unk[x] = (uint8_t)j;
+          S.depm[x] = m;
+        }
       }
-      for (int j = lane; j < k; j += 64) {
-        const uint32_t sl = h[WL.off_slot + j];
-        const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
-                                       : src + (b * (uint64_t)k + sl) * (uint64_t)L;
-        intab[(size_t)t * k + j] = (uint64_t)(uintptr_t)p;
-      }
-      uint8_t *rc = rec + (size_t)t * kDecRec;
-      if (lane < rt)
-        reinterpret_cast<uint64_t *>(rc)[lane] =
-            (uint64_t)(uintptr_t)(src + (b * (uint64_t)k + h[WL.off_unk + r0 + lane]) * (uint64_t)L);
-      if (lane == 0) {
-        reinterpret_cast<uint64_t *>(rc)[16] = (uint64_t)(uintptr_t)(h + WL.off_nz + r0);
-        reinterpret_cast<uint32_t *>(rc)[34] = (uint32_t)rt;
+      if (u == 0) {
+        reinterpret_cast<uint64_t *>(rc)[kDecRecNzPtr] = (uint64_t)(uintptr_t)(h + WL.off_nz + r0);
+        reinterpret_cast<uint32_t *>(rc)[kDecRecRt] = (uint32_t)rt;
       }
     }
     __syncthreads();
-    if (!nact) continue;
-    for (int ch = 0; ch < nchunks; ch++) {
-      const int c0 = ch * chunk_bytes;
-      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-      BsLanes<VEC> ln(lane, cb);
+    if (nact) {
+      for (int ch = 0; ch < nchunks; ch++) {
+        const int c0 = ch * chunk_bytes;
+        const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+        BsLanes<VEC> ln(lane, cb);
 #pragma unroll
-      for (int q = 0; q < BsLanes<VEC>::NP; q++) ln.off[q] += (uint32_t)c0;  // chunk offset
-      if (lane < ln.active)
-        bs_dec_call<RT, VEC>(lds_addr(intab), lds_addr(rec), (uint32_t)(nact * k), (uint32_t)k, lds_addr(coef), ln);
+        for (int q = 0; q < BsLanes<VEC>::NP; q++) ln.off[q] += (uint32_t)c0;  // chunk offset
+        if (lane < ln.active)
+          bs_dec_call<RT, VEC>(lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), (uint32_t)k,
+                               lds_addr(S.coef), ln);
+      }
+    }
+    __syncthreads();
+    if (status) {
+      if (lane < G && g0 + lane < nblocks) {
+        const uint64_t b = g0 + lane;
+        uint64_t m0 = 0, m1 = 0;
+        if (act) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
+          const int t = __popcll(am & ((1ull << lane) - 1));
+          const uint8_t *nzf = S.rec + (size_t)t * kDecRec + kDecRecNz;
+          uint32_t det = 0;
+          for (int u = e - 1; u >= 0; u--) {
+            if (nzf[u] && (S.depm[t * 16 + u] & ~det) == 0) {
+              det |= 1u << u;
+              const int j = S.unk[t * 16 + u];
+              if (j < 64) m0 |= 1ull << j; else m1 |= 1ull << (j - 64);
+            }
+          }
+        }
+        status[b] = (uint8_t)st;
+        recovered[2 * b] = m0;
+        recovered[2 * b + 1] = m1;
+      }
+    } else {
+      for (int x = lane; x < nact * 16; x += 64) {
+        const uint8_t *rc = S.rec + (size_t)(x >> 4) * kDecRec;
+        if (rc[kDecRecNz + (x & 15)])
+          reinterpret_cast<uint8_t *>(reinterpret_cast<const uint64_t *>(rc)[kDecRecNzPtr])[x & 15] = 1;
+      }
     }
   }
 }
@@ -798,12 +912,12 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
 
 template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
-                              uint8_t *ws, int r0, hipStream_t s) {
-  const int G = bs_group(RT, k, 24, kDecRec);
-  const size_t lds = (size_t)G * ((size_t)k * 24 + kDecRec);
+                              uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s) {
+  const int G = bs_group(RT, k, 24, kDecRec + 80);
+  const size_t lds = RecoverLds::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G);
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered);
 }
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
@@ -1082,8 +1196,8 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   if (rc || nblocks == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
-  const size_t lane_lds = 768 + 64 * (size_t)lane_arena_bytes(k, r);
-  if (lane_lds <= 48 * 1024) {
+  const size_t lane_lds = plan_lane_lds(k, r);
+  if (lane_lds <= 64 * 1024) {
     const uint64_t groups = (nblocks + 63) / 64;
     hipLaunchKernelGGL(k_rlc_plan_lane, dim3(grid_for(groups)), dim3(64), lane_lds, s, nblocks, (int)k,
                        (int)r, fbn_base, fbn, src_present, rep_present, ws);
@@ -1103,16 +1217,27 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   return FECGPU_OK;
 }
 
+static int launch_finalize(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *status, uint64_t *recovered,
+                           const uint8_t *ws, hipStream_t s) {
+  const uint32_t fgrid = (uint32_t)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
+  hipLaunchKernelGGL(k_rlc_finalize, dim3(fgrid), dim3(256), 0, s, nblocks, (int)k, (int)r, ws, status, recovered);
+  HIPCHK(hipGetLastError());
+  return FECGPU_OK;
+}
+
 int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
-                            uint32_t symbol_size, void *workspace, size_t workspace_bytes, void *stream) {
+                            uint32_t symbol_size, uint8_t *status, uint64_t *recovered, void *workspace,
+                            size_t workspace_bytes, void *stream) {
   static const uint64_t dummy = 0;
-  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, &dummy, &dummy, &dummy, &dummy, workspace,
+  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, &dummy, &dummy, status, recovered, workspace,
                        workspace_bytes);
-  if (rc || nblocks == 0 || r == 0) return rc;
+  if (rc || nblocks == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const WsLayout L = ws_layout(k, r);
-  const int rt = pick_rt(L.em);
+  // decode passes: the smallest tile covering e_max (one pass, finalize fused) up to 16 unknowns
+  const int rt = L.em <= 1 ? 1 : L.em <= 2 ? 2 : L.em <= 4 ? 4 : L.em <= 8 ? 8 : 16;
+  if (r == 0) return launch_finalize(nblocks, k, r, status, recovered, ws, s);
   if (use_perm_path()) {
     const int Ldw = (int)(symbol_size / 4);
     const DataCfg cfg = pick_data_cfg(Ldw);
@@ -1120,28 +1245,17 @@ int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32
       FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
                       cfg, ws, r0, s)
     }
-  } else {
-    const BsCfg cfg = pick_bs_cfg((int)symbol_size);
-    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-      FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
-                      (int)symbol_size, cfg, ws, r0, s)
-    }
+    HIPCHK(hipGetLastError());
+    return launch_finalize(nblocks, k, r, status, recovered, ws, s);
+  }
+  const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+  const bool fused = (int)L.em <= rt;  // one pass covers every unknown of every block
+  for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
+    FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+                    (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s)
   }
   HIPCHK(hipGetLastError());
-  return FECGPU_OK;
-}
-
-int fecgpu_rlc_decode_finish(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *status, uint64_t *recovered,
-                             const void *workspace, size_t workspace_bytes, void *stream) {
-  static const uint32_t dummy = 0;
-  int rc = decode_args(&dummy, &dummy, nblocks, k, r, 4, &dummy, &dummy, status, recovered, (void *)workspace,
-                       workspace_bytes);
-  if (rc || nblocks == 0) return rc;
-  const uint32_t fgrid = (uint32_t)((nblocks + 255) / 256 < 65536 ? (nblocks + 255) / 256 : 65536);
-  hipLaunchKernelGGL(k_rlc_finalize, dim3(fgrid), dim3(256), 0, (hipStream_t)stream, nblocks, (int)k, (int)r,
-                     (const uint8_t *)workspace, status, recovered);
-  HIPCHK(hipGetLastError());
-  return FECGPU_OK;
+  return fused ? FECGPU_OK : launch_finalize(nblocks, k, r, status, recovered, ws, s);
 }
 
 int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
@@ -1154,9 +1268,8 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   if ((rc = fecgpu_rlc_decode_plan(nblocks, k, r, fbn_base, fbn, src_present, rep_present, workspace,
                                    workspace_bytes, stream)))
     return rc;
-  if ((rc = fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, workspace, workspace_bytes, stream)))
-    return rc;
-  if ((rc = fecgpu_rlc_decode_finish(nblocks, k, r, status, recovered, workspace, workspace_bytes, stream)))
+  if ((rc = fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, status, recovered, workspace,
+                                    workspace_bytes, stream)))
     return rc;
   g_stats[2]++;
   g_stats[3] += nblocks;

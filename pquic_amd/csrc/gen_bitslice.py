@@ -268,7 +268,7 @@ def body(mode: str, RT: int, VEC: int, P: int):
                     f"v_readfirstlane_b32 s{S_CUR + 1}, v{TMP[1]}"]
         for q in range(NP):
             out += [f"s_mov_b64 exec, %[vm{q}]",
-                    f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]"]
+                    f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
         out.append(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
         if mode == "enc":
             out += [f"s_add_u32 s{S_CUR}, s{S_CUR}, %[L]", f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, 0"]
@@ -328,10 +328,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
     else:
-        a(f"ds_read_b128 v[{TMP[0]}:{TMP[3]}], v{OUTPTR} offset:128")
+        a(f"ds_read_b32 v{TMP[2]}, v{OUTPTR} offset:{DEC_REC_RT}")
         a("s_waitcnt lgkmcnt(0)")
-        a(f"v_readfirstlane_b32 s{S_NZ}, v{TMP[0]}")
-        a(f"v_readfirstlane_b32 s{S_NZ + 1}, v{TMP[1]}")
         a(f"v_readfirstlane_b32 s{S_RT}, v{TMP[2]}")
     for i in range(RT):
         accs = [acc_base + 8 * i + w for w in range(8)]
@@ -345,17 +343,16 @@ def body(mode: str, RT: int, VEC: int, P: int):
             a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[5]}, v{accs[6]}")
             a(f"v_or_b32 v{TMP[0]}, v{TMP[0]}, v{accs[7]}")
             a(f"v_cmp_ne_u32 vcc, 0, v{TMP[0]}")
-            a(f"v_mov_b32 v{TMP[0]}, 0")
             a(f"v_mov_b32 v{TMP[1]}, 1")
             a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
-            a(f"global_store_byte v{TMP[0]}, v{TMP[1]}, s[{S_NZ}:{S_NZ + 1}] offset:{i}")
+            a(f"ds_write_b8 v{OUTPTR}, v{TMP[1]} offset:{DEC_REC_NZ + i}")  # non-zero flag (LDS)
             a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
             a("s_waitcnt lgkmcnt(0)")
             a(f"v_readfirstlane_b32 s{S_O2}, v{TMP[2]}")
             a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{TMP[3]}")
         for q in range(NP):
             a(f"s_mov_b64 exec, %[vm{q}]")
-            a(f"{st} %[off{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]")
+            a(f"{st} %[off{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
         a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
         if mode == "enc":
             a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
@@ -370,13 +367,20 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"v_add_u32 v{OUTPTR}, {DEC_REC_BYTES}, v{OUTPTR}")
     a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
     a(".Lexit_%=:")
+    a("s_waitcnt lgkmcnt(0)")
     a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
     a(f"s_mov_b32 m0, s{S_SAVEM0}")
     return L, acc_base + 8 * RT
 
 
 def cstring(lines):
-    return "\n".join(f'      "{ln}\\n"' for ln in lines)
+    # cache-policy suffixes of the symbol loads/stores come from FEC_LD_POL / FEC_ST_POL (C string
+    # macros, defaults below) so a build can pick them without regenerating
+    out = []
+    for ln in lines:
+        ln = ln.replace("@LDPOL@", '" FEC_LD_POL "').replace("@STPOL@", '" FEC_ST_POL "')
+        out.append(f'      "{ln}\\n"')
+    return "\n".join(out)
 
 
 def emit_function(mode, RT, VEC, P):
@@ -402,7 +406,9 @@ def emit_function(mode, RT, VEC, P):
     return "\n".join(out), top
 
 
-DEC_REC_BYTES = 144  # per-block decode record in LDS: 16 x 8 B output addresses, nz base, rt
+DEC_REC_BYTES = 160  # per-block decode record in LDS: 16 x 8 B output addresses | rt @136 | nz flags @144
+DEC_REC_RT = 136
+DEC_REC_NZ = 144
 
 
 def data_base(mode: str) -> int:
@@ -429,6 +435,12 @@ def main():
              "#include <stdint.h>",
              "",
              f"#define FEC_BS_CASE_BYTES {CASE_BYTES}",
+             "#ifndef FEC_LD_POL",
+             "#define FEC_LD_POL \" nt\"  // symbol loads: read once, stream past the caches",
+             "#endif",
+             "#ifndef FEC_ST_POL",
+             "#define FEC_ST_POL \" nt\"  // repair / recovered symbol stores",
+             "#endif",
              "",
              "// Shared 256-case table: case c applies  acc[v0..v7] ^= TL[.] ^ TH[.]  for coefficient c.",
              "// It lives in the body of a never-launched kernel (HIP drops module-level asm in the",

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "lib", "libpquic_fec.so")
+# PQUIC_AMD_LIB selects another in-tree build of the same library (A/B experiments, tools/)
+LIB_PATH = os.environ.get("PQUIC_AMD_LIB") or os.path.join(PKG, "lib", "libpquic_fec.so")
 
 OK, ERR_INVALID, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
 BLOCK_RECOVERED, BLOCK_NOTHING, BLOCK_REF_UB = 0, 1, 2
@@ -46,8 +47,7 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
     L.fecgpu_rlc_decode_plan.argtypes = [u64, u32, u32, u32, v, v, v, v, sz, v]
-    L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, sz, v]
-    L.fecgpu_rlc_decode_finish.argtypes = [u64, u32, u32, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
     L.fecgpu_host_ctx_create.argtypes = [C.c_int, C.c_int, sz]
@@ -140,8 +140,8 @@ class Engine:
 
     def rlc_decode_stages(self, src, rep, src_present, rep_present, status, recovered, k, r, L, nblocks,
                           workspace, fbn_base=0, stream=None, events=None):
-        """fecgpu_rlc_decode as its three stages; events[i] (if given) recorded before stage i
-        and events[3] after the last, on the launch stream."""
+        """fecgpu_rlc_decode as its two stages (plan, apply); events[i] (if given) recorded before
+        stage i and events[2] after the last, on the launch stream."""
         st = self._stream(stream)
         torch_stream = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         rec = (lambda i: events[i].record(torch_stream)) if events else (lambda i: None)
@@ -150,13 +150,10 @@ class Engine:
                                                     _addr(rep_present), _addr(workspace), workspace.numel(), st),
                     "fecgpu_rlc_decode_plan")
         rec(1)
-        self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(workspace),
-                                                     workspace.numel(), st), "fecgpu_rlc_decode_apply")
+        self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
+                                                     _addr(recovered), _addr(workspace), workspace.numel(), st),
+                    "fecgpu_rlc_decode_apply")
         rec(2)
-        self._check(self.lib.fecgpu_rlc_decode_finish(nblocks, k, r, _addr(status), _addr(recovered),
-                                                      _addr(workspace), workspace.numel(), st),
-                    "fecgpu_rlc_decode_finish")
-        rec(3)
         return status, recovered
 
     def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,

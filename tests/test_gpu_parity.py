@@ -181,7 +181,8 @@ def test_decode_golden(eng):
 
 @pytest.mark.parametrize("k,r,L,nb,emax", [(4, 1, 1200, 300, 1), (16, 4, 1200, 500, 4), (32, 8, 1200, 200, 8),
                                            (8, 8, 40, 600, 8), (64, 16, 9000, 12, 16), (100, 30, 64, 40, 30),
-                                           (128, 128, 8, 6, 128), (10, 3, 4, 200, 3)])
+                                           (128, 128, 8, 6, 128), (10, 3, 4, 200, 3), (12, 6, 2100, 300, 6),
+                                           (40, 20, 4100, 30, 20)])
 def test_decode_vs_oracle(eng, oracle, k, r, L, nb, emax):
     rng = np.random.default_rng(k * 131 + r)
     src_h = synth_bytes(nb * k * L, 77 + k).reshape(nb, k, L)
