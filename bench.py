@@ -23,6 +23,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E 8.0 TB/s)
+# measured on MI355X with tools/microbench/hbm_ceiling_probe.hip (profiles/r01_hbm_ceiling_probe.log):
+# best plain-streaming rates for a copy (1:1) and for the encode's 4:1 read:write mix
+MEASURED_COPY_GBS = 5731.0
+MEASURED_MIX41_GBS = 5617.0
 METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 
 
@@ -58,17 +62,104 @@ def load_traffic(kernel_tag: str):
 
 
 def make_erasures(torch, nb, k, e, seed, dev):
+    """e distinct random source erasures per block; presence masks as [nb, 2] int64 (128 bits)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     keys = torch.rand((nb, k), generator=g)
     miss = keys.argsort(dim=1)[:, :e]
-    pres = torch.ones((nb, k), dtype=torch.bool)
+    pres = torch.ones((nb, 128), dtype=torch.bool)
+    pres[:, k:] = False
     pres.scatter_(1, miss, False)
-    w = 1 << torch.arange(min(k, 63), dtype=torch.int64)
     sp = torch.zeros((nb, 2), dtype=torch.int64)
-    sp[:, 0] = (pres[:, : min(k, 63)].to(torch.int64) * w).sum(1)
-    if k > 63:
-        raise SystemExit("bench erasure masks support k <= 63")
+    for w in range(2):
+        bits = pres[:, 64 * w: 64 * w + 64].to(torch.int64)
+        lo = (bits[:, :63] << torch.arange(63, dtype=torch.int64)).sum(1)
+        sp[:, w] = lo | (bits[:, 63] << 63)  # bit 63 wraps to the sign bit, as a uint64 would
     return sp.to(dev), miss
+
+
+def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
+    """One BASELINE config as a side leg: RLC encode, then decode with e random erasures,
+    device-resident, per-kernel event timing; decode correctness gated on the output."""
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
+    eng.synth_fill(src, src.numel(), seed, 0)
+    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
+    work = src.clone()
+    sp, miss = make_erasures(torch, nb, k, e, 3, dev)
+    idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
+    work.view(nb * k, L)[idx] = 0xA5
+    rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
+    rp[:, 0] = (1 << r) - 1 if r < 64 else -1
+    st = torch.empty(nb, dtype=torch.uint8, device=dev)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+    ws = eng.alloc_workspace(nb, k, r)
+    stream = torch.cuda.current_stream(dev)
+    eng.rlc_encode(src, rep, k, r, L)
+    eng.rlc_decode(work, rep, sp, rp, st, rec, k, r, L, workspace=ws)
+    torch.cuda.synchronize()
+    ok = st == 0
+    for c0 in range(0, nb, 1 << 14):
+        c1 = min(nb, c0 + (1 << 14))
+        okc = ok[c0:c1]
+        assert bool((work[c0:c1][okc] == src[c0:c1][okc]).all()), f"k{k} r{r} decode did not restore the sources"
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t = [0.0, 0.0, 0.0]
+    for _ in range(reps):
+        ev[0].record(stream)
+        eng.rlc_encode(src, rep, k, r, L)
+        eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, events=ev[1:])
+        torch.cuda.synchronize()
+        for i in range(3):
+            t[i] += ev[i].elapsed_time(ev[i + 1]) / reps
+    n_rec = int(ok.sum())
+    enc_b, app_b = (k + r) * L * nb, (k + e) * L * n_rec
+    del src, rep, work, ws
+    torch.cuda.empty_cache()
+    pay = nb * k * L / 2**30
+    return {"blocks": nb, "k": k, "r": r, "L": L, "erasures": e, "encode_ms": round(t[0], 3),
+            "plan_ms": round(t[1], 3), "apply_ms": round(t[2], 3),
+            "payload_GiB_s": round(pay / ((t[0] + t[1] + t[2]) * 1e-3), 2),
+            "encode_GB_s": round(enc_b / (t[0] * 1e-3) / 1e9, 1),
+            "encode_hbm_frac": round(enc_b / (t[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "apply_GB_s": round(app_b / (t[2] * 1e-3) / 1e9, 1),
+            "recovered_blocks": n_rec, "ref_ub_blocks": int((st == 2).sum())}
+
+
+def xor_leg(torch, eng, dev, k, L, nb, reps=3):
+    """XOR scheme (configs[0]'s scheme at GPU scale): encode, then recover one erasure per block."""
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
+    eng.synth_fill(src, src.numel(), 0x5EEDF3C0, 0)
+    rep = torch.empty((nb, 1, L), dtype=torch.uint8, device=dev)
+    work = src.clone()
+    sp, miss = make_erasures(torch, nb, k, 1, 4, dev)
+    idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
+    work.view(nb * k, L)[idx] = 0xA5
+    rp = torch.ones((nb, 2), dtype=torch.int64, device=dev)
+    rp[:, 1] = 0
+    st = torch.empty(nb, dtype=torch.uint8, device=dev)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    eng.xor_encode(src, rep, k, L)
+    eng.xor_decode(work, rep, sp, rp, st, rec, k, L)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all()) and bool((work == src).all()), "xor decode did not restore the sources"
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    te = td = 0.0
+    for _ in range(reps):
+        ev[0].record(stream)
+        eng.xor_encode(src, rep, k, L)
+        ev[1].record(stream)
+        eng.xor_decode(work, rep, sp, rp, st, rec, k, L)
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        te += ev[0].elapsed_time(ev[1]) / reps
+        td += ev[1].elapsed_time(ev[2]) / reps
+    del src, rep, work
+    torch.cuda.empty_cache()
+    pay = nb * k * L / 2**30
+    return {"blocks": nb, "k": k, "L": L, "encode_ms": round(te, 3), "decode_ms": round(td, 3),
+            "payload_GiB_s": round(pay / ((te + td) * 1e-3), 2),
+            "encode_GB_s": round((k + 1) * L * nb / (te * 1e-3) / 1e9, 1),
+            "decode_GB_s": round((k + 1) * L * nb / (td * 1e-3) / 1e9, 1)}
 
 
 def cpu_baseline(args, nthreads):
@@ -278,6 +369,11 @@ def main():
                                      "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                                      "traffic": load_traffic("rlc_encode_k32_r8")}
         del s2, r2t
+        torch.cuda.empty_cache()
+        # configs[4]: jumbo 9000-B symbols, k = 64 r = 16, encode + decode of 16 erasures
+        legs["rlc_k64_r16_L9000"] = rlc_leg(torch, eng, dev, 64, 16, 9000, 1 << 16, 16)
+        # configs[0]'s XOR scheme (k = 4, r = 1) at GPU scale: encode + single-erasure recover
+        legs["xor_k4_r1"] = xor_leg(torch, eng, dev, 4, L, 1 << 22)
 
     if rank == 0:
         if enc_ms >= apply_ms:
@@ -288,7 +384,9 @@ def main():
             roof = {"bound": "hbm", "kernel": "k_rlc_recover_bs<4,16> (RLC decode apply k=16 e=4)",
                     "achieved": round(app_gbs, 1), "bytes_per_launch": app_bytes, "launch_ms": round(apply_ms, 4),
                     "traffic": load_traffic("rlc_decode_apply_k16_e4")}
-        roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4)})
+        roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),
+                     "measured_copy_peak": MEASURED_COPY_GBS,
+                     "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4)})
         cpu = None
         if not args.no_cpu and world == 1:
             nthreads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))

@@ -206,31 +206,57 @@ __global__ __launch_bounds__(64) void k_rlc_encode(const uint32_t *__restrict__ 
 // =============================================================================================
 // RLC decode: plan (coefficients only), recover (data), finalize (zero propagation)
 // =============================================================================================
-// One wave per block.  LDS: rows[em][kpad] (full coefficient rows of the selected repairs),
-// A[em][empad] (system over unknowns), V[em][kpad] (input combinations), X[em][kpad]
-// (solution), then unk[128], sel[128], perm[128] ints and a flag word.
+// GF(2^8)/0x11D log/exp tables (exp doubled so exp[log a + log b] needs no reduction).
+struct GfLogExp { uint8_t exp[512]; uint8_t log[256]; };
+
+constexpr GfLogExp make_logexp() {
+  GfLogExp t{};
+  uint32_t x = 1;
+  for (int i = 0; i < 255; i++) {
+    t.exp[i] = (uint8_t)x;
+    t.exp[i + 255] = (uint8_t)x;
+    t.log[x] = (uint8_t)i;
+    x = ((x << 1) ^ ((x & 0x80u) ? 0x11du : 0u)) & 0xffu;
+  }
+  t.exp[510] = t.exp[0];
+  t.exp[511] = t.exp[1];
+  t.log[0] = 0;
+  return t;
+}
+
+__constant__ GfLogExp kLogExp = make_logexp();
+
+// Wave-per-block plan (systems too large for a lane): one wave replays fec_recover's coefficient
+// work for one block with the lanes spread over matrix entries.  Elimination step i updates every
+// row below the pivot at once (rows are independent within a step: no re-pivoting), and back
+// substitution is column-oriented: once x_i is known it is folded into every row above.  GF
+// arithmetic is exact, so the solution equals the reference's row-by-row recurrence.
+// LDS: log/exp | A[em][empad] | V[em][kpad] | X[em][kpad] (coefficient rows before the solve)
+//      | unk, sel, perm int[128] | terms[128] | flag.
 struct PlanLds {
-  uint8_t *rows, *A, *V, *X;
+  uint8_t *exp, *log, *A, *V, *X, *terms;
   int *unk, *sel, *perm, *flag;
 };
 
 __host__ __device__ static inline size_t plan_lds_bytes(uint32_t k, uint32_t r) {
   const WsLayout L = ws_layout(k, r);
   const size_t kpad = pad16(k), empad = pad16(L.em);
-  return pad16((uint32_t)(L.em * kpad * 3 + L.em * empad)) + 4 * (128 * 3 + 4);
+  return 768 + pad16((uint32_t)(L.em * kpad * 2 + L.em * empad)) + 4 * (128 * 3) + 128 + 16;
 }
 
 __device__ __forceinline__ PlanLds plan_carve(uint8_t *lds, int em, int kpad, int empad) {
   PlanLds p;
-  p.rows = lds;
-  p.A = p.rows + em * kpad;
+  p.exp = lds;
+  p.log = lds + 512;
+  p.A = lds + 768;
   p.V = p.A + em * empad;
   p.X = p.V + em * kpad;
-  int *ints = reinterpret_cast<int *>(lds + pad16((uint32_t)(em * kpad * 3 + em * empad)));
+  int *ints = reinterpret_cast<int *>(lds + 768 + pad16((uint32_t)(em * kpad * 2 + em * empad)));
   p.unk = ints;
   p.sel = ints + 128;
   p.perm = ints + 256;
-  p.flag = ints + 384;
+  p.terms = reinterpret_cast<uint8_t *>(ints + 384);
+  p.flag = reinterpret_cast<int *>(p.terms + 128);
   return p;
 }
 
@@ -255,8 +281,11 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
   const int kpad = (int)pad16((uint32_t)k);
   const int empad = (int)pad16((uint32_t)em);
   const PlanLds P = plan_carve(lds, em, kpad, empad);
-  uint8_t *rows = P.rows, *A = P.A, *V = P.V, *X = P.X;
+  uint8_t *A = P.A, *V = P.V, *X = P.X, *EXP = P.exp, *LOG = P.log, *terms = P.terms;
   int *unk = P.unk, *sel = P.sel, *perm = P.perm;
+  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  // x * y with y != 0 given as log y
+  auto mul_l = [&](uint32_t x, uint32_t ly) -> uint32_t { return x ? EXP[LOG[x] + ly] : 0u; };
 
   for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
     uint8_t *h = ws + b * (uint64_t)L.stride;
@@ -279,7 +308,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
       if (bit128(m0, m1, j)) unk[rank128(m0, m1, j)] = j;
     for (int i = lane; i < r; i += 64)
       if (bit128(q0, q1, i)) {
-        int e = rank128(q0, q1, i);
+        const int e = rank128(q0, q1, i);
         if (e < n) sel[e] = i;
       }
     __syncthreads();
@@ -287,69 +316,84 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
     for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
       Tmt t;
       tmt_init(t, rlc_seed(f, (uint32_t)sel[e]));
-      for (int j = 0; j < k; j++) rows[e * kpad + j] = tmt_coef(t);
+      for (int j = 0; j < k; j++) X[e * kpad + j] = tmt_coef(t);
     }
     __syncthreads();
-    // A[e][u] = rows[e][unk[u]];  V[e][j] = present j ? rows[e][j] : (j == unk[e])
-    for (int e = 0; e < n; e++) {
-      for (int u = lane; u < n; u += 64) A[e * empad + u] = rows[e * kpad + unk[u]];
-      for (int j = lane; j < k; j += 64)
-        V[e * kpad + j] = bit128(m0, m1, j) ? (uint8_t)(unk[e] == j) : rows[e * kpad + j];
+    // A[e][u] = row_e[unk[u]];  V[e][j] = present j ? row_e[j] : (j == unk[e])
+    for (int x = lane; x < n * n; x += 64) {
+      const int e = x / n, u = x - e * n;
+      A[e * empad + u] = X[e * kpad + unk[u]];
     }
-    for (int i = lane; i < n; i += 64) perm[i] = i;
+    for (int x = lane; x < n * k; x += 64) {
+      const int e = x / k, j = x - e * k;
+      V[e * kpad + j] = bit128(m0, m1, j) ? (uint8_t)(unk[e] == j) : X[e * kpad + j];
+    }
     __syncthreads();
     // sort_system (:28-40): position i takes the first row with the largest A[.][i]
     if (lane == 0) {
+      for (int i = 0; i < n; i++) perm[i] = i;
       for (int i = 0; i < n; i++) {
         int mx = i;
         for (int j = i + 1; j < n; j++)
           if (A[perm[mx] * empad + i] < A[perm[j] * empad + i]) mx = j;
-        int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t;
+        const int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t;
       }
     }
     __syncthreads();
-    // forward elimination without re-pivoting (:54-70); inv(0) = 0 makes term 0
+    // forward elimination without re-pivoting (:54-70): row_pk -= (A[pk][i] / A[pi][i]) row_pi for all
+    // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below)
     for (int i = 0; i < n - 1; i++) {
       const int pi = perm[i];
-      const uint32_t ipiv = gf_inv(A[pi * empad + i]);
-      for (int kk = i + 1; kk < n; kk++) {
-        const int pk = perm[kk];
-        const uint32_t term = gf_mul(A[pk * empad + i], ipiv);
-        __syncthreads();
-        if (term) {
-          for (int u = lane; u < n; u += 64) A[pk * empad + u] ^= (uint8_t)gf_mul(term, A[pi * empad + u]);
-          for (int j = lane; j < k; j += 64) V[pk * kpad + j] ^= (uint8_t)gf_mul(term, V[pi * kpad + j]);
-        }
-        __syncthreads();
+      const uint32_t piv = A[pi * empad + i];
+      const int below = n - 1 - i;
+      for (int x = lane; x < below; x += 64) {  // log of the term, 255 = zero term
+        const uint32_t a = A[perm[i + 1 + x] * empad + i];
+        terms[x] = (piv && a) ? (uint8_t)EXP[LOG[a] + 255u - LOG[piv]] : (uint8_t)0;
       }
+      __syncthreads();
+      const int wa = n - i, w = wa + k;  // columns i..n-1 of A, then all of V
+      for (int x = lane; x < below * w; x += 64) {
+        const int rr = x / w, c = x - rr * w;
+        const uint32_t t = terms[rr];
+        if (!t) continue;
+        const int pk = perm[i + 1 + rr];
+        const uint32_t lt = LOG[t];
+        if (c < wa) A[pk * empad + i + c] ^= (uint8_t)mul_l(A[pi * empad + i + c], lt);
+        else V[pk * kpad + c - wa] ^= (uint8_t)mul_l(V[pi * kpad + c - wa], lt);
+      }
+      __syncthreads();
     }
     // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
-    if (lane == 0) {
-      int ub = 0;
-      for (int i = 0; i < n; i++) ub |= A[perm[i] * empad + i] == 0;
-      *P.flag = ub;
-    }
-    __syncthreads();
-    if (*P.flag) {
+    const bool zd = lane < n && A[perm[lane] * empad + lane] == 0;
+    bool ub = __any(zd);
+    for (int i = 64 + lane; i < n; i += 64) ub |= A[perm[i] * empad + i] == 0;
+    if (__any(ub)) {
       if (lane == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
       continue;
     }
-    // back substitution (:71-114) on the input-combination vectors
+    // back substitution (:71-114), column-oriented: x_i = V[pi] / A[pi][i], then V[pm] -= A[pm][i] x_i
     for (int i = n - 1; i >= 0; i--) {
       const int pi = perm[i];
-      const uint32_t ip = gf_inv(A[pi * empad + i]);
-      for (int j = lane; j < k; j += 64) {
-        uint32_t v = V[pi * kpad + j];
-        for (int u = i + 1; u < n; u++) {
-          uint32_t a = A[pi * empad + u];
-          if (a) v ^= gf_mul(a, X[u * kpad + j]);
-        }
-        X[i * kpad + j] = (uint8_t)gf_mul(v, ip);
+      const uint32_t li = 255u - LOG[A[pi * empad + i]];
+      for (int j = lane; j < k; j += 64) X[i * kpad + j] = (uint8_t)mul_l(V[pi * kpad + j], li);
+      __syncthreads();
+      for (int x = lane; x < i * k; x += 64) {
+        const int m = x / k, j = x - m * k;
+        const int pm = perm[m];
+        const uint32_t a = A[pm * empad + i];
+        const uint32_t xv = X[i * kpad + j];
+        if (a && xv) V[pm * kpad + j] ^= (uint8_t)EXP[LOG[a] + LOG[xv]];
       }
-      for (int u = lane; u < n; u += 64) h[L.off_dep + i * em + u] = (u > i) && A[pi * empad + u] != 0;
+      __syncthreads();
     }
-    for (int i = 0; i < n; i++)
-      for (int j = lane; j < k; j += 64) h[L.off_D + i * k + j] = X[i * kpad + j];
+    for (int x = lane; x < n * n; x += 64) {
+      const int i = x / n, u = x - i * n;
+      h[L.off_dep + i * em + u] = (u > i) && A[perm[i] * empad + u] != 0;
+    }
+    for (int x = lane; x < n * k; x += 64) {
+      const int i = x / k, j = x - i * k;
+      h[L.off_D + i * k + j] = X[i * kpad + j];
+    }
     for (int u = lane; u < n; u += 64) {
       h[L.off_nz + u] = 0;
       h[L.off_unk + u] = (uint8_t)unk[u];
@@ -368,24 +412,6 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
 // V: em x k, lists) lives in LDS byte-interleaved across the wave (element e of lane l at
 // e * 64 + l), so a wave-uniform step touches 64 consecutive bytes.
 // ---------------------------------------------------------------------------------------------
-struct GfLogExp { uint8_t exp[512]; uint8_t log[256]; };
-
-constexpr GfLogExp make_logexp() {
-  GfLogExp t{};
-  uint32_t x = 1;
-  for (int i = 0; i < 255; i++) {
-    t.exp[i] = (uint8_t)x;
-    t.exp[i + 255] = (uint8_t)x;
-    t.log[x] = (uint8_t)i;
-    x = ((x << 1) ^ ((x & 0x80u) ? 0x11du : 0u)) & 0xffu;
-  }
-  t.exp[510] = t.exp[0];
-  t.exp[511] = t.exp[1];
-  t.log[0] = 0;
-  return t;
-}
-
-__constant__ GfLogExp kLogExp = make_logexp();
 
 __host__ __device__ static inline uint32_t lane_arena_bytes(uint32_t k, uint32_t r) {
   const uint32_t em = k < r ? k : r;
@@ -638,6 +664,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 
 struct BsCfg { int vec, nchunks, chunk_bytes; };
 
+// Lane geometry for one chunk of cb bytes: pieces of VEC bytes; when cb is not a multiple of
+// VEC the last piece is pulled back to end at cb, overlapping its neighbour.  Overlapping lanes
+// compute and store identical bytes (the map is bytewise), so the result is unchanged.
 template <int VEC>
 struct BsLanes {
   static constexpr int NP = 32 / VEC;
@@ -645,13 +674,14 @@ struct BsLanes {
   uint64_t vm[NP];
   int active;
   __device__ __forceinline__ BsLanes(int lane, int cb) {
-    const int npieces = cb / VEC;
+    const int npieces = (cb + VEC - 1) / VEC;
     active = (npieces + NP - 1) / NP;
 #pragma unroll
     for (int q = 0; q < NP; q++) {
       const int piece = lane + active * q;
       const bool ok = lane < active && piece < npieces;
-      off[q] = ok ? (uint32_t)(piece * VEC) : 0u;
+      const int o = piece * VEC < cb - VEC ? piece * VEC : cb - VEC;
+      off[q] = ok ? (uint32_t)o : 0u;
       vm[q] = __ballot(ok);
     }
   }
@@ -711,36 +741,43 @@ __host__ __device__ static inline int bs_group(int RT, int k, int per_j_bytes, i
 }
 
 
+// W waves per workgroup can split the repairs of one group of blocks: wave w owns repairs
+// r0 + w*RT .. +RT, streaming the same source rows close together in time (L2 serves the
+// repeats).  Default W = 1 (see pick_enc_tile); W > 1 is kept for FECGPU_ENC_TILE experiments.
 template <int RT, int VEC>
-__global__ __launch_bounds__(64) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
-                                                      uint64_t nblocks, int k, int r, int L, int nchunks,
-                                                      int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
-                                                      int r0, int G) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
-  const int rt = r - r0 < RT ? r - r0 : RT;
+__global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                       int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
+                                                       int r0, int G) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
+  uint8_t *lds = lds_all + (size_t)wave * G * k * 16;
+  const int r0w = r0 + wave * RT;
+  const int rt = r - r0w < RT ? r - r0w : RT;  // <= 0: this wave has no repairs (waits at barriers)
   for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
     __syncthreads();
-    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g0 + lane / RT, repair r0 + lane % RT)
+    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g0 + lane / RT, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = g0 + g;
       uint8_t *row = lds + (size_t)g * k * 16 + i;
       if (b < nblocks && i < rt) {
         Tmt t;
-        tmt_init(t, rlc_seed(block_fbn(b, fbn_base, fbn), (uint32_t)(r0 + i)));
+        tmt_init(t, rlc_seed(block_fbn(b, fbn_base, fbn), (uint32_t)(r0w + i)));
         for (int j = 0; j < k; j++) row[j * 16] = tmt_coef(t);
       } else {
         for (int j = 0; j < k; j++) row[j * 16] = 0;
       }
     }
     __syncthreads();
+    if (rt <= 0) continue;
     const uint64_t ng = nblocks - g0 < (uint64_t)G ? nblocks - g0 : (uint64_t)G;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
       BsLanes<VEC> ln(lane, cb);
       const uint64_t sp = (uint64_t)(uintptr_t)(src + (g0 * (uint64_t)k) * (uint64_t)L + c0);
-      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (g0 * (uint64_t)r + r0) * (uint64_t)L + c0);
+      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (g0 * (uint64_t)r + r0w) * (uint64_t)L + c0);
       if (lane < ln.active)
         bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, (uint32_t)(r * L), (uint32_t)(ng * k), (uint32_t)k,
                              (uint32_t)rt, lds_addr(lds), ln);
@@ -890,9 +927,12 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
   }
 }
 
+// 16-B pieces whenever a symbol holds one (a symbol length that is not a multiple of 16 gets an
+// overlapping last piece, see BsLanes); chunks of <= 2 KiB, every chunk but the last a multiple
+// of the piece size.  L is a multiple of 4 (checked at the ABI).
 static BsCfg pick_bs_cfg(int L) {
   BsCfg c;
-  c.vec = (L % 16 == 0) ? 16 : (L % 8 == 0) ? 8 : 4;
+  c.vec = (L >= 16) ? 16 : (L % 8 == 0) ? 8 : 4;
   c.nchunks = (L + 2047) / 2048;
   int cb = (L + c.nchunks - 1) / c.nchunks;
   cb = (cb + c.vec - 1) / c.vec * c.vec;
@@ -902,12 +942,12 @@ static BsCfg pick_bs_cfg(int L) {
 
 template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
-                             uint32_t fbn_base, const uint32_t *fbn, int r0, hipStream_t s) {
+                             uint32_t fbn_base, const uint32_t *fbn, int r0, int W, hipStream_t s) {
   const int G = bs_group(RT, k, 16, 0);
-  const size_t lds = (size_t)G * k * 16;
+  const size_t lds = (size_t)W * G * k * 16;
   const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G);
+  hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
+                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G);
 }
 
 template <int RT, int VEC>
@@ -1126,6 +1166,28 @@ void fecgpu_get_stats(fecgpu_stats_t *out) {
   out->decode_blocks = g_stats[3].load();
 }
 
+// Encode tiling: repairs per wave (RT) and waves per workgroup sharing the source stream.
+// FECGPU_ENC_TILE="RT,W" overrides (A/B experiments).
+struct EncTile { int rt, waves; };
+static EncTile pick_enc_tile(uint32_t r) {
+  static int ort = -1, ow = -1;
+  if (ort < 0) {
+    ort = 0;
+    if (const char *e = getenv("FECGPU_ENC_TILE")) {
+      int a = 0, b = 0;
+      if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4) {
+        ort = a;
+        ow = b;
+      }
+    }
+  }
+  if (ort > 0) return {ort, ow};
+  // measured (profiles/r01_tile_ab.log): splitting repairs over waves repeats the transpose and
+  // table work per wave and loses more VALU than the occupancy gains (k32r8 4x2: +34 %,
+  // k64r16 8x2: +10 %), so one wave carries up to 16 repairs
+  return {pick_rt(r), 1};
+}
+
 int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
                       uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn, void *stream) {
   int rc = check_common(src, rep, nblocks, k, r, symbol_size);
@@ -1141,9 +1203,11 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
     }
   } else {
     const BsCfg cfg = pick_bs_cfg((int)symbol_size);
-    for (int r0 = 0; r0 < (int)r; r0 += rt) {
+    const EncTile et = pick_enc_tile(r);
+    const int rt = et.rt;
+    for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
       FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                      (int)symbol_size, cfg, fbn_base, fbn, r0, s)
+                      (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, s)
     }
   }
   HIPCHK(hipGetLastError());
@@ -1197,7 +1261,20 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const size_t lane_lds = plan_lane_lds(k, r);
-  if (lane_lds <= 64 * 1024) {
+  static int force = -1;  // FECGPU_PLAN=wave|lane overrides the size rule (A/B experiments)
+  if (force < 0) {
+    const char *e = getenv("FECGPU_PLAN");
+    force = e && !strcmp(e, "wave") ? 1 : e && !strcmp(e, "lane") ? 2 : 0;
+  }
+  if (force != 1 && (lane_lds <= 64 * 1024 || force == 2) && lane_lds <= 160 * 1024) {
+    if (lane_lds > 65536) {
+      static bool raised = false;
+      if (!raised) {
+        HIPCHK(hipFuncSetAttribute((const void *)k_rlc_plan_lane, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024));
+        raised = true;
+      }
+    }
     const uint64_t groups = (nblocks + 63) / 64;
     hipLaunchKernelGGL(k_rlc_plan_lane, dim3(grid_for(groups)), dim3(64), lane_lds, s, nblocks, (int)k,
                        (int)r, fbn_base, fbn, src_present, rep_present, ws);

@@ -30,7 +30,7 @@ import os
 import random
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-OUT = os.path.join(HERE, "bitslice_gen.h")
+OUT = os.environ.get("FEC_GEN_OUT") or os.path.join(HERE, "bitslice_gen.h")
 
 # ----------------------------------------------------------------------------- register map
 T_BASE = 32
@@ -415,12 +415,17 @@ def data_base(mode: str) -> int:
     return DATA_BASE if mode == "enc" else DATA_BASE + 2  # tuples must start on an even VGPR
 
 
-def prefetch_depth(mode: str, RT: int) -> int:
-    """Deepest register prefetch that keeps 3 waves/SIMD (<= 168 VGPRs) where possible."""
-    for P in (8, 7, 6, 5, 4, 3, 2):
-        if data_base(mode) + 8 * P + 8 * RT <= 168:
-            return P
-    return 2
+def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
+    """Register prefetch depth P (source rows in flight per wave).  Prefer 3 waves/SIMD
+    (<= 168 VGPRs) when that still leaves P >= 4; otherwise (RT = 16) take everything up to
+    256 VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63."""
+    NP = 32 // VEC
+    budget3 = int(os.environ.get("FEC_GEN_VGPR3", "168"))
+    fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - 1) <= 63
+    p3 = max([P for P in range(2, 33) if fits(P, budget3)] or [0])
+    if p3 >= 4:
+        return min(p3, int(os.environ.get("FEC_GEN_PMAX", "8")))
+    return max([P for P in range(2, 33) if fits(P, 256)] or [2])
 
 
 CONFIGS = [(RT, VEC) for VEC in (16, 8, 4) for RT in (1, 2, 4, 8, 16)]
@@ -436,7 +441,7 @@ def main():
              "",
              f"#define FEC_BS_CASE_BYTES {CASE_BYTES}",
              "#ifndef FEC_LD_POL",
-             "#define FEC_LD_POL \" nt\"  // symbol loads: read once, stream past the caches",
+             "#define FEC_LD_POL \"\"  // symbol loads: default policy (nt loads measured slower for decode)",
              "#endif",
              "#ifndef FEC_ST_POL",
              "#define FEC_ST_POL \" nt\"  // repair / recovered symbol stores",
@@ -453,7 +458,7 @@ def main():
     tops = {}
     for mode in ("enc", "dec"):
         for RT, VEC in CONFIGS:
-            P = prefetch_depth(mode, RT)
+            P = prefetch_depth(mode, RT, VEC)
             fn, top = emit_function(mode, RT, VEC, P)
             tops[(mode, RT, VEC, P)] = top
             parts.append(fn)
