@@ -123,6 +123,11 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
                            uint32_t k, uint32_t symbol_size, const uint64_t *src_present,
                            const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
 
+/* Page-locked host memory for staging buffers (hipHostMalloc / hipHostFree), so callers in
+ * C need no HIP headers.  NULL on failure. */
+void *fecgpu_host_alloc(size_t bytes);
+void fecgpu_host_free(void *p);
+
 /* Synthetic payload generator (bench/tests): byte o of dst = byte (o mod 8) of
  * splitmix64(seed + (o/8 + 1) * 0x9e3779b97f4a7c15), o counted from `offset`. */
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream);

@@ -1,0 +1,85 @@
+/*
+ * pquic_fec_batch.h -- batching adapter for PQUIC's block FEC framework.
+ *
+ * The reference runs fec_generate_repair_symbols / fec_recover synchronously, one block per
+ * protocol-operation call (block_framework_sender.h:175-203 generate_and_queue_repair_symbols;
+ * block_framework_receiver.h:29-80 via fec_protoops.h:215-246 recover_block).  On a GPU a
+ * single block is pure launch and PCIe latency, so this adapter queues blocks from any number
+ * of connections into per-(operation, scheme, k, r) batches in page-locked memory and runs a
+ * batch through the device engine when it is full or when its oldest block has waited
+ * `max_delay_us` (the latency cap).  A worker thread runs the engine (H2D, kernels, D2H
+ * overlapped on HIP streams) while the caller keeps queueing.
+ *
+ * Completion has exactly the synchronous operation's effect: the repair symbols (or
+ * recovered source symbols) are allocated with the bound host allocator
+ * (pquic_fec_bind_host), written into the caller's fec_block_t with the reference's FPIDs,
+ * lengths and counters, and `done(user, fb, ret)` receives the value the protocol operation
+ * would have returned.  Completions run on the caller's thread inside pquic_fec_batch_poll /
+ * pquic_fec_batch_drain, never on the worker, because picoquic's allocator and connection
+ * state are single-threaded (picoquic/memory.c, plugin.c:1357-1360).
+ *
+ * The caller keeps `fb` (and its symbols) alive and unmodified until `done` runs for it.
+ */
+#ifndef PQUIC_FEC_BATCH_H
+#define PQUIC_FEC_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pquic_fec_protoops.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pquic_fec_batcher pquic_fec_batcher_t;
+
+typedef struct {
+    int device;              /* HIP device */
+    uint32_t batch_blocks;   /* a queue is flushed when it holds this many blocks (>= 1) */
+    uint32_t max_delay_us;   /* ... or when its oldest block has waited this long (poll) */
+    uint32_t max_symbol;     /* largest symbol length accepted (<= 32767, fec.h:95,109) */
+    int nstreams;            /* HIP streams the engine pipelines a batch over (>= 1) */
+} pquic_fec_batch_cfg_t;
+
+/* Called once per submitted block, on the caller's thread (see above). */
+typedef void (*pquic_fec_block_done_fn)(void *user, pquic_fec_block_t *fb, protoop_arg_t ret);
+
+typedef struct {
+    uint64_t submitted, completed;  /* blocks */
+    uint64_t batches;               /* engine calls */
+    uint64_t flushed_full, flushed_deadline, flushed_drain;
+    uint64_t immediate;             /* blocks completed at submit (preconditions failed) */
+    uint64_t engine_errors;
+} pquic_fec_batch_stats_t;
+
+/* NULL on failure (bad configuration, no device, out of pinned memory). */
+pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg);
+/* Drains (completing every queued block) and frees. */
+void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b);
+
+/* Queue fec_generate_repair_symbols (xor_scheme = 0: RLC-GF(256), 1: XOR) for `fb`, whose
+ * totals are set as the block framework sets them before the call
+ * (block_framework_sender.h:184-185).  `now_us` starts the block's latency clock.
+ * Returns 0 when accepted -- `done` is then called exactly once, possibly before this returns
+ * when the reference's preconditions fail -- or -1 (NULL argument, symbol longer than
+ * max_symbol, allocation failure), in which case `done` is never called. */
+int pquic_fec_batch_generate(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
+                             uint64_t now_us, pquic_fec_block_done_fn done, void *user);
+/* Queue fec_recover for `fb` (the receiver's block copy, fec_protoops.h:220-222). */
+int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
+                            uint64_t now_us, pquic_fec_block_done_fn done, void *user);
+
+/* Flushes every queue that is full or past its deadline at `now_us`, then runs `done` for
+ * every block whose batch has finished.  Non-blocking.  Returns the number of completions. */
+int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us);
+/* Flushes everything and waits until every queued block has completed.  Returns the number
+ * of completions. */
+int pquic_fec_batch_drain(pquic_fec_batcher_t *b);
+
+void pquic_fec_batch_get_stats(const pquic_fec_batcher_t *b, pquic_fec_batch_stats_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

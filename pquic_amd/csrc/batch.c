@@ -1,0 +1,352 @@
+/*
+ * pquic_amd/csrc/batch.c -- batching adapter for the block FEC framework
+ * (include/pquic_fec_batch.h).  Host C, like the framework it serves.
+ *
+ * Blocks are staged, as they are submitted, into the page-locked rows of an open "job" (one
+ * per operation, scheme, k and r): k source rows (+ r repair rows for recover) of `stride`
+ * bytes per block, zero-padded like the reference pads to max_length, plus per-block FEC
+ * block numbers and presence masks.  A full or overdue job goes to a worker thread that runs
+ * it through the engine's host-resident entry points (H2D, kernels, D2H pipelined on HIP
+ * streams); finished jobs are completed on the caller's thread in poll / drain with the same
+ * finish halves the synchronous operations use (fec_core.c), so a batched block ends in
+ * exactly the state the protocol operation would leave it in.
+ */
+#include "pquic_fec_batch.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fec_core.h"
+#include "fecgpu.h"
+
+enum { OP_GENERATE = 0, OP_RECOVER = 1 };
+enum { MAX_OPEN = 32 };
+
+typedef struct {
+    picoquic_cnx_t *cnx;
+    pquic_fec_block_t *fb;
+    pquic_fec_block_done_fn done;
+    void *user;
+    uint16_t maxl;
+} entry_t;
+
+typedef struct job {
+    struct job *next;
+    int op, xor_scheme;
+    uint32_t k, r, n, cap, stride;
+    size_t src_bytes, rep_bytes;   /* allocated pinned sizes */
+    uint8_t *src, *rep, *st;       /* pinned */
+    uint32_t *fbn;                 /* pinned */
+    uint64_t *sp, *rp, *rec;       /* pinned, 2 words per block */
+    entry_t *ent;
+    uint64_t t_first;
+    int rc;
+} job_t;
+
+struct pquic_fec_batcher {
+    pquic_fec_batch_cfg_t cfg;
+    uint32_t stride;
+    fecgpu_host_ctx_t *ctx;
+    job_t *open[MAX_OPEN];
+    job_t *free_jobs;
+    pthread_t worker;
+    pthread_mutex_t mu;
+    pthread_cond_t cv_todo, cv_done;
+    job_t *todo_head, *todo_tail, *done_head, *done_tail;
+    int inflight, stop;
+    pquic_fec_batch_stats_t stats;
+};
+
+static void job_free(job_t *j) {
+    if (!j) return;
+    fecgpu_host_free(j->src);
+    fecgpu_host_free(j->rep);
+    fecgpu_host_free(j->st);
+    fecgpu_host_free(j->fbn);
+    fecgpu_host_free(j->sp);
+    free(j->ent);
+    free(j);
+}
+
+/* A job for (op, scheme, k, r), from the free list when one is big enough. */
+static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
+    const uint32_t cap = b->cfg.batch_blocks, S = b->stride;
+    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
+    job_t **pp = &b->free_jobs;
+    for (; *pp; pp = &(*pp)->next)
+        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb) break;
+    job_t *j = *pp;
+    if (j) {
+        *pp = j->next;
+    } else {
+        j = calloc(1, sizeof *j);
+        if (!j) return NULL;
+        j->src_bytes = sb;
+        j->rep_bytes = rb;
+        j->src = fecgpu_host_alloc(sb);
+        j->rep = fecgpu_host_alloc(rb ? rb : 4);
+        j->st = fecgpu_host_alloc(cap);
+        j->fbn = fecgpu_host_alloc((size_t)cap * 4);
+        j->sp = fecgpu_host_alloc((size_t)cap * 48);  /* sp | rp | rec, 2 words each per block */
+        j->ent = calloc(cap, sizeof *j->ent);
+        if (!j->src || !j->rep || !j->st || !j->fbn || !j->sp || !j->ent) {
+            job_free(j);
+            return NULL;
+        }
+    }
+    j->rp = j->sp + 2 * (size_t)cap;
+    j->rec = j->rp + 2 * (size_t)cap;
+    j->next = NULL;
+    j->op = op;
+    j->xor_scheme = xor_scheme;
+    j->k = k;
+    j->r = r;
+    j->n = 0;
+    j->cap = cap;
+    j->stride = S;
+    j->rc = 0;
+    return j;
+}
+
+static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
+    fecgpu_host_ctx_t *c = b->ctx;
+    const uint32_t S = j->stride;
+    if (j->op == OP_GENERATE)
+        j->rc = j->xor_scheme ? fecgpu_xor_encode_host(c, j->src, j->rep, j->n, j->k, S)
+                              : fecgpu_rlc_encode_host(c, j->src, j->rep, j->n, j->k, j->r, S, 0, j->fbn);
+    else
+        j->rc = j->xor_scheme
+                    ? fecgpu_xor_decode_host(c, j->src, j->rep, j->n, j->k, S, j->sp, j->rp, j->st, j->rec)
+                    : fecgpu_rlc_decode_host(c, j->src, j->rep, j->n, j->k, j->r, S, 0, j->fbn, j->sp, j->rp, j->st,
+                                             j->rec);
+}
+
+static void *worker_main(void *arg) {
+    pquic_fec_batcher_t *b = arg;
+    pthread_mutex_lock(&b->mu);
+    for (;;) {
+        while (!b->todo_head && !b->stop) pthread_cond_wait(&b->cv_todo, &b->mu);
+        if (!b->todo_head) break;  /* stop requested and nothing left */
+        job_t *j = b->todo_head;
+        b->todo_head = j->next;
+        if (!b->todo_head) b->todo_tail = NULL;
+        pthread_mutex_unlock(&b->mu);
+        run_engine(b, j);
+        pthread_mutex_lock(&b->mu);
+        j->next = NULL;
+        if (b->done_tail) b->done_tail->next = j; else b->done_head = j;
+        b->done_tail = j;
+        b->inflight--;
+        pthread_cond_broadcast(&b->cv_done);
+    }
+    pthread_mutex_unlock(&b->mu);
+    return NULL;
+}
+
+pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) {
+    if (!cfg || cfg->batch_blocks < 1 || cfg->max_symbol < 1 || cfg->max_symbol > 32767 || cfg->nstreams < 1)
+        return NULL;
+    pquic_fec_batcher_t *b = calloc(1, sizeof *b);
+    if (!b) return NULL;
+    b->cfg = *cfg;
+    b->stride = fec_pad4(cfg->max_symbol);
+    const size_t chunk = (size_t)cfg->batch_blocks * 20 * b->stride / (size_t)cfg->nstreams;
+    b->ctx = fecgpu_host_ctx_create(cfg->device, cfg->nstreams, chunk < (1u << 20) ? (1u << 20) : chunk);
+    if (!b->ctx) {
+        free(b);
+        return NULL;
+    }
+    pthread_mutex_init(&b->mu, NULL);
+    pthread_cond_init(&b->cv_todo, NULL);
+    pthread_cond_init(&b->cv_done, NULL);
+    if (pthread_create(&b->worker, NULL, worker_main, b)) {
+        fecgpu_host_ctx_destroy(b->ctx);
+        free(b);
+        return NULL;
+    }
+    return b;
+}
+
+static void flush_job(pquic_fec_batcher_t *b, int slot, uint64_t *counter) {
+    job_t *j = b->open[slot];
+    b->open[slot] = NULL;
+    if (!j) return;
+    if (!j->n) {  /* nothing queued: back to the free list */
+        j->next = b->free_jobs;
+        b->free_jobs = j;
+        return;
+    }
+    (*counter)++;
+    b->stats.batches++;
+    pthread_mutex_lock(&b->mu);
+    j->next = NULL;
+    if (b->todo_tail) b->todo_tail->next = j; else b->todo_head = j;
+    b->todo_tail = j;
+    b->inflight++;
+    pthread_cond_signal(&b->cv_todo);
+    pthread_mutex_unlock(&b->mu);
+}
+
+/* The open job for a key, opening one (and if every slot is taken, flushing the oldest). */
+static job_t *open_job(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r, int *slot_out) {
+    int free_slot = -1, oldest = -1;
+    for (int s = 0; s < MAX_OPEN; s++) {
+        job_t *j = b->open[s];
+        if (!j) {
+            if (free_slot < 0) free_slot = s;
+            continue;
+        }
+        if (j->op == op && j->xor_scheme == xor_scheme && j->k == k && j->r == r) {
+            *slot_out = s;
+            return j;
+        }
+        if (oldest < 0 || j->t_first < b->open[oldest]->t_first) oldest = s;
+    }
+    if (free_slot < 0) {
+        flush_job(b, oldest, &b->stats.flushed_full);
+        free_slot = oldest;
+    }
+    job_t *j = job_get(b, op, xor_scheme, k, r);
+    if (!j) return NULL;
+    b->open[free_slot] = j;
+    *slot_out = free_slot;
+    return j;
+}
+
+static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int op, int xor_scheme,
+                  uint64_t now_us, pquic_fec_block_done_fn done, void *user) {
+    if (!b || !fb || !done) return -1;
+    if (!g_fec_bound) {
+        b->stats.immediate++;
+        done(user, fb, PQUIC_FEC_ERR_UNBOUND);
+        return 0;
+    }
+    uint16_t maxl = 0;
+    const uint32_t k = fb->total_source_symbols;
+    uint32_t r = fb->total_repair_symbols;
+    if (op == OP_GENERATE) {
+        if (fec_generate_check(fb, xor_scheme, &maxl)) {  /* the reference returns 1, nothing done */
+            b->stats.immediate++;
+            done(user, fb, 1);
+            return 0;
+        }
+    } else {
+        const int chk = fec_recover_check(fb, xor_scheme, &maxl);
+        if (chk != FEC_STAGE_OK) {
+            b->stats.immediate++;
+            if (chk == FEC_STAGE_REJECT) g_fec_stats.errors++;
+            done(user, fb, chk == FEC_STAGE_REJECT ? PQUIC_FEC_ERR_UNBOUND : (protoop_arg_t)chk);
+            return 0;
+        }
+        if (xor_scheme) r = 1;
+    }
+    if (maxl > b->cfg.max_symbol) return -1;
+    int slot;
+    job_t *j = open_job(b, op, xor_scheme, k, r, &slot);
+    if (!j) return -1;
+    const uint32_t i = j->n, S = j->stride;
+    uint8_t *src = j->src + (size_t)i * k * S;
+    if (op == OP_GENERATE) {
+        fec_generate_stage(fb, src, S);
+    } else {
+        fec_recover_stage(fb, xor_scheme, maxl, src, j->rep + (size_t)i * r * S, S, j->sp + 2 * (size_t)i,
+                          j->rp + 2 * (size_t)i);
+    }
+    j->fbn[i] = fb->fec_block_number & 0xffffffu;
+    j->ent[i] = (entry_t){cnx, fb, done, user, maxl};
+    if (!i) j->t_first = now_us;
+    j->n = i + 1;
+    b->stats.submitted++;
+    if (j->n == j->cap) flush_job(b, slot, &b->stats.flushed_full);
+    return 0;
+}
+
+int pquic_fec_batch_generate(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
+                             uint64_t now_us, pquic_fec_block_done_fn done, void *user) {
+    return submit(b, cnx, fb, OP_GENERATE, xor_scheme ? 1 : 0, now_us, done, user);
+}
+
+int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
+                            uint64_t now_us, pquic_fec_block_done_fn done, void *user) {
+    return submit(b, cnx, fb, OP_RECOVER, xor_scheme ? 1 : 0, now_us, done, user);
+}
+
+/* Completes every finished job: the finish halves of the protocol operations, then done(). */
+static int collect(pquic_fec_batcher_t *b) {
+    pthread_mutex_lock(&b->mu);
+    job_t *j = b->done_head;
+    b->done_head = b->done_tail = NULL;
+    pthread_mutex_unlock(&b->mu);
+    int n = 0;
+    while (j) {
+        job_t *next = j->next;
+        const uint32_t S = j->stride;
+        if (j->rc) b->stats.engine_errors++;
+        for (uint32_t i = 0; i < j->n; i++) {
+            entry_t *e = &j->ent[i];
+            protoop_arg_t ret;
+            if (j->rc) {
+                g_fec_stats.errors++;
+                ret = PQUIC_FEC_ERR_UNBOUND;
+            } else if (j->op == OP_GENERATE) {
+                ret = fec_generate_finish(e->cnx, e->fb, j->rep + (size_t)i * j->r * S, S, e->maxl);
+            } else {
+                ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
+                                         j->src + (size_t)i * j->k * S, S, e->maxl);
+            }
+            if (j->op == OP_GENERATE) g_fec_stats.generate_calls++; else g_fec_stats.recover_calls++;
+            e->done(e->user, e->fb, ret);
+            n++;
+        }
+        b->stats.completed += j->n;
+        j->n = 0;
+        j->next = b->free_jobs;
+        b->free_jobs = j;
+        j = next;
+    }
+    return n;
+}
+
+int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us) {
+    if (!b) return 0;
+    for (int s = 0; s < MAX_OPEN; s++) {
+        job_t *j = b->open[s];
+        if (j && j->n && now_us - j->t_first >= b->cfg.max_delay_us) flush_job(b, s, &b->stats.flushed_deadline);
+    }
+    return collect(b);
+}
+
+int pquic_fec_batch_drain(pquic_fec_batcher_t *b) {
+    if (!b) return 0;
+    for (int s = 0; s < MAX_OPEN; s++)
+        if (b->open[s]) flush_job(b, s, &b->stats.flushed_drain);
+    pthread_mutex_lock(&b->mu);
+    while (b->inflight) pthread_cond_wait(&b->cv_done, &b->mu);
+    pthread_mutex_unlock(&b->mu);
+    return collect(b);
+}
+
+void pquic_fec_batch_get_stats(const pquic_fec_batcher_t *b, pquic_fec_batch_stats_t *out) {
+    if (b && out) *out = b->stats;
+}
+
+void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
+    if (!b) return;
+    pquic_fec_batch_drain(b);
+    pthread_mutex_lock(&b->mu);
+    b->stop = 1;
+    pthread_cond_broadcast(&b->cv_todo);
+    pthread_mutex_unlock(&b->mu);
+    pthread_join(b->worker, NULL);
+    while (b->free_jobs) {
+        job_t *j = b->free_jobs;
+        b->free_jobs = j->next;
+        job_free(j);
+    }
+    fecgpu_host_ctx_destroy(b->ctx);
+    pthread_mutex_destroy(&b->mu);
+    pthread_cond_destroy(&b->cv_todo);
+    pthread_cond_destroy(&b->cv_done);
+    free(b);
+}

@@ -1,0 +1,163 @@
+/*
+ * pquic_amd/csrc/fec_core.c -- the block <-> row-layout halves of the FEC scheme operations
+ * (see fec_core.h).  Host C, like the reference pluglets whose behaviour each function cites.
+ */
+#include "fec_core.h"
+
+#include <string.h>
+
+#include "fecgpu.h"
+
+/* malloc_repair_symbol (plugins/fec/fec.h:231-244): zeroed struct, fpid, data */
+static pquic_repair_symbol_t *new_repair(picoquic_cnx_t *cnx, uint64_t fpid_raw, uint16_t len) {
+    pquic_repair_symbol_t *s = g_fec_api.my_malloc(cnx, sizeof *s);
+    uint8_t *d = g_fec_api.my_malloc(cnx, len);
+    if (!s || !d) {
+        if (s) g_fec_api.my_free(cnx, s);
+        if (d) g_fec_api.my_free(cnx, d);
+        return NULL;
+    }
+    memset(s, 0, sizeof *s);
+    s->fpid.raw = fpid_raw;
+    s->data = d;
+    s->data_length = len;
+    return s;
+}
+
+/* malloc_source_symbol (plugins/fec/fec.h:201-213) */
+static pquic_source_symbol_t *new_source(picoquic_cnx_t *cnx, uint32_t fpid_raw, uint16_t len) {
+    pquic_source_symbol_t *s = g_fec_api.my_malloc(cnx, sizeof *s);
+    uint8_t *d = g_fec_api.my_malloc(cnx, len);
+    if (!s || !d) {
+        if (s) g_fec_api.my_free(cnx, s);
+        if (d) g_fec_api.my_free(cnx, d);
+        return NULL;
+    }
+    memset(s, 0, sizeof *s);
+    s->fpid.raw = fpid_raw;
+    s->data = d;
+    s->data_length = len;
+    return s;
+}
+
+int fec_generate_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *maxl) {
+    const int k = fb->total_source_symbols, r = fb->total_repair_symbols;
+    /* rlc_fec_scheme_generate_gf256.c:34-39 / xor_fec_scheme_generate.c:45-50 */
+    if ((xor_scheme ? r != 1 : r == 0) || k < 1 || fb->current_source_symbols != fb->total_source_symbols)
+        return 1;
+    uint16_t m = 0;
+    for (int j = 0; j < k; j++)
+        if (fb->source_symbols[j] && fb->source_symbols[j]->data_length > m) m = fb->source_symbols[j]->data_length;
+    *maxl = m;
+    return 0;
+}
+
+void fec_generate_stage(const pquic_fec_block_t *fb, uint8_t *src_rows, uint32_t stride) {
+    for (int j = 0; j < fb->total_source_symbols; j++) {  /* zero-padded to max_length (:41-55) */
+        uint8_t *row = src_rows + (size_t)j * stride;
+        const pquic_source_symbol_t *ss = fb->source_symbols[j];
+        const uint16_t n = ss ? ss->data_length : 0;
+        if (n) memcpy(row, ss->data, n);
+        memset(row + n, 0, stride - n);
+    }
+}
+
+protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, const uint8_t *rep_rows,
+                                  uint32_t stride, uint16_t maxl) {
+    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+    for (int i = 0; i < fb->total_repair_symbols; i++) {
+        /* repair fpid: raw 0, fec_block_number, symbol_number = i, fec_scheme_specific 0
+         * (rlc_fec_scheme_generate_gf256.c:57-61; xor_fec_scheme_generate.c:71-75) */
+        pquic_repair_symbol_t *rs = new_repair(cnx, ((uint64_t)fbn << 8) | (uint64_t)(i & 0xff), maxl);
+        if (!rs) return PQUIC_ERROR_MEMORY;
+        memcpy(rs->data, rep_rows + (size_t)i * stride, maxl);
+        fb->repair_symbols[i] = rs;
+    }
+    return 0;
+}
+
+int fec_recover_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *maxl) {
+    const int r = fb->total_repair_symbols;
+    if (xor_scheme) {
+        if (r != 1 || fb->current_source_symbols + fb->current_repair_symbols != fb->total_source_symbols)
+            return 1;  /* xor_fec_scheme.c:45-49 */
+        if (!fb->repair_symbols[0]) return 1;  /* the reference dereferences NULL here (:50-51) */
+        *maxl = fb->repair_symbols[0]->data_length;
+        return FEC_STAGE_OK;
+    }
+    if (r == 0 || fb->current_source_symbols == fb->total_source_symbols ||
+        fb->current_source_symbols + fb->current_repair_symbols < fb->total_source_symbols)
+        return 0;  /* rlc_fec_scheme_gf256.c:140-144 */
+    int first = -1;
+    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+    for (int i = 0; i < r; i++) {
+        const pquic_repair_symbol_t *rs = fb->repair_symbols[i];
+        if (!rs) continue;
+        if (first < 0) first = i;
+        /* the seed is the repair's own FPID (:200); the engine derives it from the block
+         * number and the slot, which the block framework keeps equal
+         * (block_framework_receiver.h:29-56, fec.h:292-299) */
+        if (rs->fpid.f.source_fpid.raw != ((fbn << 8) | (uint32_t)(i & 0xff))) return FEC_STAGE_REJECT;
+    }
+    if (first < 0) return 0;
+    *maxl = fb->repair_symbols[first]->data_length;  /* :186 */
+    return FEC_STAGE_OK;
+}
+
+void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t maxl, uint8_t *src_rows,
+                       uint8_t *rep_rows, uint32_t stride, uint64_t sp[2], uint64_t rp[2]) {
+    const int k = fb->total_source_symbols, r = xor_scheme ? 1 : fb->total_repair_symbols;
+    sp[0] = sp[1] = rp[0] = rp[1] = 0;
+    for (int j = 0; j < k; j++) {
+        uint8_t *row = src_rows + (size_t)j * stride;
+        const pquic_source_symbol_t *ss = fb->source_symbols[j];
+        uint16_t n = 0;
+        if (ss) {  /* bytes past max_length are never read back (:205): truncate */
+            n = ss->data_length < maxl ? ss->data_length : maxl;
+            memcpy(row, ss->data, n);
+            sp[j >> 6] |= 1ull << (j & 63);
+        }
+        memset(row + n, 0, stride - n);
+    }
+    for (int i = 0; i < r; i++) {
+        uint8_t *row = rep_rows + (size_t)i * stride;
+        const pquic_repair_symbol_t *rs = fb->repair_symbols[i];
+        uint16_t n = 0;
+        if (rs) {
+            n = rs->data_length < maxl ? rs->data_length : maxl;
+            memcpy(row, rs->data, n);
+            rp[i >> 6] |= 1ull << (i & 63);
+        }
+        memset(row + n, 0, stride - n);
+    }
+}
+
+protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme, uint8_t status,
+                                 const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl) {
+    const int k = fb->total_source_symbols;
+    if (status == FECGPU_BLOCK_REF_UB) g_fec_stats.ref_ub_blocks++;
+    if (!xor_scheme) {
+        const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+        for (int j = 0; j < k && status == FECGPU_BLOCK_RECOVERED; j++) {  /* :218-236 */
+            if (!((rec[j >> 6] >> (j & 63)) & 1)) continue;
+            pquic_source_symbol_t *ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl);
+            if (!ss) continue;  /* the reference skips an unallocatable symbol (:222-226) */
+            memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
+            fb->source_symbols[j] = ss;
+            fb->current_source_symbols++;
+            g_fec_stats.recovered_symbols++;
+        }
+        return 0;
+    }
+    protoop_arg_t ret = 1;
+    for (int j = 0; j < k && status == FECGPU_BLOCK_RECOVERED; j++) {
+        if (!((rec[j >> 6] >> (j & 63)) & 1)) continue;
+        pquic_source_symbol_t *ss = new_source(cnx, (fb->fec_block_number << 8) | (uint32_t)j, maxl);
+        if (!ss) return PQUIC_ERROR_MEMORY;
+        memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
+        fb->source_symbols[j] = ss;  /* current_source_symbols is NOT incremented (:72) */
+        g_fec_stats.recovered_symbols++;
+        ret = 0;
+    }
+    return ret;
+}

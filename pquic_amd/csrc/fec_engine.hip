@@ -23,7 +23,11 @@
 #include <stdlib.h>
 
 #include "fec_device.h"
+#ifdef FEC_BS_GEN_HEADER  // A/B experiments: an alternative generated body set
+#include FEC_BS_GEN_HEADER
+#else
 #include "bitslice_gen.h"
+#endif
 #include "../../include/fecgpu.h"
 
 using namespace fecdev;

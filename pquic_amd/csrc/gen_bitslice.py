@@ -300,17 +300,31 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a("s_waitcnt lgkmcnt(0)")
         for w in range(ncw):
             a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-        for i in range(RT):
-            a(f"s_bfe_u32 s{S_T}, s{S_C[i // 4]}, 0x{(8 << 16) | (8 * (i % 4)):x}")
-            a(f"s_mul_i32 s{S_T}, s{S_T}, {CASE_BYTES}")
-            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
+        if os.environ.get("FEC_GEN_FAKE_DISPATCH"):  # timing experiment only: wrong results
+            for i in range(RT):
+                for o, (nl, nh) in enumerate(case_rows(19)):
+                    acc = acc_base + 8 * i + o
+                    a(f"v_bitop3_b32 v{acc}, v{acc}, {v(TL[nl])}, {v(TH[nh])} bitop3:0x96")
+            RT_calls = 0
+        else:
+            RT_calls = RT
+        fixed_target = bool(os.environ.get("FEC_GEN_FIXED_TARGET"))  # timing experiment only
+        if fixed_target:
+            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, {19 * CASE_BYTES}")
             a(f"s_addc_u32 s{S_TGT + 1}, s{S_TAB + 1}, 0")
+        for i in range(RT_calls):
+            if not fixed_target:
+                a(f"s_bfe_u32 s{S_T}, s{S_C[i // 4]}, 0x{(8 << 16) | (8 * (i % 4)):x}")
+                a(f"s_mul_i32 s{S_T}, s{S_T}, {CASE_BYTES}")
+                a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
+                a(f"s_addc_u32 s{S_TGT + 1}, s{S_TAB + 1}, 0")
             if i == 0:
                 a(f"s_set_gpr_idx_on {acc_base}, gpr_idx(SRC0,DST)")
             else:
                 a(f"s_set_gpr_idx_idx {acc_base + 8 * i}")
             a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
-        a("s_set_gpr_idx_off")
+        if RT_calls:
+            a("s_set_gpr_idx_off")
         a(f"s_add_u32 s{S_S}, s{S_S}, 1")
         a(f"s_add_u32 s{S_J}, s{S_J}, 1")
         a(f"s_cmp_eq_u32 s{S_J}, %[k]")

@@ -200,3 +200,15 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uin
 }
 
 }  // extern "C"
+
+extern "C" {
+void *fecgpu_host_alloc(size_t bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void fecgpu_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+}  // extern "C"

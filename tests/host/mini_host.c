@@ -175,3 +175,149 @@ long mh_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, 
     free_block(fb);
     return (long)ret;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Batching adapter (include/pquic_fec_batch.h): blocks built exactly as above, submitted to
+ * one batcher, completed through its callback; results read back per ticket.
+ * ------------------------------------------------------------------------------------------ */
+#include "pquic_fec_batch.h"
+
+typedef struct {
+    pquic_fec_block_t *fb;
+    pquic_source_symbol_t *before[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
+    long ret;
+    int done, calls, k, r;
+} ticket_t;
+
+static pquic_fec_batcher_t *g_batcher;
+static ticket_t *g_tickets;
+static long g_nt, g_capt;
+static picoquic_cnx_t g_bcnx;
+
+static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
+    ticket_t *t = &g_tickets[(long)(intptr_t)user];
+    (void)fb;
+    t->ret = (long)ret;
+    t->done = 1;
+    t->calls++;
+}
+
+int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsigned max_symbol, int nstreams) {
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, max_symbol, nstreams};
+    g_batcher = pquic_fec_batcher_create(&cfg);
+    return g_batcher ? 0 : -1;
+}
+
+static long new_ticket(pquic_fec_block_t *fb, int k, int r) {
+    if (g_nt == g_capt) {
+        g_capt = g_capt ? 2 * g_capt : 1024;
+        g_tickets = realloc(g_tickets, g_capt * sizeof *g_tickets);
+    }
+    ticket_t *t = &g_tickets[g_nt];
+    memset(t, 0, sizeof *t);
+    t->fb = fb;
+    t->k = k;
+    t->r = r;
+    return g_nt++;
+}
+
+/* returns the ticket (>= 0) or -1 when the batcher refused the block */
+long mh_batch_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
+                       int src_stride, uint64_t now_us) {
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    fb->fec_block_number = fbn;
+    for (int j = 0; j < k; j++) fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+    fb->current_source_symbols = (uint8_t)k;
+    fb->total_source_symbols = (uint8_t)k;
+    fb->total_repair_symbols = (uint8_t)r;
+    long t = new_ticket(fb, k, r);
+    if (pquic_fec_batch_generate(g_batcher, &g_bcnx, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
+        free_block(fb);
+        g_nt--;
+        return -1;
+    }
+    return t;
+}
+
+long mh_batch_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
+                      const uint8_t *src_present, int src_stride, const uint8_t *rep, const uint16_t *rep_len,
+                      const uint8_t *rep_present, const uint64_t *rep_fpid, int rep_stride, uint64_t now_us) {
+    picoquic_cnx_t c;
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    fb->fec_block_number = fbn;
+    fb->total_source_symbols = (uint8_t)k;
+    fb->total_repair_symbols = (uint8_t)r;
+    for (int j = 0; j < k; j++)
+        if (src_present[j]) {
+            fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+            fb->current_source_symbols++;
+        }
+    for (int i = 0; i < r; i++)
+        if (rep_present[i]) {
+            pquic_repair_symbol_t *rs = mh_malloc(&c, sizeof *rs);
+            memset(rs, 0, sizeof *rs);
+            rs->fpid.raw = rep_fpid[i];
+            rs->data = mh_malloc(&c, rep_len[i]);
+            memcpy(rs->data, rep + (size_t)i * rep_stride, rep_len[i]);
+            rs->data_length = rep_len[i];
+            fb->repair_symbols[i] = rs;
+            fb->current_repair_symbols++;
+        }
+    long t = new_ticket(fb, k, r);
+    memcpy(g_tickets[t].before, fb->source_symbols, sizeof g_tickets[t].before);
+    if (pquic_fec_batch_recover(g_batcher, &g_bcnx, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
+        free_block(fb);
+        g_nt--;
+        return -1;
+    }
+    return t;
+}
+
+int mh_batch_poll(uint64_t now_us) { return pquic_fec_batch_poll(g_batcher, now_us); }
+int mh_batch_drain(void) { return pquic_fec_batch_drain(g_batcher); }
+
+/* ticket state: -1 not done; else the operation's value.  calls = number of done() calls */
+long mh_batch_status(long t, int *calls) {
+    *calls = g_tickets[t].calls;
+    return g_tickets[t].done ? g_tickets[t].ret : -1;
+}
+
+/* generate result: repairs of ticket t */
+void mh_batch_repairs(long t, uint8_t *rep_out, uint16_t *rep_len, uint64_t *rep_fpid, int rep_stride) {
+    ticket_t *tk = &g_tickets[t];
+    for (int i = 0; i < tk->r; i++) {
+        pquic_repair_symbol_t *rs = tk->fb->repair_symbols[i];
+        rep_len[i] = rs ? rs->data_length : 0;
+        rep_fpid[i] = rs ? rs->fpid.raw : 0;
+        if (rs) memcpy(rep_out + (size_t)i * rep_stride, rs->data, rs->data_length);
+    }
+}
+
+/* recover result: inserted sources of ticket t (as mh_recover reports them) */
+void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss) {
+    ticket_t *tk = &g_tickets[t];
+    for (int j = 0; j < tk->k; j++) {
+        pquic_source_symbol_t *ss = tk->fb->source_symbols[j];
+        recovered[j] = ss && ss != tk->before[j];
+        out_len[j] = recovered[j] ? ss->data_length : 0;
+        if (recovered[j]) memcpy(out + (size_t)j * out_stride, ss->data, ss->data_length);
+    }
+    *cur_ss = tk->fb->current_source_symbols;
+}
+
+void mh_batch_get_stats(uint64_t out[8]) {
+    pquic_fec_batch_stats_t s;
+    pquic_fec_batch_get_stats(g_batcher, &s);
+    out[0] = s.submitted; out[1] = s.completed; out[2] = s.batches; out[3] = s.flushed_full;
+    out[4] = s.flushed_deadline; out[5] = s.flushed_drain; out[6] = s.immediate; out[7] = s.engine_errors;
+}
+
+/* frees every ticket's block and the batcher */
+void mh_batch_close(void) {
+    pquic_fec_batcher_destroy(g_batcher);
+    g_batcher = NULL;
+    for (long t = 0; t < g_nt; t++) free_block(g_tickets[t].fb);
+    free(g_tickets);
+    g_tickets = NULL;
+    g_nt = g_capt = 0;
+}

@@ -18,6 +18,8 @@ src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
 eng.synth_fill(src, src.numel(), 1, 0)
 rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
 eng.rlc_encode(src, rep, k, r, L)
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ev[0].record()
 if mode == "enc":
     for _ in range(reps):
         eng.rlc_encode(src, rep, k, r, L)
@@ -32,5 +34,6 @@ else:
     ws = eng.alloc_workspace(nb, k, r)
     for _ in range(reps):
         eng.rlc_decode(src, rep, sp, rp, st, rec, k, r, L, workspace=ws)
+ev[1].record()
 torch.cuda.synchronize()
-print("done", mode, k, r, nb)
+print(f"done {mode} k={k} r={r} L={L} blocks={nb}: {ev[0].elapsed_time(ev[1]) / reps:.3f} ms per call")
