@@ -248,6 +248,34 @@ def pcie_legs(torch, args, dev):
                                        "note": "decode copies whole source rows both ways"}}
 
 
+def batching_legs(dev_index, args):
+    """§8f row 1: the block framework's blocks through the batching adapter
+    (include/pquic_fec_batch.h), end to end from host packet buffers: host staging into pinned
+    queues, PCIe, kernels, completion on the caller thread.  tools/batch_load.c plays the
+    single-threaded sender over 64 connections."""
+    import ctypes as C
+    path = os.path.join(ROOT, "tools", "libbatchload.so")
+    if not os.path.exists(path):
+        return {}
+    lib = C.CDLL(path)
+    lib.bl_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint, C.c_uint, C.c_int,
+                           C.c_double, C.POINTER(C.c_double)]
+    legs = {}
+    for name, nblocks, batch, delay, offered in (("saturated", 200000, 4096, 2000, 0.0),
+                                                 ("paced_2GiBps", 100000, 4096, 250, 2.0)):
+        out = (C.c_double * 8)()
+        rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, out)
+        if rc:
+            legs["batch_" + name] = {"error": rc}
+            continue
+        legs["batch_" + name] = {
+            "k": args.k, "r": args.r, "L": args.symbol, "blocks": nblocks, "connections": 64,
+            "batch_blocks": batch, "max_delay_us": delay, "offered_GiB_s": offered or None,
+            "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
+            "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1)}
+    return legs
+
+
 def main():
     args = parse()
     import torch
@@ -346,6 +374,7 @@ def main():
     del work, ws
     if not args.no_legs and not args.no_pcie and world == 1:
         legs.update(pcie_legs(torch, args, dev))
+        legs.update(batching_legs(dev.index or 0, args))
     if not args.no_legs and world == 1:
         # north-star leg: k = 32, r = 8 encode, 2^21 blocks (one GPU's share of config 4)
         nb2, k2, r2 = 1 << 21, 32, 8

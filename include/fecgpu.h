@@ -63,6 +63,15 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
                       uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
                       void *stream);
 
+/* Sliding-window RLC encode (window_framework_sender.h:214-250): window w protects the k
+ * consecutive symbols starting at symbol w * step of one symbol stream (windows overlap when
+ * step < k; symbols[] holds (nwindows - 1) * step + k rows of symbol_size bytes).  Window
+ * blocks carry fec_block_number 0 (malloc_fec_block(cnx, 0), :218), so every window's
+ * coefficients are seeded by the repair index alone:
+ *   rep[w][i] = sum_j coef(0, i)[j] * symbols[w * step + j]. */
+int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t step, uint32_t k, uint32_t r,
+                             uint32_t symbol_size, void *rep, void *stream);
+
 /* XOR encode (r == 1): rep[b][0] = XOR_j src[b][j]. */
 int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k,
                       uint32_t symbol_size, void *stream);

@@ -752,7 +752,7 @@ template <int RT, int VEC>
 __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
-                                                       int r0, int G) {
+                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
@@ -767,7 +767,8 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
       uint8_t *row = lds + (size_t)g * k * 16 + i;
       if (b < nblocks && i < rt) {
         Tmt t;
-        tmt_init(t, rlc_seed(block_fbn(b, fbn_base, fbn), (uint32_t)(r0w + i)));
+        const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
+        tmt_init(t, rlc_seed(f, (uint32_t)(r0w + i)));
         for (int j = 0; j < k; j++) row[j * 16] = tmt_coef(t);
       } else {
         for (int j = 0; j < k; j++) row[j * 16] = 0;
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
       BsLanes<VEC> ln(lane, cb);
-      const uint64_t sp = (uint64_t)(uintptr_t)(src + (g0 * (uint64_t)k) * (uint64_t)L + c0);
+      const uint64_t sp = (uint64_t)(uintptr_t)(src + g0 * sbs + c0);  // G == 1 unless sbs == k * L
       const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (g0 * (uint64_t)r + r0w) * (uint64_t)L + c0);
       if (lane < ln.active)
         bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, (uint32_t)(r * L), (uint32_t)(ng * k), (uint32_t)k,
@@ -944,14 +945,18 @@ static BsCfg pick_bs_cfg(int L) {
   return c;
 }
 
+// sbs: bytes from one block's first source to the next block's (k * L for packed blocks; a
+// sliding window's step * L, where consecutive blocks overlap).  The asm streams a group's
+// sources as one run of contiguous rows, so overlapping blocks go one per group.
 template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
-                             uint32_t fbn_base, const uint32_t *fbn, int r0, int W, hipStream_t s) {
-  const int G = bs_group(RT, k, 16, 0);
+                             uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
+                             hipStream_t s) {
+  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, 16, 0) : 1;
   const size_t lds = (size_t)W * G * k * 16;
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
-                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G);
+                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step);
 }
 
 template <int RT, int VEC>
@@ -1211,12 +1216,29 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
     const int rt = et.rt;
     for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
       FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                      (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, s)
+                      (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
     }
   }
   HIPCHK(hipGetLastError());
   g_stats[0]++;
   g_stats[1] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t step, uint32_t k, uint32_t r,
+                             uint32_t symbol_size, void *rep, void *stream) {
+  int rc = check_common(symbols, rep, nwindows, k, r, symbol_size);
+  if (rc || nwindows == 0 || r == 0) return rc;
+  if (step == 0) return set_err(FECGPU_ERR_INVALID, "%s", "window step must be >= 1");
+  const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+  const int rt = pick_rt(r);
+  for (int r0 = 0; r0 < (int)r; r0 += rt) {
+    FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)symbols, (uint8_t *)rep, nwindows, (int)k, (int)r,
+                    (int)symbol_size, cfg, 0u, nullptr, r0, 1, (uint64_t)step * symbol_size, 0u, (hipStream_t)stream)
+  }
+  HIPCHK(hipGetLastError());
+  g_stats[0]++;
+  g_stats[1] += nwindows;
   return FECGPU_OK;
 }
 

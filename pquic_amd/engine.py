@@ -42,6 +42,7 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_last_error.restype = C.c_char_p
     L.fecgpu_rlc_encode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v]
     L.fecgpu_xor_encode.argtypes = [v, v, u64, u32, u32, v]
+    L.fecgpu_rlc_window_encode.argtypes = [v, u64, u32, u32, u32, u32, v, v]
     L.fecgpu_rlc_decode_workspace.argtypes = [u64, u32, u32]
     L.fecgpu_rlc_decode_workspace.restype = sz
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
@@ -110,6 +111,12 @@ class Engine:
         nb = nblocks if nblocks is not None else src.numel() // (k * L)
         self._check(self.lib.fecgpu_rlc_encode(_addr(src), _addr(rep), nb, k, r, L, fbn_base,
                                                _addr(fbn), self._stream(stream)), "fecgpu_rlc_encode")
+        return rep
+
+    def rlc_window_encode(self, symbols, rep, nwindows: int, step: int, k: int, r: int, L: int, stream=None):
+        """Sliding-window encode: window w = symbols[w*step : w*step + k], block number 0."""
+        self._check(self.lib.fecgpu_rlc_window_encode(_addr(symbols), nwindows, step, k, r, L, _addr(rep),
+                                                      self._stream(stream)), "fecgpu_rlc_window_encode")
         return rep
 
     def xor_encode(self, src, rep, k: int, L: int, nblocks: int | None = None, stream=None):

@@ -342,3 +342,51 @@ def test_host_path_matches_oracle(oracle):
     ok = st == DEC_RECOVERED
     assert np.array_equal(work[ok], src[ok])
     hp.close()
+
+
+@pytest.mark.parametrize("k,r,step,L,nw", [(30, 5, 10, 1200, 40), (30, 5, 1, 1200, 70), (16, 4, 16, 1200, 33),
+                                           (8, 3, 12, 300, 20), (30, 8, 7, 9000, 9)])
+def test_window_encode_vs_oracle(eng, oracle, k, r, step, L, nw):
+    """Sliding-window RLC (window_framework_sender.h:214-250): overlapping windows of one symbol
+    stream, block number 0, i.e. coefficients seeded by the repair index alone."""
+    nsym = (nw - 1) * step + k
+    sym_h = synth_bytes(nsym * L, 4242 + step).reshape(nsym, L)
+    sym = to_dev(sym_h)
+    rep = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_window_encode(sym, rep, nw, step, k, r, L)
+    torch.cuda.synchronize()
+    got = rep.cpu().numpy()
+    for w in range(nw):
+        want = oracle.rlc_encode_block(0, list(sym_h[w * step: w * step + k]), r)[1]
+        for i in range(r):
+            assert np.array_equal(got[w, i], want[i]), (w, i)
+
+
+def test_window_decode_vs_oracle(eng, oracle):
+    """Window receiver (window_framework_receiver.h): each window's received symbols gathered
+    into a block with fec_block_number 0 and decoded; the engine's per-block block-number array
+    carries the zeros."""
+    k, r, step, L, nw = 30, 5, 10, 1200, 60
+    nsym = (nw - 1) * step + k
+    rng = np.random.default_rng(9)
+    sym_h = synth_bytes(nsym * L, 99).reshape(nsym, L)
+    rep = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_window_encode(to_dev(sym_h), rep, nw, step, k, r, L)
+    rep_h = rep.cpu().numpy()
+    src_h = np.stack([sym_h[w * step: w * step + k] for w in range(nw)])
+    sp = np.zeros((nw, 2), np.uint64)
+    rp = np.zeros((nw, 2), np.uint64)
+    for w in range(nw):
+        e = int(rng.integers(0, r + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[w] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        rp[w] = masks_from_lists(1, r, [list(range(r))])[0]
+    zeros = np.zeros(nw, np.uint32)
+    work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn=zeros)
+    for w in range(nw):  # window blocks all use block number 0: decode each with the oracle
+        blk = work[w].copy()
+        want_st, want_rec = oracle.rlc_decode_batch(blk[None], rep_h[w][None], sp[w][None], rp[w][None], 0)
+        assert st[w] == want_st[0] and np.array_equal(rec[w], want_rec[0]), w
+        for j in bits(rec[w], k):
+            assert np.array_equal(got[w, j], src_h[w, j])
+    assert (st == DEC_RECOVERED).sum() > nw // 2

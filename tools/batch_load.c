@@ -1,0 +1,139 @@
+/*
+ * tools/batch_load.c -- load generator for the batching adapter (include/pquic_fec_batch.h),
+ * used by bench.py's batching leg.  Plays a single-threaded picoquic sender: `nconn`
+ * connections each fill FEC blocks of k source symbols (L bytes, from a synthetic payload
+ * pool) and hand every full block to the batcher, optionally paced to an offered load; the
+ * completion callback stamps the block's latency and frees the repair symbols as the framework
+ * does after sending them (block_framework_sender.h:125-133).  Reports end-to-end throughput
+ * (host staging + PCIe + kernels) and the submit -> completion latency distribution.
+ */
+#define _POSIX_C_SOURCE 199309L
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "pquic_fec_batch.h"
+
+struct st_picoquic_cnx_t { int id; };
+
+static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) { (void)c; (void)ak; (void)p; return 0; }
+static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t v) { (void)c; (void)ak; (void)p; (void)v; }
+static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) { (void)c; return malloc(n); }
+static void bl_free(picoquic_cnx_t *c, void *p) { (void)c; free(p); }
+
+static uint64_t now_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+typedef struct {
+    pquic_fec_block_t fb;
+    uint64_t t_submit;
+    int busy;
+} slot_t;
+
+static uint64_t *g_lat;
+static long g_nlat;
+
+static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
+    slot_t *s = user;
+    (void)ret;
+    g_lat[g_nlat++] = now_us() - s->t_submit;
+    for (int i = 0; i < fb->total_repair_symbols; i++) {
+        pquic_repair_symbol_t *rs = fb->repair_symbols[i];
+        if (rs) { free(rs->data); free(rs); fb->repair_symbols[i] = NULL; }
+    }
+    s->busy = 0;
+}
+
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* out: [0] payload GiB/s, [1] p50 us, [2] p99 us, [3] max us, [4] batches, [5] wall s,
+ *      [6] blocks completed, [7] mean blocks per batch.  Returns 0 or -1. */
+int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks, unsigned max_delay_us,
+           int nstreams, double offered_gib_s, double out[8]) {
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free};
+    if (pquic_fec_bind_host(&api, device)) return -1;
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
+    pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
+    if (!b) return -1;
+    /* blocks in flight at most: every queued batch plus one being filled, per connection slot */
+    const long nslots = (long)batch_blocks * 4 + nconn + 64;
+    slot_t *slots = calloc(nslots, sizeof *slots);
+    const size_t pool_bytes = (size_t)64 * k * L;  /* 64 blocks of distinct payload, reused */
+    uint8_t *pool = malloc(pool_bytes);
+    pquic_source_symbol_t *ss = calloc((size_t)nslots * k, sizeof *ss);
+    g_lat = malloc(sizeof *g_lat * (size_t)(nblocks + nblocks / 5 + 1));
+    g_nlat = 0;
+    picoquic_cnx_t *cnx = calloc(nconn, sizeof *cnx);
+    if (!slots || !pool || !ss || !g_lat || !cnx) return -1;
+    uint64_t x = 0x5EEDF3C0;
+    for (size_t o = 0; o < pool_bytes; o++) {  /* xorshift payload */
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        pool[o] = (uint8_t)x;
+    }
+    for (int c = 0; c < nconn; c++) cnx[c].id = c;
+    const double bytes_per_block = (double)k * L;
+    long next_slot = 0;
+    /* pass 0 warms up (pinned queue buffers allocated, device buffers grown), pass 1 is measured */
+    uint64_t t0 = 0;
+    pquic_fec_batch_stats_t st0;
+    memset(&st0, 0, sizeof st0);
+    for (int pass = 0; pass < 2; pass++) {
+        const long nb = pass ? nblocks : nblocks / 5 + 1;
+        if (pass) {
+            pquic_fec_batch_drain(b);
+            pquic_fec_batch_get_stats(b, &st0);
+            g_nlat = 0;
+        }
+        t0 = now_us();
+        for (long blk = 0; blk < nb; blk++) {
+            if (offered_gib_s > 0) {  /* pace: block blk is due at t0 + blk * bytes / rate */
+                const uint64_t due = t0 + (uint64_t)(blk * bytes_per_block / (offered_gib_s * 1073741824.0) * 1e6);
+                while (now_us() < due) pquic_fec_batch_poll(b, now_us());
+            }
+            slot_t *s = &slots[next_slot];
+            while (s->busy) pquic_fec_batch_poll(b, now_us());  /* back-pressure: slot still in flight */
+            const long si = next_slot;
+            next_slot = (next_slot + 1) % nslots;
+            memset(&s->fb, 0, sizeof s->fb);
+            const uint32_t fbn = (uint32_t)(blk / nconn) & 0xffffffu;
+            s->fb.fec_block_number = fbn;
+            for (int j = 0; j < k; j++) {
+                pquic_source_symbol_t *sym = &ss[si * k + j];
+                sym->fpid.raw = (fbn << 8) | (uint32_t)j;
+                sym->data = pool + ((size_t)(blk % 64) * k + j) * L;
+                sym->data_length = (uint16_t)L;
+                s->fb.source_symbols[j] = sym;
+            }
+            s->fb.current_source_symbols = s->fb.total_source_symbols = (uint8_t)k;
+            s->fb.total_repair_symbols = (uint8_t)r;
+            s->busy = 1;
+            s->t_submit = now_us();
+            if (pquic_fec_batch_generate(b, &cnx[blk % nconn], &s->fb, 0, s->t_submit, on_done, s)) return -1;
+            if ((blk & 15) == 0) pquic_fec_batch_poll(b, now_us());
+        }
+    }
+    pquic_fec_batch_drain(b);
+    const double wall = (now_us() - t0) * 1e-6;
+    pquic_fec_batch_stats_t st;
+    pquic_fec_batch_get_stats(b, &st);
+    pquic_fec_batcher_destroy(b);
+    qsort(g_lat, g_nlat, sizeof *g_lat, cmp_u64);
+    out[0] = nblocks * bytes_per_block / wall / 1073741824.0;
+    out[1] = g_nlat ? (double)g_lat[g_nlat / 2] : 0;
+    out[2] = g_nlat ? (double)g_lat[(long)(g_nlat * 0.99)] : 0;
+    out[3] = g_nlat ? (double)g_lat[g_nlat - 1] : 0;
+    out[4] = (double)(st.batches - st0.batches);
+    out[5] = wall;
+    out[6] = (double)(st.completed - st0.completed);
+    out[7] = out[4] > 0 ? out[6] / out[4] : 0;
+    free(slots); free(pool); free(ss); free(g_lat); free(cnx);
+    g_lat = NULL;
+    return 0;
+}
