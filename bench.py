@@ -376,6 +376,22 @@ def main():
         legs.update(pcie_legs(torch, args, dev))
         legs.update(batching_legs(dev.index or 0, args))
     if not args.no_legs and world == 1:
+        # §8f row 2: the repair symbols of the whole batch as FEC frames (header + payload) on the device
+        fstride = (14 + L + 15) // 16 * 16
+        frames = torch.empty(nb * r * fstride, dtype=torch.uint8, device=dev)
+        eng.write_repair_frames(rep, frames, nb, r, L, L, fstride, k, r, fbn_base=fbn_base)
+        a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(5):
+            eng.write_repair_frames(rep, frames, nb, r, L, L, fstride, k, r, fbn_base=fbn_base)
+        b_.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b_) / 5
+        fb = nb * r * (L + fstride)  # read the repairs, write the frame slots
+        legs["repair_frames_k16_r4"] = {"kernel": "k_write_repair_frames", "frames": nb * r, "frame_stride": fstride,
+                                        "ms": round(ms, 3), "algorithmic_GB_s": round(fb / (ms * 1e-3) / 1e9, 1)}
+        del frames
+    if not args.no_legs and world == 1:
         # north-star leg: k = 32, r = 8 encode, 2^21 blocks (one GPU's share of config 4)
         nb2, k2, r2 = 1 << 21, 32, 8
         del src, rep

@@ -132,6 +132,17 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
                            uint32_t k, uint32_t symbol_size, const uint64_t *src_present,
                            const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
 
+/* FEC frames for a batch of repair symbols, ready for packet buffers (the block framework's
+ * get_repair_payload_from_queue + write_fec_frame, block_framework_sender.h:100-133,
+ * protoops/write_fec_frame.c; wire format in pquic_fec_frames.h).  Frame b*r + i, at
+ * frames + (b*r + i) * frame_stride, is the 14-byte header {fin 1, data_length, offset 1,
+ * repair FPID (fbn_b << 8) | i, nss, nrs} followed by the first data_length bytes of rep[b][i];
+ * the rest of the slot is zeroed.  Device buffers; symbol_size and frame_stride multiples of 4,
+ * frame_stride >= 14 + data_length. */
+int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, uint32_t symbol_size,
+                               uint16_t data_length, uint32_t fbn_base, const uint32_t *fbn, uint8_t nss, uint8_t nrs,
+                               void *frames, uint32_t frame_stride, void *stream);
+
 /* Page-locked host memory for staging buffers (hipHostMalloc / hipHostFree), so callers in
  * C need no HIP headers.  NULL on failure. */
 void *fecgpu_host_alloc(size_t bytes);

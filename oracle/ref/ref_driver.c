@@ -26,7 +26,7 @@
 #include <unistd.h>
 
 #include <stddef.h>
-#include "fec/fec.h"             /* resolved with -I$(REF)/plugins */
+#include "fec/fec_protoops.h"     /* fec.h + frame helpers; resolved with -I$(REF)/plugins */
 #include "fec/prng/tinymt32.c"
 
 /* ---- pluglet API stubs ---- */
@@ -249,4 +249,84 @@ int ref_layout(uint64_t *out) {
     out[6] = offsetof(repair_symbol_t, data);
     out[7] = sizeof(repair_fpid_t);
     return 8;
+}
+
+/* ---- frame codecs ---------------------------------------------------
+ * FEC frame header and SFPID frame: the reference's own inline helpers (fec.h:175-194,
+ * fec_protoops.h:92-100).  RECOVERED frame: the reference pluglets write_simple_recovered_frame.c
+ * and parse_simple_recovered_frame.c, compiled in place and run through the stubs above. */
+int ref_write_fec_frame_header(int fin, int data_length, int offset, uint64_t fpid_raw, int nss, int nrs,
+                               uint8_t *out) {
+    fec_frame_header_t h;
+    memset(&h, 0, sizeof h);
+    h.fin_bit = fin;
+    h.data_length = data_length;
+    h.offset = offset;
+    h.repair_fec_payload_id.raw = fpid_raw;
+    h.nss = nss;
+    h.nrs = nrs;
+    write_fec_frame_header(&h, out);
+    return 1 + (int)sizeof(fec_frame_header_t);
+}
+
+void ref_parse_fec_frame_header(const uint8_t *in, uint64_t *fields) {
+    fec_frame_header_t h;
+    memset(&h, 0, sizeof h);
+    parse_fec_frame_header(&h, (uint8_t *)in + 1);
+    fields[0] = h.fin_bit;
+    fields[1] = h.data_length;
+    fields[2] = h.offset;
+    fields[3] = h.repair_fec_payload_id.raw;
+    fields[4] = h.nss;
+    fields[5] = h.nrs;
+}
+
+int ref_write_sfpid_frame(uint32_t raw, uint8_t *out, size_t bytes_max) {
+    source_fpid_frame_t f;
+    size_t consumed = 0;
+    f.source_fpid.raw = raw;
+    int ret = helper_write_source_fpid_frame(NULL, &f, out, bytes_max, &consumed);
+    return ret ? -ret : (int)consumed;
+}
+
+uint32_t ref_parse_sfpid_frame(const uint8_t *in) {
+    source_fpid_frame_t f;
+    parse_sfpid_frame(&f, (uint8_t *)in + 1);
+    return f.source_fpid.raw;
+}
+
+protoop_arg_t ref_write_recovered_frame(picoquic_cnx_t *cnx);
+protoop_arg_t ref_parse_recovered_frame(picoquic_cnx_t *cnx);
+
+/* returns the pluglet's value; *consumed = output[0] */
+long ref_write_recovered(const uint64_t *packets, int n, uint8_t *bytes, long bytes_len, long *consumed) {
+    recovered_packets_t *rp = malloc(sizeof *rp);
+    rp->packets = malloc(sizeof(uint64_t) * (n ? n : 1));
+    memcpy(rp->packets, packets, sizeof(uint64_t) * n);
+    rp->number_of_packets = (uint8_t)n;
+    memset(g_in, 0, sizeof g_in);
+    memset(g_out, 0, sizeof g_out);
+    g_in[0] = (protoop_arg_t)bytes;
+    g_in[1] = (protoop_arg_t)(bytes + bytes_len);
+    g_in[2] = (protoop_arg_t)rp;
+    long ret = (long)ref_write_recovered_frame(NULL);  /* frees rp */
+    *consumed = (long)g_out[0];
+    return ret;
+}
+
+/* returns bytes consumed (parse return - bytes) or -1 for NULL; packets/n from output[0] */
+long ref_parse_recovered(const uint8_t *bytes, long bytes_len, uint64_t *packets, int *n) {
+    memset(g_in, 0, sizeof g_in);
+    memset(g_out, 0, sizeof g_out);
+    g_in[0] = (protoop_arg_t)bytes;
+    g_in[1] = (protoop_arg_t)(bytes + bytes_len);
+    protoop_arg_t end = ref_parse_recovered_frame(NULL);
+    uint8_t *sp = (uint8_t *)g_out[0];
+    *n = 0;
+    if (sp) {
+        *n = sp[0];
+        memcpy(packets, sp + 1, sizeof(uint64_t) * sp[0]);
+        free(sp);
+    }
+    return end ? (long)((const uint8_t *)end - bytes) : -1;
 }

@@ -1051,6 +1051,58 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
   }
 }
 
+// FEC frames for batched repair symbols (the block framework's get_repair_payload_from_queue +
+// write_fec_frame, block_framework_sender.h:100-133, protoops/write_fec_frame.c): frame (b, i) =
+// 0x2a | BE16(len << 1 | fin=1) | offset=1 | BE64((fbn_b << 8) | i) | nss | nrs | repair bytes.
+// One thread per output dword; the payload sits 14 bytes into the frame, so each output dword
+// is assembled from two aligned source dwords with v_alignbyte.  Bytes past 14 + len are zeroed.
+__device__ __forceinline__ uint32_t frame_header_byte(int o, uint32_t len, uint64_t raw, uint32_t nss, uint32_t nrs) {
+  const uint32_t v16 = (len << 1) | 1u;
+  switch (o) {
+    case 0: return 0x2a;
+    case 1: return (v16 >> 8) & 0xff;
+    case 2: return v16 & 0xff;
+    case 3: return 1;
+    case 12: return nss;
+    case 13: return nrs;
+    default: return (uint32_t)(raw >> (8 * (11 - o))) & 0xff;  // o = 4..11, big-endian
+  }
+}
+
+__global__ void k_write_repair_frames(const uint32_t *__restrict__ rep, uint64_t nframes, uint32_t r, uint32_t Lw,
+                                      uint32_t len, uint32_t fbn_base, const uint32_t *fbn, uint32_t nss,
+                                      uint32_t nrs, uint32_t *__restrict__ frames, uint32_t fw) {
+  const uint64_t total = nframes * fw;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t f = t / fw;
+    const uint32_t w = (uint32_t)(t - f * fw);
+    const uint64_t b = f / r;
+    const uint32_t i = (uint32_t)(f - b * r);
+    const uint32_t *row = rep + f * (uint64_t)Lw;
+    uint32_t out;
+    if (w >= 4) {  // bytes 4w .. 4w+3 = payload bytes 4w-14 .. 4w-11 = row dwords (w-4) [2..3], (w-3) [0..1]
+      const uint32_t lo = (w - 4) < Lw ? row[w - 4] : 0u, hi = (w - 3) < Lw ? row[w - 3] : 0u;
+      out = __builtin_amdgcn_alignbyte(hi, lo, 2);
+    } else {
+      const uint32_t fb = fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
+      const uint64_t raw = ((uint64_t)fb << 8) | i;
+      out = 0;
+      for (int q = 0; q < 4; q++) {
+        const int o = 4 * (int)w + q;
+        const uint32_t byte = o < 14 ? frame_header_byte(o, len, raw, nss, nrs)
+                                     : (row[0] >> (8 * (o - 14))) & 0xff;  // o = 14, 15: payload 0, 1
+        out |= byte << (8 * q);
+      }
+    }
+    // zero the bytes past the frame's end (14 + len) within the slot
+    const int valid = (int)(14 + len) - 4 * (int)w;
+    if (valid <= 0) out = 0;
+    else if (valid < 4) out &= (1u << (8 * valid)) - 1u;
+    frames[f * fw + w] = out;
+  }
+}
+
 __global__ void k_synth_fill(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t offset) {
   // one 8-byte word of the stream per thread; unaligned head/tail handled bytewise
   const uint64_t first = offset >> 3, last = (offset + nbytes + 7) >> 3;
@@ -1401,6 +1453,23 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   HIPCHK(hipGetLastError());
   g_stats[2]++;
   g_stats[3] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, uint32_t symbol_size,
+                               uint16_t data_length, uint32_t fbn_base, const uint32_t *fbn, uint8_t nss, uint8_t nrs,
+                               void *frames, uint32_t frame_stride, void *stream) {
+  if (!rep || !frames) return set_err(FECGPU_ERR_INVALID, "%s", "NULL buffer");
+  if (symbol_size % 4 || frame_stride % 4) return set_err(FECGPU_ERR_INVALID, "%s", "sizes must be multiples of 4");
+  if (data_length > symbol_size || data_length > 0x7fff || frame_stride < 14u + data_length)
+    return set_err(FECGPU_ERR_INVALID, "%s", "data_length exceeds the symbol, 15 bits or the frame slot");
+  if (!nblocks || !r) return FECGPU_OK;
+  const uint64_t nf = nblocks * r, total = nf * (frame_stride / 4);
+  const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
+  hipLaunchKernelGGL(k_write_repair_frames, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint32_t *)rep, nf,
+                     r, symbol_size / 4, (uint32_t)data_length, fbn_base, fbn, (uint32_t)nss, (uint32_t)nrs,
+                     (uint32_t *)frames, frame_stride / 4);
+  HIPCHK(hipGetLastError());
   return FECGPU_OK;
 }
 

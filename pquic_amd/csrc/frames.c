@@ -1,0 +1,107 @@
+/*
+ * pquic_amd/csrc/frames.c -- wire codecs of the FEC plugin's frames (include/pquic_fec_frames.h).
+ * Host C; each function cites the reference code it restates.
+ */
+#include "pquic_fec_frames.h"
+
+#include <string.h>
+
+static void put_be(uint64_t v, uint8_t *b, int n) {  /* encode_un (fec.h) */
+    for (int i = 0; i < n; i++) b[i] = (uint8_t)(v >> (8 * (n - i - 1)));
+}
+
+static uint64_t get_be(const uint8_t *b, int n) {  /* decode_un (fec.h) */
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | b[i];
+    return v;
+}
+
+size_t pquic_fec_write_fec_frame_header(const pquic_fec_frame_header_t *h, uint8_t *out) {
+    out[0] = PQUIC_FEC_FEC_TYPE;
+    /* the packed header's first u16: fin_bit is bit 0, data_length bits 1..15 */
+    put_be((uint16_t)((h->fin & 1u) | ((uint32_t)(h->data_length & 0x7fffu) << 1)), out + 1, 2);
+    out[3] = h->offset;
+    put_be(h->repair_fpid_raw, out + 4, 8);
+    out[12] = h->nss;
+    out[13] = h->nrs;
+    return PQUIC_FEC_FRAME_HEADER_BYTES;
+}
+
+void pquic_fec_parse_fec_frame_header(const uint8_t *in, pquic_fec_frame_header_t *h) {
+    const uint16_t v = (uint16_t)get_be(in + 1, 2);
+    h->fin = v & 1u;
+    h->data_length = v >> 1;
+    h->offset = in[3];
+    h->repair_fpid_raw = get_be(in + 4, 8);
+    h->nss = in[12];
+    h->nrs = in[13];
+}
+
+int pquic_fec_write_sfpid_frame(uint32_t source_fpid_raw, uint8_t *out, size_t bytes_max, size_t *consumed) {
+    if (bytes_max < 5) return PQUIC_FEC_FRAME_BUFFER_TOO_SMALL;
+    out[0] = PQUIC_FEC_SOURCE_FPID_TYPE;
+    put_be(source_fpid_raw, out + 1, 4);
+    *consumed = 5;
+    return 0;
+}
+
+uint32_t pquic_fec_parse_sfpid_frame(const uint8_t *in) { return (uint32_t)get_be(in + 1, 4); }
+
+int pquic_fec_write_recovered_frame(const uint64_t *packets, uint8_t n, uint8_t *bytes, const uint8_t *bytes_max,
+                                    size_t *consumed) {
+    *consumed = 0;
+    if (n == 0 || bytes_max - bytes < 10) return -1;  /* :27-33 */
+    size_t c = 0;
+    bytes[c++] = PQUIC_FEC_RECOVERED_TYPE;
+    bytes[c++] = n;
+    memcpy(bytes + c, &packets[0], 8);  /* host byte order, as the reference's my_memcpy */
+    c += 8;
+    uint8_t range_length = 0;
+    for (int i = 1; i < n; i++) {
+        if (packets[i] <= packets[i - 1] || packets[i] - packets[i - 1] > 0xFF) return -1;  /* :45-50 */
+        /* the reference's "equal packet extends the range" branch (:51-52) is unreachable
+         * after the strict-increase check: every packet is written as (range 0, gap) */
+        if (bytes_max - (bytes + c) < 2) return -1;
+        bytes[c++] = range_length;
+        bytes[c++] = (uint8_t)(packets[i] - packets[i - 1]);
+        range_length = 0;
+    }
+    *consumed = c;
+    return 0;
+}
+
+const uint8_t *pquic_fec_parse_recovered_frame(const uint8_t *bytes, const uint8_t *bytes_max, uint64_t *packets,
+                                               uint8_t *n_out) {
+    *n_out = 0;
+    if (bytes_max - bytes < 10) return NULL;  /* :21-27 */
+    const uint8_t *p = bytes + 1;
+    const uint8_t n = *p++;
+    uint64_t last;
+    memcpy(&last, p, 8);
+    p += 8;
+    packets[0] = last;
+    int count = 1, is_gap = 0;
+    while (count < n && p < bytes_max) {
+        const uint8_t range = *p++;
+        if (!is_gap) {
+            if (count + range > n) return NULL;  /* :44-50 */
+            for (int j = 0; j < range; j++) packets[count++] = ++last;
+            is_gap = 1;
+        } else {
+            const uint8_t skip = (uint8_t)(range + 1);  /* uint8_t n_packets_to_skip: 255 wraps to 0 (:61) */
+            last += (uint64_t)skip + 1;
+
+            packets[count++] = last;
+            is_gap = 0;
+        }
+    }
+    if (count != n) return NULL;  /* :69-75 (also n == 0) */
+    *n_out = n;
+    return p;
+}
+
+size_t pquic_fec_source_symbol_header(uint64_t packet_number, uint8_t *out) {
+    out[0] = PQUIC_FEC_MAGIC_NUMBER;
+    put_be(packet_number, out + 1, 8);
+    return PQUIC_FEC_SOURCE_SYMBOL_HEADER_BYTES;
+}

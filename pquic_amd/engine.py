@@ -43,6 +43,7 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_rlc_encode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v]
     L.fecgpu_xor_encode.argtypes = [v, v, u64, u32, u32, v]
     L.fecgpu_rlc_window_encode.argtypes = [v, u64, u32, u32, u32, u32, v, v]
+    L.fecgpu_write_repair_frames.argtypes = [v, u64, u32, u32, C.c_uint16, u32, v, C.c_uint8, C.c_uint8, v, u32, v]
     L.fecgpu_rlc_decode_workspace.argtypes = [u64, u32, u32]
     L.fecgpu_rlc_decode_workspace.restype = sz
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
@@ -118,6 +119,14 @@ class Engine:
         self._check(self.lib.fecgpu_rlc_window_encode(_addr(symbols), nwindows, step, k, r, L, _addr(rep),
                                                       self._stream(stream)), "fecgpu_rlc_window_encode")
         return rep
+
+    def write_repair_frames(self, rep, frames, nblocks: int, r: int, L: int, data_length: int, frame_stride: int,
+                            nss: int, nrs: int, fbn_base: int = 0, fbn=None, stream=None):
+        """FEC frames (header + payload) for every repair of a batch, on the device."""
+        self._check(self.lib.fecgpu_write_repair_frames(_addr(rep), nblocks, r, L, data_length, fbn_base, _addr(fbn),
+                                                        nss, nrs, _addr(frames), frame_stride, self._stream(stream)),
+                    "fecgpu_write_repair_frames")
+        return frames
 
     def xor_encode(self, src, rep, k: int, L: int, nblocks: int | None = None, stream=None):
         nb = nblocks if nblocks is not None else src.numel() // (k * L)
