@@ -110,7 +110,8 @@ def test_source_symbol_header(lib):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nb,r,L,dlen,stride", [(257, 4, 1200, 1200, 1216), (33, 8, 1200, 1000, 1400),
-                                                (5, 16, 9000, 8998, 9016), (64, 1, 8, 3, 20)])
+                                                (5, 16, 9000, 8998, 9016), (64, 1, 8, 3, 20),
+                                                (33, 8, 1200, 1000, 1216), (40, 3, 1600, 1590, 1616)])
 def test_device_repair_frames(lib, nb, r, L, dlen, stride):
     """fecgpu_write_repair_frames vs the host codec (itself pinned to the reference) + payload."""
     import numpy as np
