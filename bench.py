@@ -47,15 +47,18 @@ def parse():
     return p.parse_args()
 
 
-def load_traffic(kernel_tag: str):
-    """HBM bytes per launch from the committed PMC profile (profiles/*_pmc.json), if any."""
+def load_traffic(kernel_tag: str, blocks: int | None = None):
+    """HBM bytes per launch from the committed PMC profile (profiles/pmc_traffic.json), scaled to
+    `blocks` when the profile recorded its per-block figure."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            d = json.load(f)
-        v = d.get(kernel_tag, {}).get("hbm_bytes_per_launch_corrected")
+            d = json.load(f).get(kernel_tag, {})
+        if blocks and d.get("hbm_bytes_per_block_corrected"):
+            return float(d["hbm_bytes_per_block_corrected"]) * blocks
+        v = d.get("hbm_bytes_per_launch_corrected")
         return float(v) if v else None
     except Exception:
         return None
@@ -364,12 +367,12 @@ def main():
         "rlc_encode_k16_r4": {"kernel": "k_rlc_encode_bs<4,16>", "ms": round(enc_ms, 3),
                               "payload_GiB_s": round(payload / (enc_ms * 1e-3) / 2**30, 2),
                               "algorithmic_GB_s": round(enc_gbs, 1), "hbm_frac": round(enc_gbs / HBM_PEAK_GBS, 4),
-                              "bytes_per_launch": enc_bytes, "traffic": load_traffic("rlc_encode_k16_r4")},
+                              "bytes_per_launch": enc_bytes, "traffic": load_traffic("rlc_encode_k16_r4", nb)},
         "rlc_decode_k16_e4": {"ms": round(dec_ms, 3), "plan_ms": round(plan_ms, 3), "apply_ms": round(apply_ms, 3),
                               "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
                               "apply_kernel": "k_rlc_recover_bs<4,16>", "apply_algorithmic_GB_s": round(app_gbs, 1),
                               "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
-                              "ref_ub_blocks": n_ub, "traffic": load_traffic("rlc_decode_apply_k16_e4")},
+                              "ref_ub_blocks": n_ub, "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)},
     }
     del work, ws
     if not args.no_legs and not args.no_pcie and world == 1:
@@ -388,7 +391,7 @@ def main():
         torch.cuda.synchronize()
         ms = a.elapsed_time(b_) / 5
         fb = nb * r * (L + fstride)  # read the repairs, write the frame slots
-        legs["repair_frames_k16_r4"] = {"kernel": "k_write_repair_frames", "frames": nb * r, "frame_stride": fstride,
+        legs["repair_frames_k16_r4"] = {"kernel": "k_write_repair_frames16", "frames": nb * r, "frame_stride": fstride,
                                         "ms": round(ms, 3), "algorithmic_GB_s": round(fb / (ms * 1e-3) / 1e9, 1)}
         del frames
     if not args.no_legs and world == 1:
@@ -412,7 +415,7 @@ def main():
         legs["rlc_encode_k32_r8"] = {"ms": round(ms, 3), "blocks": nb2,
                                      "payload_GiB_s": round(nb2 * k2 * L / (ms * 1e-3) / 2**30, 2),
                                      "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
-                                     "traffic": load_traffic("rlc_encode_k32_r8")}
+                                     "traffic": load_traffic("rlc_encode_k32_r8", nb2)}
         del s2, r2t
         torch.cuda.empty_cache()
         # configs[4]: jumbo 9000-B symbols, k = 64 r = 16, encode + decode of 16 erasures
@@ -424,11 +427,11 @@ def main():
         if enc_ms >= apply_ms:
             roof = {"bound": "hbm", "kernel": "k_rlc_encode_bs<4,16> (RLC encode k=16 r=4)",
                     "achieved": round(enc_gbs, 1), "bytes_per_launch": enc_bytes, "launch_ms": round(enc_ms, 4),
-                    "traffic": load_traffic("rlc_encode_k16_r4")}
+                    "traffic": load_traffic("rlc_encode_k16_r4", nb)}
         else:
             roof = {"bound": "hbm", "kernel": "k_rlc_recover_bs<4,16> (RLC decode apply k=16 e=4)",
                     "achieved": round(app_gbs, 1), "bytes_per_launch": app_bytes, "launch_ms": round(apply_ms, 4),
-                    "traffic": load_traffic("rlc_decode_apply_k16_e4")}
+                    "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)}
         roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),
                      "measured_copy_peak": MEASURED_COPY_GBS,
                      "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4)})
