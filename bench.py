@@ -288,10 +288,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal knobs for a box with fewer GPUs than ranks (never set by the driver):
+    # PQUIC_BENCH_SHARE_GPU=1 maps rank -> device local % count, PQUIC_BENCH_BACKEND=gloo
+    # because RCCL refuses two ranks on one device
+    backend = os.environ.get("PQUIC_BENCH_BACKEND", "nccl")
+    if os.environ.get("PQUIC_BENCH_SHARE_GPU") == "1":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     eng = Engine(local)
@@ -352,7 +358,7 @@ def main():
     enc_ms, plan_ms, apply_ms = seg  # apply includes the zero/undetermined rule (fused for e <= 16)
     dec_ms = plan_ms + apply_ms
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
