@@ -172,6 +172,20 @@ class Engine:
         rec(2)
         return status, recovered
 
+    def rlc_decode_plan(self, src_present, rep_present, k, r, nblocks, workspace, fbn_base=0, fbn=None,
+                        stream=None):
+        """fecgpu_rlc_decode_plan: coefficient-only stage (needs only the presence masks)."""
+        self._check(self.lib.fecgpu_rlc_decode_plan(nblocks, k, r, fbn_base, _addr(fbn), _addr(src_present),
+                                                    _addr(rep_present), _addr(workspace), workspace.numel(),
+                                                    self._stream(stream)), "fecgpu_rlc_decode_plan")
+
+    def rlc_decode_apply(self, src, rep, status, recovered, k, r, L, nblocks, workspace, stream=None):
+        """fecgpu_rlc_decode_apply: the data pass plus the zero/undetermined rule."""
+        self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
+                                                     _addr(recovered), _addr(workspace), workspace.numel(),
+                                                     self._stream(stream)), "fecgpu_rlc_decode_apply")
+        return status, recovered
+
     def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,
                    nblocks: int | None = None, stream=None):
         nb = nblocks if nblocks is not None else src.numel() // (k * L)
