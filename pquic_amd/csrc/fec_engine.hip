@@ -564,6 +564,189 @@ __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, i
 #undef AR
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-resident lane-per-block plan for small systems (k <= 4 * KD, e_max <= EM; configs 2-4).
+// The same replay as k_rlc_plan_lane, with the lane's system held in VGPRs instead of an LDS
+// arena: A rows as packed bytes (u64), V rows as KD dwords.  sort_system's row permutation is
+// applied physically (predicated swaps), so the rows leave in P order and need no indirection.
+// Row operations multiply a packed row by the lane's scalar with the v_perm product tables of
+// fec_device.h (4 bytes per v_perm triple); scalar inverses and products use the log/exp tables
+// in LDS.  GF arithmetic is exact, so every byte equals the reference's (rlc_fec_scheme_gf256.c
+// :28-115, 178-236), and a zero diagonal after elimination is the reference's crash (:74-77).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t gf_mulc(uint32_t x, const PermTab &t) {
+  return gf_mac(0u, perm_selectors(x), t.t01, t.t2);
+}
+
+template <int EM>
+__device__ __forceinline__ uint64_t gf_mulc_row(uint64_t x, const PermTab &t) {
+  if constexpr (EM <= 4) return (uint64_t)gf_mulc((uint32_t)x, t);
+  else return (uint64_t)gf_mulc((uint32_t)x, t) | ((uint64_t)gf_mulc((uint32_t)(x >> 32), t) << 32);
+}
+
+__device__ __forceinline__ uint32_t col8(uint64_t row, int i) { return (uint32_t)(row >> (8 * i)) & 0xffu; }
+
+template <int KD, int EM>
+__global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                     const uint32_t *fbn, const uint64_t *sp,
+                                                     const uint64_t *rp, uint8_t *ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  const int em = (int)L.em;
+  const uint8_t *EXP = lds, *LOG = lds + 512;
+  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  __syncthreads();
+  const uint32_t orow = plan_out_row(L.stride);
+  uint8_t *h = lds + 768 + (size_t)lane * orow;  // this lane's workspace record (LDS copy)
+  const uint64_t kmask = k < 64 ? (1ull << k) - 1 : ~0ull;
+  for (uint64_t base = (uint64_t)blockIdx.x * 64; base < nblocks; base += (uint64_t)gridDim.x * 64) {
+    const uint64_t b = base + lane;
+    if (b < nblocks) do {
+      const uint64_t s0 = sp[2 * b] & kmask;  // k <= 32: the high word never matters
+      uint64_t q0 = rp[2 * b], q1 = rp[2 * b + 1];
+      clip128(q0, q1, r);
+      const int cur_ss = __popcll(s0);
+      const int cur_rs = __popcll(q0) + __popcll(q1);
+      if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
+        h[0] = FECGPU_BLOCK_NOTHING;
+        h[1] = 0;
+        break;
+      }
+      const int n = k - cur_ss;  // <= em <= EM
+      const uint64_t miss = ~s0 & kmask;
+      uint64_t U = 0, S = 0;  // unknown source ids / selected repair ids, one byte each
+      {
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          if ((miss >> j) & 1) U |= (uint64_t)j << (8 * u++);
+        int e = 0;
+        for (int i = 0; i < r && e < n; i++)
+          if (bit128(q0, q1, i)) S |= (uint64_t)i << (8 * e++);
+      }
+      uint64_t A[EM];
+      uint32_t V[EM][KD];
+#pragma unroll
+      for (int e = 0; e < EM; e++) {
+        A[e] = 0;
+#pragma unroll
+        for (int d = 0; d < KD; d++) V[e][d] = 0;
+      }
+      const uint32_t f = block_fbn(b, fbn_base, fbn);
+#pragma unroll
+      for (int e = 0; e < EM; e++) {  // system rows, :194-212
+        if (e < n) {
+          Tmt t;
+          tmt_init(t, rlc_seed(f, col8(S, e)));
+          int u = 0;
+#pragma unroll
+          for (int j = 0; j < 4 * KD; j++) {
+            if (j < k) {
+              const uint32_t c = tmt_coef(t);
+              const bool ms = (miss >> j) & 1;
+              V[e][j >> 2] |= (ms ? (uint32_t)(u == e) : c) << (8 * (j & 3));
+              if (ms) A[e] |= (uint64_t)c << (8 * u++);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EM; i++) {  // sort_system :28-40 (first maximum wins; rows swapped in place)
+        if (i < n) {
+          int mx = i;
+          uint32_t best = col8(A[i], i);
+#pragma unroll
+          for (int j = i + 1; j < EM; j++)
+            if (j < n && best < col8(A[j], i)) { best = col8(A[j], i); mx = j; }
+#pragma unroll
+          for (int j = i + 1; j < EM; j++) {
+            if (j == mx) {
+              const uint64_t ta = A[i]; A[i] = A[j]; A[j] = ta;
+#pragma unroll
+              for (int d = 0; d < KD; d++) { const uint32_t tv = V[i][d]; V[i][d] = V[j][d]; V[j][d] = tv; }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EM - 1; i++) {  // elimination without re-pivoting :54-70
+        const uint32_t piv = col8(A[i], i);
+        if (i < n - 1 && piv) {
+          const uint32_t lip = 255u - LOG[piv];
+#pragma unroll
+          for (int kk = i + 1; kk < EM; kk++) {
+            const uint32_t a = col8(A[kk], i);
+            if (kk < n && a) {
+              const PermTab T = perm_table(EXP[LOG[a] + lip]);  // a / piv
+              A[kk] ^= gf_mulc_row<EM>(A[i], T);
+#pragma unroll
+              for (int d = 0; d < KD; d++)
+                if (4 * d < k) V[kk][d] ^= gf_mulc(V[i][d], T);
+            }
+          }
+        }
+      }
+      bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
+#pragma unroll
+      for (int i = 0; i < EM; i++) ub |= i < n && col8(A[i], i) == 0;
+      if (ub) {
+        h[0] = FECGPU_BLOCK_REF_UB;
+        h[1] = 0;
+        break;
+      }
+#pragma unroll
+      for (int i = EM - 1; i >= 0; i--) {  // back substitution :71-114; X_i replaces row i
+        if (i < n) {
+#pragma unroll
+          for (int u = i + 1; u < EM; u++) {
+            const uint32_t a = col8(A[i], u);
+            if (u < n && a) {
+              const PermTab T = perm_table(a);
+#pragma unroll
+              for (int d = 0; d < KD; d++)
+                if (4 * d < k) V[i][d] ^= gf_mulc(V[u][d], T);
+            }
+          }
+          const PermTab T = perm_table(EXP[255u - LOG[col8(A[i], i)]]);  // 1 / diagonal
+#pragma unroll
+          for (int d = 0; d < KD; d++)
+            if (4 * d < k) V[i][d] = gf_mulc(V[i][d], T);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EM; i++) {
+        if (i < n) {
+          uint8_t *D = h + L.off_D + i * k;
+#pragma unroll
+          for (int j = 0; j < 4 * KD; j++)
+            if (j < k) D[j] = (uint8_t)(V[i][j >> 2] >> (8 * (j & 3)));
+          for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && col8(A[i], u) != 0;
+          h[L.off_nz + i] = 0;
+          h[L.off_unk + i] = (uint8_t)col8(U, i);
+          h[L.off_sel + i] = (uint8_t)col8(S, i);
+        }
+      }
+      {
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          h[L.off_slot + j] = ((miss >> j) & 1) ? (uint8_t)(0x80 | col8(S, u++)) : (uint8_t)j;
+      }
+      h[0] = FECGPU_BLOCK_RECOVERED;
+      h[1] = (uint8_t)n;
+    } while (0);
+    __syncthreads();
+    const uint32_t nrows = nblocks - base < 64 ? (uint32_t)(nblocks - base) : 64u;
+    const uint32_t rdw = L.stride / 4, odw = orow / 4;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
+    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(lds + 768);
+    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
+      const uint32_t row = x / rdw;
+      dst[x] = srcw[row * odw + (x - row * rdw)];
+    }
+    __syncthreads();
+  }
+}
+
 template <int RT, int W>
 __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
                                                     const uint32_t *__restrict__ rep, uint64_t nblocks,
@@ -1392,10 +1575,24 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const size_t lane_lds = plan_lane_lds(k, r);
-  static int force = -1;  // FECGPU_PLAN=wave|lane overrides the size rule (A/B experiments)
-  if (force < 0) {
-    const char *e = getenv("FECGPU_PLAN");
-    force = e && !strcmp(e, "wave") ? 1 : e && !strcmp(e, "lane") ? 2 : 0;
+  // FECGPU_PLAN=reg|lane|wave overrides the size rule (A/B experiments, cross-checks in the tests);
+  // read per call so a test process can compare the plan kernels on the same inputs
+  const char *pe = getenv("FECGPU_PLAN");
+  const int force = pe && !strcmp(pe, "wave") ? 1 : pe && !strcmp(pe, "lane") ? 2 : pe && !strcmp(pe, "reg") ? 3 : 0;
+  const uint32_t em = ws_layout(k, r).em;
+  if ((force == 0 || force == 3) && k <= 32 && em <= 8) {
+    const size_t reg_lds = 768 + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
+    const uint64_t groups = (nblocks + 63) / 64;
+#define FEC_PLAN_REG(KD, EM)                                                                         \
+  hipLaunchKernelGGL((k_rlc_plan_reg<KD, EM>), dim3(grid_for(groups)), dim3(64), reg_lds, s, nblocks, \
+                     (int)k, (int)r, fbn_base, fbn, src_present, rep_present, ws)
+    if (k <= 16 && em <= 4) FEC_PLAN_REG(4, 4);
+    else if (k <= 16) FEC_PLAN_REG(4, 8);
+    else if (em <= 4) FEC_PLAN_REG(8, 4);
+    else FEC_PLAN_REG(8, 8);
+#undef FEC_PLAN_REG
+    HIPCHK(hipGetLastError());
+    return FECGPU_OK;
   }
   if (force != 1 && (lane_lds <= 64 * 1024 || force == 2) && lane_lds <= 160 * 1024) {
     if (lane_lds > 65536) {

@@ -436,6 +436,9 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     NP = 32 // VEC
     budget3 = int(os.environ.get("FEC_GEN_VGPR3", "168"))
     fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - 1) <= 63
+    forced = os.environ.get(f"FEC_GEN_LIMIT_RT{RT}")  # A/B: VGPR limit for this tile size
+    if forced:
+        return max([P for P in range(2, 33) if fits(P, int(forced))] or [2])
     p3 = max([P for P in range(2, 33) if fits(P, budget3)] or [0])
     if p3 >= 4:
         return min(p3, int(os.environ.get("FEC_GEN_PMAX", "8")))

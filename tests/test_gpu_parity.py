@@ -390,3 +390,67 @@ def test_window_decode_vs_oracle(eng, oracle):
         for j in bits(rec[w], k):
             assert np.array_equal(got[w, j], src_h[w, j])
     assert (st == DEC_RECOVERED).sum() > nw // 2
+
+
+def _ws_fields(ws, k, r, n_blocks):
+    """Meaningful fields of each decode-plan record (unwritten bytes are scratch)."""
+    em = min(k, r)
+    p16 = lambda x: (x + 15) & ~15  # noqa: E731
+    off_unk = 16
+    off_sel = off_unk + p16(em)
+    off_slot = off_sel + p16(em)
+    off_nz = off_slot + p16(k)
+    off_D = off_nz + p16(em)
+    off_dep = off_D + p16(em * k)
+    stride = off_dep + p16(em * em)
+    out = []
+    for b in range(n_blocks):
+        h = ws[b * stride:(b + 1) * stride]
+        st, n = int(h[0]), int(h[1])
+        if st != DEC_RECOVERED:
+            out.append((st,))
+            continue
+        out.append((st, n, h[off_unk:off_unk + n].tobytes(), h[off_sel:off_sel + n].tobytes(),
+                    h[off_slot:off_slot + k].tobytes(), h[off_nz:off_nz + n].tobytes(),
+                    h[off_D:off_D + n * k].tobytes(),
+                    b"".join(h[off_dep + i * em: off_dep + i * em + n].tobytes() for i in range(n))))
+    return out
+
+
+@pytest.mark.parametrize("k,r,nb", [(1, 1, 64), (4, 1, 300), (16, 4, 2000), (12, 6, 700), (16, 8, 500),
+                                    (30, 3, 400), (32, 8, 600), (9, 9, 300)])
+def test_plan_kernels_agree(eng, k, r, nb):
+    """The three plan kernels (register lane-per-block, LDS lane-per-block, wave-per-block)
+    write identical decode records -- same unknowns, repair selection, solution rows D,
+    dependency flags, and the same reference-crash verdicts -- on random erasure patterns."""
+    import os
+    rng = np.random.default_rng(k * 1000 + r)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        e = int(rng.integers(0, min(k, r) + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        nrep = int(rng.integers(max(0, e - 1), r + 1))
+        rp[b] = masks_from_lists(1, r, [rng.choice(r, nrep, replace=False).tolist()])[0]
+    fbn = torch.from_numpy(rng.integers(0, 1 << 24, nb, dtype=np.int64).astype(np.int32)).to(DEV)
+    spd, rpd = to_dev(sp), to_dev(rp)
+    res = {}
+    old = os.environ.get("FECGPU_PLAN")
+    try:
+        for kind in ("reg", "lane", "wave"):
+            os.environ["FECGPU_PLAN"] = kind
+            ws = eng.alloc_workspace(nb, k, r)
+            ws.fill_(0xEE)
+            eng.rlc_decode_plan(spd, rpd, k, r, nb, ws, fbn=fbn)
+            torch.cuda.synchronize()
+            res[kind] = _ws_fields(ws.cpu().numpy(), k, r, nb)
+    finally:
+        if old is None:
+            os.environ.pop("FECGPU_PLAN", None)
+        else:
+            os.environ["FECGPU_PLAN"] = old
+    assert res["reg"] == res["lane"]
+    assert res["reg"] == res["wave"]
+    sts = {t[0] for t in res["reg"]}
+    assert DEC_RECOVERED in sts
