@@ -877,12 +877,15 @@ struct BsLanes {
 #define BS_CALL_ENC(RT)                                                                             \
   do {                                                                                              \
     if constexpr (VEC == 16)                                                                        \
-      bs_enc_r##RT##_v16(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.vm[0], ln.vm[1]); \
+      bs_enc_r##RT##_v16(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.vm[0], \
+                         ln.vm[1]);                                                                \
     else if constexpr (VEC == 8)                                                                    \
-      bs_enc_r##RT##_v8(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], \
+      bs_enc_r##RT##_v8(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
+                        ln.off[3],                                                                  \
                         ln.vm[0], ln.vm[1], ln.vm[2], ln.vm[3]);                                    \
     else                                                                                            \
-      bs_enc_r##RT##_v4(sp, rpp, L, rstride, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], ln.off[3], \
+      bs_enc_r##RT##_v4(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
+                        ln.off[3],                                                                  \
                         ln.off[4], ln.off[5], ln.off[6], ln.off[7], ln.vm[0], ln.vm[1], ln.vm[2],   \
                         ln.vm[3], ln.vm[4], ln.vm[5], ln.vm[6], ln.vm[7]);                          \
   } while (0)
@@ -901,8 +904,11 @@ struct BsLanes {
   } while (0)
 
 template <int RT, int VEC>
-__device__ __forceinline__ void bs_enc_call(uint64_t sp, uint64_t rpp, uint32_t L, uint32_t rstride, uint32_t nsrc,
-                                            uint32_t k, uint32_t rt, uint32_t ca, const BsLanes<VEC> &ln) {
+__device__ __forceinline__ void bs_enc_call(uint64_t sp, uint64_t rpp, uint32_t L, uint64_t rstep, uint64_t sdelta,
+                                            uint32_t nsrc, uint32_t k, uint32_t rt, uint32_t ca,
+                                            const BsLanes<VEC> &ln) {
+  const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
+  const uint32_t sdlo = (uint32_t)sdelta, sdhi = (uint32_t)(sdelta >> 32);
   if constexpr (RT == 1) BS_CALL_ENC(1);
   else if constexpr (RT == 2) BS_CALL_ENC(2);
   else if constexpr (RT == 4) BS_CALL_ENC(4);
@@ -923,6 +929,12 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
 // blocks per group: 64 / RT coefficient lanes per block, bounded by the LDS budget
 __host__ __device__ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes) {
   int g = 64 / RT;
+#ifndef __HIP_DEVICE_COMPILE__
+  if (const char *e = getenv("FECGPU_GROUP")) {  // A/B experiments: cap the blocks per group
+    const int cap = atoi(e);
+    while (g > 1 && g > cap) g >>= 1;
+  }
+#endif
   while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
   return g;
 }
@@ -935,20 +947,27 @@ template <int RT, int VEC>
 __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
-                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step) {
+                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
   uint8_t *lds = lds_all + (size_t)wave * G * k * 16;
   const int r0w = r0 + wave * RT;
   const int rt = r - r0w < RT ? r - r0w : RT;  // <= 0: this wave has no repairs (waits at barriers)
-  for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
+  // Group q holds G blocks.  Interleaved (ilv): blocks q, q + NG, q + 2 NG, ... so the waves resident
+  // at one time stream neighbouring blocks (dense HBM pages); otherwise blocks qG .. qG + G - 1.
+  const uint64_t NG = (nblocks + G - 1) / G;
+  const uint64_t bstep = ilv ? NG : 1;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    const uint64_t b0 = ilv ? q : q * G;
+    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
-    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g0 + lane / RT, repair r0w + lane % RT)
+    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
-      const uint64_t b = g0 + g;
+      const uint64_t b = b0 + g * bstep;
       uint8_t *row = lds + (size_t)g * k * 16 + i;
-      if (b < nblocks && i < rt) {
+      if (g < ng && i < rt) {
         Tmt t;
         const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
         tmt_init(t, rlc_seed(f, (uint32_t)(r0w + i)));
@@ -959,16 +978,17 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
     }
     __syncthreads();
     if (rt <= 0) continue;
-    const uint64_t ng = nblocks - g0 < (uint64_t)G ? nblocks - g0 : (uint64_t)G;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
       BsLanes<VEC> ln(lane, cb);
-      const uint64_t sp = (uint64_t)(uintptr_t)(src + g0 * sbs + c0);  // G == 1 unless sbs == k * L
-      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (g0 * (uint64_t)r + r0w) * (uint64_t)L + c0);
+      const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);  // G == 1 unless sbs == k * L
+      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0w) * (uint64_t)L + c0);
+      const uint64_t rstep = bstep * (uint64_t)r * L;                 // repair rows of the next block
+      const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;          // source rows: after the k-th row
       if (lane < ln.active)
-        bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, (uint32_t)(r * L), (uint32_t)(ng * k), (uint32_t)k,
-                             (uint32_t)rt, lds_addr(lds), ln);
+        bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, rstep, sdelta, (uint32_t)(ng * k), (uint32_t)k, (uint32_t)rt,
+                             lds_addr(lds), ln);
     }
   }
 }
@@ -1005,16 +1025,21 @@ template <int RT, int VEC>
 __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
-                                                       uint8_t *status, uint64_t *recovered) {
+                                                       uint8_t *status, uint64_t *recovered, int ilv) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   RecoverLds S(lds, G, k);
-  for (uint64_t g0 = (uint64_t)blockIdx.x * G; g0 < nblocks; g0 += (uint64_t)gridDim.x * G) {
+  const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
+  const uint64_t bstep = ilv ? NG : 1;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    const uint64_t b0 = ilv ? q : q * G;
+    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const int ng = left < (uint64_t)G ? (int)left : G;
     bool act = false;
     int st = FECGPU_BLOCK_NOTHING, e = 0;
-    if (lane < G && g0 + lane < nblocks) {
-      const uint8_t *h = ws + (g0 + lane) * (uint64_t)WL.stride;
+    if (lane < ng) {
+      const uint8_t *h = ws + (b0 + lane * bstep) * (uint64_t)WL.stride;
       st = h[0];
       e = h[1];
       act = st == FECGPU_BLOCK_RECOVERED && e > r0;
@@ -1031,7 +1056,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
     // coefficient rows and input addresses, one (block, input j) pair per lane
     for (int x = lane; x < nact * k; x += 64) {
       const int t = x / k, j = x - t * k;
-      const uint64_t b = g0 + S.gid[t];
+      const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
       const uint8_t *h = ws + b * (uint64_t)WL.stride;
       uint8_t c[16];
@@ -1051,7 +1076,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
     // records: output addresses, rt, flags; for the fused finalize the dependency masks
     for (int x = lane; x < nact * 16; x += 64) {
       const int t = x >> 4, u = x & 15;
-      const uint64_t b = g0 + S.gid[t];
+      const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
       const uint8_t *h = ws + b * (uint64_t)WL.stride;
       uint8_t *rc = S.rec + (size_t)t * kDecRec;
@@ -1086,8 +1111,8 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
     }
     __syncthreads();
     if (status) {
-      if (lane < G && g0 + lane < nblocks) {
-        const uint64_t b = g0 + lane;
+      if (lane < ng) {
+        const uint64_t b = b0 + lane * bstep;
         uint64_t m0 = 0, m1 = 0;
         if (act) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
           const int t = __popcll(am & ((1ull << lane) - 1));
@@ -1131,6 +1156,13 @@ static BsCfg pick_bs_cfg(int L) {
 // sbs: bytes from one block's first source to the next block's (k * L for packed blocks; a
 // sliding window's step * L, where consecutive blocks overlap).  The asm streams a group's
 // sources as one run of contiguous rows, so overlapping blocks go one per group.
+// Interleaved groups (default): a group's blocks are NG apart, so the resident waves stream
+// neighbouring blocks.  FECGPU_INTERLEAVE=0 restores contiguous groups (A/B experiments).
+static int interleave_groups() {
+  const char *e = getenv("FECGPU_INTERLEAVE");
+  return e ? atoi(e) != 0 : 1;
+}
+
 template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
@@ -1139,7 +1171,7 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
   const size_t lds = (size_t)W * G * k * 16;
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
-                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step);
+                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups());
 }
 
 template <int RT, int VEC>
@@ -1149,7 +1181,7 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
   const size_t lds = RecoverLds::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered);
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups());
 }
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \

@@ -61,7 +61,9 @@ S_S = 88
 S_O2 = 90
 S_RT = 92
 S_NZ = 94
-SGPR_CLOBBER = list(range(60, 96))
+S_JL = 96        # enc: sources loaded in the current block (the prefetch crosses block boundaries)
+S_DJ = 98        # enc: pointer jump applied when a block's last source has been loaded
+SGPR_CLOBBER = list(range(60, 100))
 MASKS = [0x55555555, 0x33333333, 0x0F0F0F0F]
 STAGES = [  # (shift, mask index, pairs)
     (1, 0, [(0, 1), (2, 3), (4, 5), (6, 7)]),
@@ -257,6 +259,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"v_mov_b32 v{OUTPTR}, %[outtab]")
     a(f"s_mov_b32 s{S_S}, 0")
     a(f"s_mov_b32 s{S_J}, 0")
+    if mode == "enc":
+        a(f"s_mov_b32 s{S_JL}, 0")
 
     def load_source(buf):
         out = []
@@ -271,7 +275,16 @@ def body(mode: str, RT: int, VEC: int, P: int):
                     f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
         out.append(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
         if mode == "enc":
-            out += [f"s_add_u32 s{S_CUR}, s{S_CUR}, %[L]", f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, 0"]
+            # next row of this block, or -- after its k-th row -- the first row of the group's next
+            # block, which starts bstep blocks further on (interleaved groups: %[sdlo/hi] = delta)
+            out += [f"s_add_u32 s{S_CUR}, s{S_CUR}, %[L]", f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, 0",
+                    f"s_add_u32 s{S_JL}, s{S_JL}, 1",
+                    f"s_cmp_eq_u32 s{S_JL}, %[k]",
+                    f"s_cselect_b32 s{S_DJ}, %[sdlo], 0",
+                    f"s_cselect_b32 s{S_DJ + 1}, %[sdhi], 0",
+                    f"s_cselect_b32 s{S_JL}, 0, s{S_JL}",
+                    f"s_add_u32 s{S_CUR}, s{S_CUR}, s{S_DJ}",
+                    f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_DJ + 1}"]
         return out
 
     for q in range(P - 1):  # prologue: sources 0 .. P-2
@@ -375,8 +388,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
     for r in range(acc_base, acc_base + 8 * RT):
         a(f"v_mov_b32 v{r}, 0")
     if mode == "enc":
-        a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rstride]")
-        a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, 0")
+        a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rslo]")  # next block of the group (64-bit step)
+        a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, %[rshi]")
     else:
         a(f"v_add_u32 v{OUTPTR}, {DEC_REC_BYTES}, v{OUTPTR}")
     a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
@@ -404,9 +417,10 @@ def emit_function(mode, RT, VEC, P):
     offs = ", ".join(f"uint32_t off{q}" for q in range(NP))
     vms = ", ".join(f"uint64_t vm{q}" for q in range(NP))
     if mode == "enc":
-        sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rstride, "
+        sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rslo, "
+               f"uint32_t rshi, uint32_t sdlo, uint32_t sdhi, "
                f"uint32_t nsrc, uint32_t k, uint32_t rt, uint32_t coef, {offs}, {vms})")
-        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rstride] "s"(rstride)', '[rt] "s"(rt)']
+        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rslo] "s"(rslo)', '[rshi] "s"(rshi)', '[sdlo] "s"(sdlo)', '[sdhi] "s"(sdhi)', '[rt] "s"(rt)']
     else:
         sig = (f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, uint32_t nsrc, "
                f"uint32_t k, uint32_t coef, {offs}, {vms})")

@@ -1,0 +1,79 @@
+"""In-process A/B of runtime knobs (environment variables the engine reads per call), so every
+variant runs on the same buffers in the same process: alternates variants for several cycles and
+prints median kernel times.  Removes the process-to-process variance (buffer placement) that
+dominates whole-bench A/B runs.
+usage: python tools/ab_inproc.py "name:VAR=VAL,VAR=VAL" ... [--cycles N] [--reps R]"""
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from pquic_amd import Engine  # noqa: E402
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+cycles = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--cycles=")), 5))
+reps = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--reps=")), 5))
+variants = []
+for spec in args or ["base"]:
+    name, _, env = spec.partition(":")
+    variants.append((name, dict(kv.split("=", 1) for kv in env.split(",") if kv)))
+knobs = sorted({k for _, e in variants for k in e})
+
+eng = Engine(0)
+dev = torch.device("cuda:0")
+L = 1200
+
+
+def setup(k, r, nb, e):
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
+    eng.synth_fill(src, src.numel(), 1, 0)
+    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
+    eng.rlc_encode(src, rep, k, r, L)
+    sp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
+    sp[:, 0] = ((1 << k) - 1) & ~((1 << e) - 1)
+    rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
+    rp[:, 0] = (1 << r) - 1
+    st = torch.empty(nb, dtype=torch.uint8, device=dev)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+    ws = eng.alloc_workspace(nb, k, r)
+    return src, rep, sp, rp, st, rec, ws
+
+
+cases = []
+for (k, r, nb, mode) in [(16, 4, 1 << 20, "enc"), (16, 4, 1 << 20, "dec"), (32, 8, 1 << 20, "enc")]:
+    bufs = setup(k, r, nb, min(k, r))
+    cases.append((f"{mode} k{k} r{r}", k, r, nb, mode, bufs))
+
+
+def run(case):
+    _, k, r, nb, mode, (src, rep, sp, rp, st, rec, ws) = case
+    if mode == "enc":
+        eng.rlc_encode(src, rep, k, r, L)
+    else:
+        eng.rlc_decode(src, rep, sp, rp, st, rec, k, r, L, workspace=ws)
+
+
+times = {(v[0], c[0]): [] for v in variants for c in cases}
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+for cyc in range(cycles):
+    for name, env in variants:
+        for kn in knobs:
+            os.environ.pop(kn, None)
+        os.environ.update(env)
+        for c in cases:
+            run(c)  # warm
+            ev[0].record()
+            for _ in range(reps):
+                run(c)
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[(name, c[0])].append(ev[0].elapsed_time(ev[1]) / reps)
+print(f"{'variant':24s} " + " ".join(f"{c[0]:>14s}" for c in cases) + "   (median ms over cycles; min)")
+for name, _ in variants:
+    cells = []
+    for c in cases:
+        t = times[(name, c[0])]
+        cells.append(f"{statistics.median(t):7.3f}/{min(t):6.3f}")
+    print(f"{name:24s} " + " ".join(f"{x:>14s}" for x in cells))
