@@ -445,18 +445,25 @@ def data_base(mode: str) -> int:
 
 def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     """Register prefetch depth P (source rows in flight per wave).  Prefer 3 waves/SIMD
-    (<= 168 VGPRs) when that still leaves P >= 4; otherwise (RT = 16) take everything up to
-    256 VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63."""
+    (<= 168 VGPRs) when that still leaves P >= PMIN3; otherwise take everything up to 256
+    VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63.
+    The decode wrapper keeps ~14 more VGPRs live across the asm than the asm's own window
+    (measured with -Rpass-analysis=kernel-resource-usage), so its budgets carry a margin --
+    without it the recover kernels tip over a VGPR granule and lose a wave per SIMD."""
     NP = 32 // VEC
-    budget3 = int(os.environ.get("FEC_GEN_VGPR3", "168"))
+    margin = int(os.environ.get("FEC_GEN_DEC_MARGIN", "14")) if mode == "dec" else 0
+    budget3 = int(os.environ.get("FEC_GEN_VGPR3", "168")) - margin
+    # 2-wave budget for decode: RT=8 needs a larger margin than RT=16 (measured: a 242 budget at
+    # RT=8 compiled to 256 VGPRs + 4 AGPRs = 1 wave/SIMD, k32 e8 apply 13 ms -> 7.6 ms at 222)
+    budget2 = 256 - margin - (8 if mode == "dec" and RT <= 8 else 0)
     fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - 1) <= 63
-    forced = os.environ.get(f"FEC_GEN_LIMIT_RT{RT}")  # A/B: VGPR limit for this tile size
-    if forced:
-        return max([P for P in range(2, 33) if fits(P, int(forced))] or [2])
+    forced = os.environ.get(f"FEC_GEN_LIMIT_{mode.upper()}_RT{RT}") or os.environ.get(f"FEC_GEN_LIMIT_RT{RT}")
+    if forced:  # A/B: VGPR limit for this tile size
+        return max([P for P in range(2, 33) if fits(P, int(forced) - margin)] or [2])
     p3 = max([P for P in range(2, 33) if fits(P, budget3)] or [0])
-    if p3 >= 4:
+    if p3 >= int(os.environ.get("FEC_GEN_PMIN3", "4")):
         return min(p3, int(os.environ.get("FEC_GEN_PMAX", "8")))
-    return max([P for P in range(2, 33) if fits(P, 256)] or [2])
+    return max([P for P in range(2, 33) if fits(P, budget2)] or [2])
 
 
 CONFIGS = [(RT, VEC) for VEC in (16, 8, 4) for RT in (1, 2, 4, 8, 16)]
