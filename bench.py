@@ -23,10 +23,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E 8.0 TB/s)
-# measured on MI355X with tools/microbench/hbm_ceiling_probe.hip (profiles/r01_hbm_ceiling_probe.log):
-# best plain-streaming rates for a copy (1:1) and for the encode's 4:1 read:write mix
-MEASURED_COPY_GBS = 5731.0
-MEASURED_MIX41_GBS = 5617.0
+# measured on MI355X (profiles/r01_copy_style_probe.log, tools/microbench/copy_style_probe.hip): the best
+# plain-streaming rates -- one-shot float4 copy (1:1) and a one-shot 4:1 read:write mix (nt loads and
+# stores); and the FEC data path's own access pattern with trivial compute
+# (profiles/r01_block_pattern_probe.log: k16 r4 rows, one wave per interleaved group of 16 blocks)
+MEASURED_COPY_GBS = 6282.0
+MEASURED_MIX41_GBS = 6440.0
+PATTERN_CEILING_GBS = 5479.0
 METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 
 
@@ -440,7 +443,10 @@ def main():
                     "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)}
         roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),
                      "measured_copy_peak": MEASURED_COPY_GBS,
-                     "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4)})
+                     "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4),
+                     "measured_mix41_peak": MEASURED_MIX41_GBS,
+                     "pattern_ceiling": PATTERN_CEILING_GBS,
+                     "frac_of_pattern_ceiling": round(roof["achieved"] / PATTERN_CEILING_GBS, 4)})
         cpu = None
         if not args.no_cpu and world == 1:
             nthreads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
