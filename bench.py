@@ -250,8 +250,9 @@ def pcie_legs(torch, args, dev):
     return {"pcie_e2e_encode_k16_r4": {"blocks": nb, "payload_GiB_s": round(pay / t_enc, 2),
                                        "pcie_GB_s": round((k + r) * L * nb / t_enc / 1e9, 1)},
             "pcie_e2e_decode_k16_e4": {"blocks": nb, "payload_GiB_s": round(pay / t_dec, 2),
-                                       "pcie_GB_s": round((2 * k + r) * L * nb / t_dec / 1e9, 1),
-                                       "note": "decode copies whole source rows both ways"}}
+                                       "pcie_GB_s": round((k + r + e) * L * nb / t_dec / 1e9, 1),
+                                       "note": "pinned host buffers: block rows H2D, recovered rows written "
+                                               "by the apply kernel straight into host memory"}}
 
 
 def batching_legs(dev_index, args):

@@ -102,6 +102,15 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
 int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
                             uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
                             void *workspace, size_t workspace_bytes, void *stream);
+/* apply with the recovered symbols written to dst instead of in place: dst has src's layout
+ * ([block][k][symbol_size]) and receives only the recovered rows (every other byte of dst is left
+ * untouched); src is only read.  dst may be any memory the device can write -- e.g. page-locked
+ * host packet buffers, so recovered symbols cross PCIe once and nothing else comes back
+ * (fecgpu_rlc_decode_host uses this for pinned buffers). */
+int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint64_t nblocks,
+                               uint32_t k, uint32_t r, uint32_t symbol_size, uint8_t *status,
+                               uint64_t *recovered, void *workspace, size_t workspace_bytes,
+                               void *stream);
 
 /* XOR decode (r == 1), same conventions. */
 int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
@@ -114,8 +123,9 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
  * pipelined over sub-batches of about `chunk_bytes` of payload on `nstreams` HIP streams so
  * that PCIe transfers overlap the kernels.  Synchronous: results are in host memory on
  * return.  Used by the protoop adapters (one block per call) and by the PCIe-inclusive
- * measurement.  Decode copies whole source rows both ways (received sources in, recovered
- * sources back in place). */
+ * measurement.  Decode copies the block's rows in; recovered sources come back either written
+ * by the kernel straight into the caller's buffer (page-locked src: only recovered rows cross
+ * PCIe device-to-host) or, for pageable src, by copying whole source rows back. */
 typedef struct fecgpu_host_ctx fecgpu_host_ctx_t;
 fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk_bytes);
 void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *ctx);

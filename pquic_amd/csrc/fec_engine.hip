@@ -32,7 +32,7 @@
 
 using namespace fecdev;
 
-#define FECGPU_VERSION "pquic_amd fecgpu 0.1 (gfx950, v_perm GF(256) data path)"
+#define FECGPU_VERSION "pquic_amd fecgpu 0.2 (gfx950, bitsliced GF(256) data path)"
 
 static thread_local char g_err[256];
 static std::atomic<uint64_t> g_stats[4];
@@ -751,7 +751,7 @@ template <int RT, int W>
 __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
                                                     const uint32_t *__restrict__ rep, uint64_t nblocks,
                                                     int k, int r, int Ldw, int nchunks, int chunk_dw,
-                                                    uint8_t *ws, int r0) {
+                                                    uint8_t *ws, int r0, uint32_t *dst) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
@@ -787,7 +787,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
 #pragma unroll
     for (int i = 0; i < RT; i++) {
       if (i < rt) {
-        uint32_t *ob = src + (b * (uint64_t)k + h[L.off_unk + r0 + i]) * (uint64_t)Ldw + c0;
+        uint32_t *ob = dst + (b * (uint64_t)k + h[L.off_unk + r0 + i]) * (uint64_t)Ldw + c0;
         uint32_t any = 0;
 #pragma unroll
         for (int w = 0; w < W; w++) {
@@ -1025,7 +1025,8 @@ template <int RT, int VEC>
 __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
-                                                       uint8_t *status, uint64_t *recovered, int ilv) {
+                                                       uint8_t *status, uint64_t *recovered, int ilv,
+                                                       uint8_t *dst) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
@@ -1083,7 +1084,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
       rc[kDecRecNz + u] = 0;
       if (u < rt) {
         const int j = h[WL.off_unk + r0 + u];
-        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(src + (b * (uint64_t)k + j) * (uint64_t)L);
+        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
           for (int v = u + 1; v < rt; v++) m |= (uint32_t)(h[WL.off_dep + u * WL.em + v] != 0) << v;
@@ -1176,12 +1177,13 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
 
 template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
-                              uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s) {
+                              uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
+                              uint8_t *dst) {
   const int G = bs_group(RT, k, 24, kDecRec + 80);
   const size_t lds = RecoverLds::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups());
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst);
 }
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
@@ -1431,10 +1433,10 @@ static void launch_encode(const uint32_t *src, uint32_t *rep, uint64_t nb, int k
 
 template <int RT, int W>
 static void launch_recover(uint32_t *src, const uint32_t *rep, uint64_t nb, int k, int r, int Ldw,
-                           const DataCfg &c, uint8_t *ws, int r0, hipStream_t s) {
+                           const DataCfg &c, uint8_t *ws, int r0, hipStream_t s, uint32_t *dst) {
   size_t lds = DataLds<RT>::bytes(k);
   hipLaunchKernelGGL((k_rlc_recover<RT, W>), dim3(grid_for(nb * c.nchunks)), dim3(64), lds, s, src,
-                     rep, nb, k, r, Ldw, c.nchunks, c.chunk_dw, ws, r0);
+                     rep, nb, k, r, Ldw, c.nchunks, c.chunk_dw, ws, r0, dst);
 }
 
 #define FEC_DISPATCH_W(FN, RT, ...)                       \
@@ -1662,14 +1664,19 @@ static int launch_finalize(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *st
   return FECGPU_OK;
 }
 
-int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
-                            uint32_t symbol_size, uint8_t *status, uint64_t *recovered, void *workspace,
-                            size_t workspace_bytes, void *stream) {
+// The data pass of decode; recovered symbols go to dst (same [block][k][L] layout as src; dst == src
+// is the in-place form).  Inputs are only ever read from src/rep, outputs only written to dst.
+static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                             uint32_t r, uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
+                             void *workspace, size_t workspace_bytes, hipStream_t s) {
   static const uint64_t dummy = 0;
   int rc = decode_args(src, rep, nblocks, k, r, symbol_size, &dummy, &dummy, status, recovered, workspace,
                        workspace_bytes);
   if (rc || nblocks == 0) return rc;
-  hipStream_t s = (hipStream_t)stream;
+  if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL output buffer");
+  if ((uintptr_t)dst % 4) return set_err(FECGPU_ERR_INVALID, "%s", "output buffer must be 4-byte aligned");
+  g_stats[2]++;  // decode calls / blocks are counted at the data pass (fecgpu_rlc_decode and the staged API)
+  g_stats[3] += nblocks;
   uint8_t *ws = (uint8_t *)workspace;
   const WsLayout L = ws_layout(k, r);
   // decode passes: the smallest tile covering e_max (one pass, finalize fused) up to 16 unknowns
@@ -1680,7 +1687,7 @@ int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32
     const DataCfg cfg = pick_data_cfg(Ldw);
     for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
       FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                      cfg, ws, r0, s)
+                      cfg, ws, r0, s, (uint32_t *)dst)
     }
     HIPCHK(hipGetLastError());
     return launch_finalize(nblocks, k, r, status, recovered, ws, s);
@@ -1689,10 +1696,25 @@ int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32
   const bool fused = (int)L.em <= rt;  // one pass covers every unknown of every block
   for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
     FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
-                    (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s)
+                    (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
+                    (uint8_t *)dst)
   }
   HIPCHK(hipGetLastError());
   return fused ? FECGPU_OK : launch_finalize(nblocks, k, r, status, recovered, ws, s);
+}
+
+int fecgpu_rlc_decode_apply(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                            uint32_t symbol_size, uint8_t *status, uint64_t *recovered, void *workspace,
+                            size_t workspace_bytes, void *stream) {
+  return decode_apply_impl(src, rep, src, nblocks, k, r, symbol_size, status, recovered, workspace,
+                           workspace_bytes, (hipStream_t)stream);
+}
+
+int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                               uint32_t r, uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
+                               void *workspace, size_t workspace_bytes, void *stream) {
+  return decode_apply_impl(src, rep, dst, nblocks, k, r, symbol_size, status, recovered, workspace,
+                           workspace_bytes, (hipStream_t)stream);
 }
 
 int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
@@ -1708,8 +1730,6 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   if ((rc = fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, status, recovered, workspace,
                                     workspace_bytes, stream)))
     return rc;
-  g_stats[2]++;
-  g_stats[3] += nblocks;
   return FECGPU_OK;
 }
 

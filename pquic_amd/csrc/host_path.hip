@@ -153,6 +153,16 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
   HCHK(hipSetDevice(c->device));
   const size_t sb = (size_t)k * L, rb = (size_t)r * L;
   const uint64_t n = sub_batch(c, nblocks, sb + rb);
+  // page-locked src (hipHostMalloc / registered): the apply kernel writes the recovered rows
+  // straight into it over PCIe, so nothing but status comes back by copy
+  uint8_t *zdst = nullptr;
+  if (!xr) {
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, src) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer)
+      zdst = (uint8_t *)pa.devicePointer;
+    else
+      (void)hipGetLastError();  // pageable memory: clear the sticky query error
+  }
   int si = 0;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
@@ -176,11 +186,14 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
     } else {
       const size_t wsb = fecgpu_rlc_decode_workspace(n, k, r);
       HCHK(grow(&s.d_ws, &s.cap_ws, wsb));
-      rc = fecgpu_rlc_decode(s.d_src, s.d_rep, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu),
-                             fbn ? d_fbn : nullptr, d_sp, d_rp, d_st, d_rec, s.d_ws, s.cap_ws, s.st);
+      rc = fecgpu_rlc_decode_plan(m, k, r, (uint32_t)((fbn_base + b0) & 0xffffffu), fbn ? d_fbn : nullptr, d_sp,
+                                  d_rp, s.d_ws, s.cap_ws, s.st);
+      if (!rc)
+        rc = fecgpu_rlc_decode_apply_to(s.d_src, s.d_rep, zdst ? zdst + b0 * sb : s.d_src, m, k, r, L, d_st, d_rec,
+                                        s.d_ws, s.cap_ws, s.st);
     }
     if (rc) return rc;
-    HCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
+    if (!zdst) HCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
     HCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
     HCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
   }

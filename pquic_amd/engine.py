@@ -50,6 +50,7 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
     L.fecgpu_rlc_decode_plan.argtypes = [u64, u32, u32, u32, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_apply_to.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
     L.fecgpu_host_ctx_create.argtypes = [C.c_int, C.c_int, sz]
@@ -184,6 +185,14 @@ class Engine:
         self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
                                                      _addr(recovered), _addr(workspace), workspace.numel(),
                                                      self._stream(stream)), "fecgpu_rlc_decode_apply")
+        return status, recovered
+
+    def rlc_decode_apply_to(self, src, rep, dst, status, recovered, k, r, L, nblocks, workspace, stream=None):
+        """fecgpu_rlc_decode_apply_to: as apply, recovered symbols written to dst (src's layout)."""
+        self._check(self.lib.fecgpu_rlc_decode_apply_to(_addr(src), _addr(rep), _addr(dst), nblocks, k, r, L,
+                                                        _addr(status), _addr(recovered), _addr(workspace),
+                                                        workspace.numel(), self._stream(stream)),
+                    "fecgpu_rlc_decode_apply_to")
         return status, recovered
 
     def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,
