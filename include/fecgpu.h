@@ -123,9 +123,10 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
  * pipelined over sub-batches of about `chunk_bytes` of payload on `nstreams` HIP streams so
  * that PCIe transfers overlap the kernels.  Synchronous: results are in host memory on
  * return.  Used by the protoop adapters (one block per call) and by the PCIe-inclusive
- * measurement.  Decode copies the block's rows in; recovered sources come back either written
- * by the kernel straight into the caller's buffer (page-locked src: only recovered rows cross
- * PCIe device-to-host) or, for pageable src, by copying whole source rows back. */
+ * measurement.  Page-locked buffers (fecgpu_host_alloc, hipHostMalloc, registered) are zero-copy:
+ * the kernels read the blocks and write repairs / recovered rows directly over PCIe, so only the
+ * bytes the operation needs cross the bus.  Pageable buffers are staged by copies (decode then
+ * copies whole source rows back). */
 typedef struct fecgpu_host_ctx fecgpu_host_ctx_t;
 fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk_bytes);
 void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *ctx);

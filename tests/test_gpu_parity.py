@@ -529,3 +529,19 @@ def test_host_decode_zero_copy_pinned(oracle):
     assert np.array_equal(pin.numpy()[ok], src[ok])
     assert np.array_equal(pin.numpy()[~ok], ref[~ok])
     hp.close()
+
+
+def test_host_encode_zero_copy_pinned(oracle):
+    """fecgpu_rlc_encode_host on page-locked buffers (the kernel reads sources from and writes
+    repairs to host memory over PCIe), twice on the same buffers with new contents in between."""
+    from pquic_amd import HostPath
+    hp = HostPath(0, 3, 1 << 20)
+    nb, k, r, L = 900, 16, 4, 1200
+    srcp = torch.empty((nb, k, L), dtype=torch.uint8).pin_memory()
+    repp = torch.empty((nb, r, L), dtype=torch.uint8).pin_memory()
+    for seed in (11, 12):
+        src = synth_bytes(nb * k * L, seed).reshape(nb, k, L)
+        srcp.numpy()[:] = src
+        hp.rlc_encode(srcp, repp, nb, k, r, L, seed)
+        assert np.array_equal(repp.numpy(), oracle.rlc_encode_batch(src, r, seed))
+    hp.close()
