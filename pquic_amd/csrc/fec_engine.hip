@@ -951,7 +951,8 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
-  uint8_t *lds = lds_all + (size_t)wave * G * k * 16;
+  constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);  // per source: RT (>= 4) u16 case offsets
+  uint8_t *lds = lds_all + (size_t)wave * G * k * CSB;
   const int r0w = r0 + wave * RT;
   const int rt = r - r0w < RT ? r - r0w : RT;  // <= 0: this wave has no repairs (waits at barriers)
   // Group q holds G blocks.  Interleaved (ilv): blocks q, q + NG, q + 2 NG, ... so the waves resident
@@ -966,14 +967,19 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
     if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
-      uint8_t *row = lds + (size_t)g * k * 16 + i;
+      uint16_t *row = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB) + i;  // field i of source j
       if (g < ng && i < rt) {
         Tmt t;
         const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
         tmt_init(t, rlc_seed(f, (uint32_t)(r0w + i)));
-        for (int j = 0; j < k; j++) row[j * 16] = tmt_coef(t);
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = (uint16_t)((tmt_coef(t) + 1u) * FEC_BS_CASE_BYTES);
       } else {
-        for (int j = 0; j < k; j++) row[j * 16] = 0;
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;  // ends the chain: repair i is not live
+      }
+      if constexpr (RT < 4) {  // the unused fields of a 4-field row end the chain as well
+        if (i == 0)
+          for (int j = 0; j < k; j++)
+            for (int x = RT; x < 4; x++) row[j * (CSB / 2) + x] = 0;
       }
     }
     __syncthreads();
@@ -999,8 +1005,10 @@ __global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict
 // rule runs here from LDS (non-zero flags from the asm body, dependency masks and unknown ids
 // staged during setup) and status[]/recovered[] are written for every block of the group.
 // Otherwise the flags are OR-ed into the workspace for k_rlc_finalize.
+template <int RT>
 struct RecoverLds {
-  uint8_t *coef;     // [G][k][16] coefficient rows (u fastest)
+  static constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
+  uint8_t *coef;     // [G][k][CSB] u16 case offsets (u fastest), as the asm's chains read them
   uint64_t *intab;   // [G][k] input symbol addresses
   uint8_t *rec;      // [G] x kDecRec records read by the asm body
   uint8_t *gid;      // [64] compacted slot -> block in group
@@ -1008,12 +1016,12 @@ struct RecoverLds {
   uint8_t *unk;      // [G][16] unknown -> source index (fused finalize)
   uint32_t *depm;    // [G][16] unknowns row u still references after elimination (fused finalize)
   __host__ __device__ static size_t bytes(int G, int k) {
-    return (size_t)G * ((size_t)k * 24 + kDecRec + 16 + 64) + 128;
+    return (size_t)G * ((size_t)k * (CSB + 8) + kDecRec + 16 + 64) + 128;
   }
   __device__ RecoverLds(uint8_t *l, int G, int k) {
     coef = l;
-    intab = reinterpret_cast<uint64_t *>(l + (size_t)G * k * 16);
-    rec = l + (size_t)G * k * 24;
+    intab = reinterpret_cast<uint64_t *>(l + (size_t)G * k * CSB);
+    rec = l + (size_t)G * k * (CSB + 8);
     depm = reinterpret_cast<uint32_t *>(rec + (size_t)G * kDecRec);
     unk = reinterpret_cast<uint8_t *>(depm + G * 16);
     gid = unk + G * 16;
@@ -1030,7 +1038,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
-  RecoverLds S(lds, G, k);
+  RecoverLds<RT> S(lds, G, k);
   const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
@@ -1060,15 +1068,11 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
       const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
       const uint8_t *h = ws + b * (uint64_t)WL.stride;
-      uint8_t c[16];
+      constexpr int NF = RecoverLds<RT>::CSB / 2;  // fields per source (>= 4)
+      uint16_t *row = reinterpret_cast<uint16_t *>(S.coef + (size_t)x * RecoverLds<RT>::CSB);
 #pragma unroll
-      for (int u = 0; u < 16; u++) c[u] = (u < RT && u < rt) ? h[WL.off_D + (r0 + u) * k + j] : 0;
-      uint4 cv;
-      cv.x = c[0] | c[1] << 8 | c[2] << 16 | (uint32_t)c[3] << 24;
-      cv.y = c[4] | c[5] << 8 | c[6] << 16 | (uint32_t)c[7] << 24;
-      cv.z = c[8] | c[9] << 8 | c[10] << 16 | (uint32_t)c[11] << 24;
-      cv.w = c[12] | c[13] << 8 | c[14] << 16 | (uint32_t)c[15] << 24;
-      *reinterpret_cast<uint4 *>(S.coef + (size_t)x * 16) = cv;
+      for (int u = 0; u < NF; u++)  // case offset of D[u][j]; 0 past the live unknowns ends the chain
+        row[u] = (u < rt) ? (uint16_t)((h[WL.off_D + (r0 + u) * k + j] + 1u) * FEC_BS_CASE_BYTES) : (uint16_t)0;
       const uint32_t sl = h[WL.off_slot + j];
       const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
                                      : src + (b * (uint64_t)k + sl) * (uint64_t)L;
@@ -1168,8 +1172,8 @@ template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                              hipStream_t s) {
-  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, 16, 0) : 1;
-  const size_t lds = (size_t)W * G * k * 16;
+  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0) : 1;
+  const size_t lds = (size_t)W * G * k * FEC_BS_COEF_ROW_BYTES(RT);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
                      r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups());
@@ -1179,8 +1183,8 @@ template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                               uint8_t *dst) {
-  const int G = bs_group(RT, k, 24, kDecRec + 80);
-  const size_t lds = RecoverLds::bytes(G, k);
+  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80);
+  const size_t lds = RecoverLds<RT>::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
                      L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst);

@@ -14,10 +14,15 @@ How a lane computes  acc_i += c_ij * S_j  over GF(2^8)/0x11D for 32 bytes at a t
   v_bitop3_b32 (3-input XOR):  acc_o ^= TL[row_o & 15] ^ TH[row_o >> 4].
   A coefficient therefore costs at most 8 full-rate VALU ops per 32 bytes.
 * Dispatch.  The 8 register indices depend on the wave-uniform coefficient c, so the code
-  is selected per coefficient: a shared table of 256 cases (72 bytes each, 32 KiB-aligned)
-  is entered with s_swappc_b64 and left with s_setpc_b64.  The case code names the
-  accumulator planes as v0..v7; s_set_gpr_idx_on(SRC0,DST) relocates them to repair i's
-  accumulators (ACC_BASE + 8 i), while the table operands (SRC1/SRC2) stay absolute.
+  is selected per coefficient from a shared table of 256 cases (88 bytes each, 32 KiB-aligned,
+  entry 0 a return stub).  The case code names the accumulator planes as v0..v7;
+  s_set_gpr_idx_on(SRC0,DST) relocates them to repair i's accumulators (ACC_BASE + 8 i), while
+  the table operands (SRC1/SRC2) stay absolute.  Cases are CHAINED: the wrapper stages each
+  source's coefficients as 16-bit case offsets ((c + 1) * 88, 0 = end), four to a 64-bit SGPR
+  queue; the caller enters the first case with s_swappc_b64, and every case's tail advances M0
+  by 8, shifts the queue and jumps straight to the next case (the zero field lands on the stub,
+  which returns).  One taken branch per coefficient instead of a call and a return; tiles with
+  fewer live repairs (rt < RT) end their chain early.
 * Output.  The same three exchange rounds are an involution, so applying them to the
   accumulator planes yields the repair bytes in the original word order.
 
@@ -37,33 +42,34 @@ T_BASE = 32
 TL = {n: T_BASE + n - 1 for n in range(1, 16)}          # v32..v46
 TH = {n: T_BASE + 15 + n - 1 for n in range(1, 16)}     # v47..v61
 TMP = [62, 63, 64, 65]
-CO = [66, 67, 68, 69]
-COPTR = 70
-INPTR = 71
-OUTPTR = 72  # decode only; decode data buffers start one register later
-DATA_BASE = 72
-CASE_BYTES = 72
+CO = TMP  # coefficient fields: read into the transpose temporaries once the transpose is done
+COPTR = 66
+INPTR = 67   # decode only
+OUTPTR = 68  # decode only
+DATA_BASE = 68  # encode; decode data buffers start at 70 (tuples must start on an even VGPR)
+CASE_BYTES = 88  # <= 8 VOP3 (64 B) + the 20-byte chain tail; table entry 0 is the return stub
 # stage-0 destinations (scratch, overwritten by the combos), stage-2 destinations (planes)
 XS = [TL[3], TL[5], TL[6], TL[7], TH[3], TH[5], TH[6], TH[7]]
 PL = [TL[1], TL[2], TL[4], TL[8], TH[1], TH[2], TH[4], TH[8]]
 # SGPRs owned by the asm bodies
 S_TAB, S_TGT, S_RET, S_T, S_J = 60, 62, 64, 66, 67
-S_C = [68, 69, 70, 71]
+S_C = [68, 69, 70, 71]  # coefficient-field dwords of the current source (readfirstlane of CO)
+S_CQ = 84        # chain queue: the remaining 16-bit case offsets of the running chain (shared with
+                 # the decode epilogue's exec save, which never overlaps a chain)
 S_MASK = [72, 73, 74]
 S_T2 = 75
 S_CUR = 76
 S_SAVEM0 = 78
+S_RT = 79
 S_SAVEEX = 80
 S_OUT = 82
 S_T3 = 84
 S_EPI = 86
 S_S = 88
+S_JL = 89        # enc: sources loaded in the current block (the prefetch crosses block boundaries)
 S_O2 = 90
-S_RT = 92
-S_NZ = 94
-S_JL = 96        # enc: sources loaded in the current block (the prefetch crosses block boundaries)
-S_DJ = 98        # enc: pointer jump applied when a block's last source has been loaded
-SGPR_CLOBBER = list(range(60, 100))
+S_DJ = 92        # enc: pointer jump applied when a block's last source has been loaded
+SGPR_CLOBBER = list(range(60, 94))  # s0-s59 and s94-s101 stay with the compiler
 MASKS = [0x55555555, 0x33333333, 0x0F0F0F0F]
 STAGES = [  # (shift, mask index, pairs)
     (1, 0, [(0, 1), (2, 3), (4, 5), (6, 7)]),
@@ -143,6 +149,9 @@ def v(n):
 
 def emit_table():
     lines = ['  .text', '  .p2align 15', '  .globl fec_bs_case_table', '  .hidden fec_bs_case_table', 'fec_bs_case_table:']
+    # entry 0: the chain's end (a zero field) returns to the caller
+    lines.append(f"  s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+    lines.append(f"  .org fec_bs_case_table + {CASE_BYTES}")
     for c in range(256):
         body = []
         for o, (nl, nh) in enumerate(case_rows(c)):
@@ -152,9 +161,14 @@ def emit_table():
                 body.append(f"v_xor_b32 v{o}, v{o}, {v(TL[nl])}")
             elif nh:
                 body.append(f"v_xor_b32 v{o}, v{o}, {v(TH[nh])}")
-        body.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+        # chain tail: next repair's accumulators, next 16-bit case offset, jump (entry 0 returns)
+        body += [f"s_add_u32 m0, m0, 8",
+                 f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
+                 f"s_pack_ll_b32_b16 s{S_T}, s{S_CQ}, 0",
+                 f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}",
+                 f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
         lines += ["  " + b for b in body]
-        lines.append(f"  .org fec_bs_case_table + {CASE_BYTES * (c + 1)}")
+        lines.append(f"  .org fec_bs_case_table + {CASE_BYTES * (c + 2)}")
     return lines
 
 
@@ -215,6 +229,12 @@ LOADOP = {16: ("global_load_dwordx4", "global_store_dwordx4", 4),
           4: ("global_load_dword", "global_store_dword", 1)}
 
 
+def coef_row_bytes(RT: int) -> int:
+    """LDS bytes per source of a coefficient row: max(4, RT) little-endian u16 fields, field i =
+    (c_i + 1) * CASE_BYTES (the case's offset in the table), 0 = end of chain."""
+    return 2 * max(4, RT)
+
+
 def regrange(base, n):
     return f"v{base}" if n == 1 else f"v[{base}:{base + n - 1}]"
 
@@ -242,6 +262,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
     a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
     a(f"s_add_u32 s{S_TAB}, s{S_TAB}, fec_bs_case_table@rel32@lo+4")
     a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, fec_bs_case_table@rel32@hi+12")
+    # the table is one 32 KiB-aligned block: every target shares TAB's high word
+    a(f"s_mov_b32 s{S_TGT + 1}, s{S_TAB + 1}")
     a(f"s_getpc_b64 s[{S_EPI}:{S_EPI + 1}]")
     a(".Lepipc_%=:")
     a(f"s_add_u32 s{S_EPI}, s{S_EPI}, .Lepi_%= - .Lepipc_%=")
@@ -292,8 +314,10 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_cbranch_scc0 .Lpro_done_%=")
         L.extend(load_source(q))
     a(".Lpro_done_%=:")
-    ncw = 1 if RT <= 4 else (2 if RT <= 8 else 4)
-    dsr = {1: "ds_read_b32", 2: "ds_read_b64", 4: "ds_read_b128"}[ncw]
+    csb = coef_row_bytes(RT)  # per source: max(4, RT) 16-bit case offsets
+    dsr = "ds_read_b64" if csb == 8 else "ds_read_b128"
+    ndw = min(4, csb // 4)
+    nch = max(1, RT // 4)  # chains of up to 4 cases (one 64-bit queue each)
     for b in range(P):
         nb = (b + P - 1) % P
         a(f".Lbody{b}_%=:")
@@ -306,38 +330,31 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f".Lnopf{b}_%=:")
         a("s_waitcnt vmcnt(0)")
         a(f".Lpf{b}_%=:")
-        a(f"{dsr} {regrange(CO[0], ncw)}, v{COPTR}")
-        a(f"v_add_u32 v{COPTR}, 16, v{COPTR}")
         L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
+        # the coefficient fields land in the (now free) transpose temporaries under the combos
+        a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
+        if csb <= 16:
+            a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
         L.extend(combos())
         a("s_waitcnt lgkmcnt(0)")
-        for w in range(ncw):
+        for w in range(ndw):
             a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-        if os.environ.get("FEC_GEN_FAKE_DISPATCH"):  # timing experiment only: wrong results
-            for i in range(RT):
-                for o, (nl, nh) in enumerate(case_rows(19)):
-                    acc = acc_base + 8 * i + o
-                    a(f"v_bitop3_b32 v{acc}, v{acc}, {v(TL[nl])}, {v(TH[nh])} bitop3:0x96")
-            RT_calls = 0
-        else:
-            RT_calls = RT
-        fixed_target = bool(os.environ.get("FEC_GEN_FIXED_TARGET"))  # timing experiment only
-        if fixed_target:
-            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, {19 * CASE_BYTES}")
-            a(f"s_addc_u32 s{S_TGT + 1}, s{S_TAB + 1}, 0")
-        for i in range(RT_calls):
-            if not fixed_target:
-                a(f"s_bfe_u32 s{S_T}, s{S_C[i // 4]}, 0x{(8 << 16) | (8 * (i % 4)):x}")
-                a(f"s_mul_i32 s{S_T}, s{S_T}, {CASE_BYTES}")
-                a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
-                a(f"s_addc_u32 s{S_TGT + 1}, s{S_TAB + 1}, 0")
-            if i == 0:
-                a(f"s_set_gpr_idx_on {acc_base}, gpr_idx(SRC0,DST)")
-            else:
-                a(f"s_set_gpr_idx_idx {acc_base + 8 * i}")
+        if csb == 32:  # second half of the offsets lands while the first two chains run
+            a(f"ds_read_b128 {regrange(CO[0], 4)}, v{COPTR} offset:16")
+            a(f"v_add_u32 v{COPTR}, 32, v{COPTR}")
+        for ch in range(nch):
+            if ch == 2:  # RT = 16: offsets 8..15 (no VALU may run in GPR-index mode)
+                a("s_set_gpr_idx_off")
+                a("s_waitcnt lgkmcnt(0)")
+                for w in range(4):
+                    a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+            a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
+            a(f"s_pack_ll_b32_b16 s{S_T}, s{S_CQ}, 0")
+            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
+            if ch % 2 == 0:  # chain 1 continues M0 where chain 0 left it (4 cases later)
+                a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
             a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
-        if RT_calls:
-            a("s_set_gpr_idx_off")
+        a("s_set_gpr_idx_off")
         a(f"s_add_u32 s{S_S}, s{S_S}, 1")
         a(f"s_add_u32 s{S_J}, s{S_J}, 1")
         a(f"s_cmp_eq_u32 s{S_J}, %[k]")
@@ -440,7 +457,7 @@ DEC_REC_NZ = 144
 
 
 def data_base(mode: str) -> int:
-    return DATA_BASE if mode == "enc" else DATA_BASE + 2  # tuples must start on an even VGPR
+    return DATA_BASE if mode == "enc" else OUTPTR + 2  # tuples must start on an even VGPR
 
 
 def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
@@ -478,6 +495,8 @@ def main():
              "#include <stdint.h>",
              "",
              f"#define FEC_BS_CASE_BYTES {CASE_BYTES}",
+             "// LDS coefficient row per source: max(4, RT) u16 fields (c + 1) * FEC_BS_CASE_BYTES, 0 ends a chain",
+             "#define FEC_BS_COEF_ROW_BYTES(RT) (2 * ((RT) < 4 ? 4 : (RT)))",
              "#ifndef FEC_LD_POL",
              "#define FEC_LD_POL \"\"  // symbol loads: default policy (nt loads measured slower for decode)",
              "#endif",

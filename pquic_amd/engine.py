@@ -28,10 +28,11 @@ class FecGpuStats(C.Structure):
                 ("decode_calls", C.c_uint64), ("decode_blocks", C.c_uint64)]
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libpquic_fec.so.  Raises if it is missing -- never falls back to CPU."""
+def load_library(path: str = LIB_PATH, private: bool = False):
+    """Load libpquic_fec.so.  Raises if it is missing -- never falls back to CPU.
+    private=True loads another build side by side (its own handle; in-process A/B tools)."""
     global _lib
-    if _lib is not None:
+    if _lib is not None and not private:
         return _lib
     if not os.path.exists(path):
         raise FecGpuError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
@@ -60,7 +61,8 @@ def load_library(path: str = LIB_PATH):
     L.fecgpu_rlc_decode_host.argtypes = [v, v, v, u64, u32, u32, u32, u32, v, v, v, v, v]
     L.fecgpu_xor_encode_host.argtypes = [v, v, v, u64, u32, u32]
     L.fecgpu_xor_decode_host.argtypes = [v, v, v, u64, u32, u32, v, v, v, v]
-    _lib = L
+    if not private:
+        _lib = L
     return L
 
 
@@ -77,10 +79,10 @@ def _addr(x):
 class Engine:
     """Batched FEC engine on one device.  Mirrors fecgpu_* one to one."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lib_path: str | None = None):
         import torch
         self.torch = torch
-        self.lib = load_library()
+        self.lib = load_library(lib_path, private=True) if lib_path else load_library()
         self.device = device
         rc = self.lib.fecgpu_init(device)
         if rc != OK:

@@ -2,6 +2,8 @@
 variant runs on the same buffers in the same process: alternates variants for several cycles and
 prints median kernel times.  Removes the process-to-process variance (buffer placement) that
 dominates whole-bench A/B runs.
+A variant may also name another build of the library: "name:LIB=pquic_amd/lib/variants/X/libpquic_fec.so"
+(loaded side by side under its own handle).
 usage: python tools/ab_inproc.py "name:VAR=VAL,VAR=VAL" ... [--cycles N] [--reps R]"""
 import os
 import statistics
@@ -19,20 +21,22 @@ variants = []
 for spec in args or ["base"]:
     name, _, env = spec.partition(":")
     variants.append((name, dict(kv.split("=", 1) for kv in env.split(",") if kv)))
-knobs = sorted({k for _, e in variants for k in e})
+knobs = sorted({k for _, e in variants for k in e if k != "LIB"})
 
-eng = Engine(0)
+eng0 = Engine(0)
+engines = {name: (Engine(0, lib_path=e["LIB"]) if "LIB" in e else eng0) for name, e in variants}
+eng = eng0
 dev = torch.device("cuda:0")
 L = 1200
 
 
-def setup(k, r, nb, e):
+def setup(k, r, nb, e, L):
     src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
     eng.synth_fill(src, src.numel(), 1, 0)
     rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
     eng.rlc_encode(src, rep, k, r, L)
     sp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
-    sp[:, 0] = ((1 << k) - 1) & ~((1 << e) - 1)
+    sp[:, 0] = (((1 << k) - 1) & ~((1 << e) - 1)) if k < 63 else -(1 << e)
     rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
     rp[:, 0] = (1 << r) - 1
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -42,13 +46,16 @@ def setup(k, r, nb, e):
 
 
 cases = []
-for (k, r, nb, mode) in [(16, 4, 1 << 20, "enc"), (16, 4, 1 << 20, "dec"), (32, 8, 1 << 20, "enc")]:
-    bufs = setup(k, r, nb, min(k, r))
-    cases.append((f"{mode} k{k} r{r}", k, r, nb, mode, bufs))
+CASES = [(16, 4, 1 << 20, "enc", 1200), (16, 4, 1 << 20, "dec", 1200), (32, 8, 1 << 20, "enc", 1200)]
+if "--wide" in sys.argv:  # also the r >= 8 decode and configs[4] (jumbo symbols)
+    CASES += [(32, 8, 1 << 19, "dec", 1200), (64, 16, 1 << 15, "enc", 9000), (64, 16, 1 << 15, "dec", 9000)]
+for (k, r, nb, mode, L) in CASES:
+    bufs = setup(k, r, nb, min(k, r), L)
+    cases.append((f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L, bufs))
 
 
-def run(case):
-    _, k, r, nb, mode, (src, rep, sp, rp, st, rec, ws) = case
+def run(case, eng):
+    _, k, r, nb, mode, L, (src, rep, sp, rp, st, rec, ws) = case
     if mode == "enc":
         eng.rlc_encode(src, rep, k, r, L)
     else:
@@ -61,19 +68,20 @@ for cyc in range(cycles):
     for name, env in variants:
         for kn in knobs:
             os.environ.pop(kn, None)
-        os.environ.update(env)
+        os.environ.update({kk: vv for kk, vv in env.items() if kk != "LIB"})
+        e = engines[name]
         for c in cases:
-            run(c)  # warm
+            run(c, e)  # warm
             ev[0].record()
             for _ in range(reps):
-                run(c)
+                run(c, e)
             ev[1].record()
             torch.cuda.synchronize()
             times[(name, c[0])].append(ev[0].elapsed_time(ev[1]) / reps)
-print(f"{'variant':24s} " + " ".join(f"{c[0]:>14s}" for c in cases) + "   (median ms over cycles; min)")
+print(f"{'variant':24s} " + " ".join(f"{c[0]:>16s}" for c in cases) + "   (median ms over cycles; min)")
 for name, _ in variants:
     cells = []
     for c in cases:
         t = times[(name, c[0])]
         cells.append(f"{statistics.median(t):7.3f}/{min(t):6.3f}")
-    print(f"{name:24s} " + " ".join(f"{x:>14s}" for x in cells))
+    print(f"{name:24s} " + " ".join(f"{x:>16s}" for x in cells))
