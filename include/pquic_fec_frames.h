@@ -63,6 +63,20 @@ const uint8_t *pquic_fec_parse_recovered_frame(const uint8_t *bytes, const uint8
 /* packet_payload_to_source_symbol.c:16-18: the 9-byte source-symbol prefix. Returns 9. */
 size_t pquic_fec_source_symbol_header(uint64_t packet_number, uint8_t *out);
 
+/* The transport's frame skipper (picoquic skip_frame protoop, picoquic_internal.h:1185,
+ * run by helper_skip_frame, plugins/helpers.h:234-245): *consumed = length of the frame at
+ * bytes.  Its return value is ignored, like the reference does. */
+typedef int (*pquic_fec_skip_frame_fn)(void *ctx, const uint8_t *bytes, size_t bytes_max, size_t *consumed,
+                                       int *pure_ack);
+
+/* packet_payload_to_source_symbol.c:6-36: builds the source symbol of a packet into buffer
+ * (room for 9 + payload_length bytes): the 9-byte prefix, then every frame of the payload
+ * except ACK (0x02), PADDING (0x00) and CRYPTO (0x06), frames delimited by `skip`.  Returns
+ * the symbol length 9 + copied bytes.  A skipper that consumes 0 bytes ends the walk (the
+ * reference would loop forever there). */
+uint32_t pquic_fec_payload_to_source_symbol(const uint8_t *payload, uint32_t payload_length, uint64_t packet_number,
+                                            uint8_t *buffer, pquic_fec_skip_frame_fn skip, void *ctx);
+
 #ifdef __cplusplus
 }
 #endif

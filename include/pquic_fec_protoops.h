@@ -86,6 +86,9 @@ typedef struct {
     void (*set_cnx)(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, protoop_arg_t val);
     void *(*my_malloc)(picoquic_cnx_t *cnx, unsigned int size);
     void (*my_free)(picoquic_cnx_t *cnx, void *ptr);
+    /* optional: the skip_frame protoop (helper_skip_frame, plugins/helpers.h:234-245); needed
+     * only by pquic_fec_packet_payload_to_source_symbol */
+    int (*skip_frame)(picoquic_cnx_t *cnx, uint8_t *bytes, size_t bytes_max, size_t *consumed, int *pure_ack);
 } pquic_fec_host_api_t;
 
 /* Bind picoquic's accessors; returns 0.  Until bound every protoop returns
@@ -104,6 +107,14 @@ protoop_arg_t pquic_fec_rlc_recover(picoquic_cnx_t *cnx);
 protoop_arg_t pquic_fec_xor_create_fec_schemes(picoquic_cnx_t *cnx);
 protoop_arg_t pquic_fec_xor_generate_repair_symbols(picoquic_cnx_t *cnx);
 protoop_arg_t pquic_fec_xor_recover(picoquic_cnx_t *cnx);
+
+/* packet_payload_to_source_symbol (protoops/packet_payload_to_source_symbol.c:6-36, manifest
+ * fec_core.plugin:20): inputs [0] payload bytes, [1] symbol buffer, [2] payload length,
+ * [3] packet number; returns the symbol length, PQUIC_ERROR_MEMORY for a NULL buffer, or
+ * PQUIC_FEC_ERR_UNBOUND without a bound skip_frame.  The pluglet's store to
+ * bpf_state.current_symbol_length is not reproduced: both callers overwrite or never read it
+ * (incoming_encrypted.c:29-33, schedule_frames_on_path.c:47). */
+protoop_arg_t pquic_fec_packet_payload_to_source_symbol(picoquic_cnx_t *cnx);
 
 /* Counters of adapter activity (calls, blocks the reference would have crashed on). */
 typedef struct {

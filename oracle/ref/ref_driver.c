@@ -330,3 +330,56 @@ long ref_parse_recovered(const uint8_t *bytes, long bytes_len, uint64_t *packets
     }
     return end ? (long)((const uint8_t *)end - bytes) : -1;
 }
+
+/* ---- source-symbol capture: protoops/packet_payload_to_source_symbol.c ----
+ * The pluglet walks the packet payload with the transport's skip_frame protoop
+ * (helper_skip_frame, plugins/helpers.h:234-245).  The transport's frame parser is not part of
+ * this path, so the driver answers skip_frame with a synthetic grammar shared with
+ * tests/test_frames.py: PADDING (0x00) consumes its run of zero bytes (as picoquic's
+ * skip_frame does); every other type is [type][len][len bytes], capped at the payload end.
+ * The pluglet's bpf_state write (state->current_symbol_length) goes to a local state that
+ * get_cnx_metadata hands out. */
+int ref_skip_frame_synthetic(const uint8_t *bytes, size_t bytes_max, size_t *consumed) {
+    if (bytes_max == 0) { *consumed = 0; return -1; }
+    size_t n;
+    if (bytes[0] == 0x00) {
+        n = 1;
+        while (n < bytes_max && bytes[n] == 0x00) n++;
+    } else {
+        n = bytes_max < 2 ? bytes_max : 2 + (size_t)bytes[1];
+        if (n > bytes_max) n = bytes_max;
+    }
+    *consumed = n;
+    return 0;
+}
+
+static bpf_state g_state;
+protoop_arg_t get_cnx_metadata(picoquic_cnx_t *cnx, int idx) { (void)cnx; (void)idx; return (protoop_arg_t)&g_state; }
+void set_cnx_metadata(picoquic_cnx_t *cnx, int idx, protoop_arg_t val) { (void)cnx; (void)idx; (void)val; }
+protoop_arg_t plugin_run_protoop(picoquic_cnx_t *cnx, protoop_params_t *pp, char *pid_str, protoop_id_t *pid) {
+    (void)cnx; (void)pid;
+    if (strcmp(pid_str, PROTOOPID_NOPARAM_SKIP_FRAME) == 0) {
+        size_t consumed = 0;
+        int ret = ref_skip_frame_synthetic((const uint8_t *)pp->inputv[0], (size_t)pp->inputv[1], &consumed);
+        pp->outputv[0] = (protoop_arg_t)consumed;
+        pp->outputv[1] = 0;
+        return (protoop_arg_t)ret;
+    }
+    return 0;
+}
+
+protoop_arg_t ref_packet_payload_to_source_symbol(picoquic_cnx_t *cnx);
+
+/* returns the pluglet's value (symbol length); the symbol is written to buffer */
+long ref_payload_to_source_symbol(const uint8_t *payload, uint32_t len, uint64_t pn, uint8_t *buffer,
+                                  uint32_t *state_len) {
+    memset(g_in, 0, sizeof g_in);
+    memset(g_out, 0, sizeof g_out);
+    g_in[0] = (protoop_arg_t)payload;
+    g_in[1] = (protoop_arg_t)buffer;
+    g_in[2] = (protoop_arg_t)len;
+    g_in[3] = (protoop_arg_t)pn;
+    long ret = (long)ref_packet_payload_to_source_symbol(NULL);
+    *state_len = g_state.current_symbol_length;
+    return ret;
+}

@@ -105,3 +105,23 @@ size_t pquic_fec_source_symbol_header(uint64_t packet_number, uint8_t *out) {
     put_be(packet_number, out + 1, 8);
     return PQUIC_FEC_SOURCE_SYMBOL_HEADER_BYTES;
 }
+
+uint32_t pquic_fec_payload_to_source_symbol(const uint8_t *payload, uint32_t payload_length, uint64_t packet_number,
+                                            uint8_t *buffer, pquic_fec_skip_frame_fn skip, void *ctx) {
+    pquic_fec_source_symbol_header(packet_number, buffer);              /* :16-18 */
+    uint32_t in_symbol = 0, in_payload = 0;
+    while (in_payload < payload_length) {                               /* :25-33 */
+        const uint8_t t = payload[in_payload];
+        const int ignore = t == 0x02 || t == 0x00 || t == 0x06;         /* ack, padding, crypto_hs */
+        size_t consumed = 0;
+        int pure_ack = 0;
+        (void)skip(ctx, payload + in_payload, payload_length - in_payload, &consumed, &pure_ack);
+        if (consumed == 0) break;
+        if (!ignore) {
+            memcpy(buffer + PQUIC_FEC_SOURCE_SYMBOL_HEADER_BYTES + in_symbol, payload + in_payload, consumed);
+            in_symbol += (uint32_t)consumed;
+        }
+        in_payload += (uint32_t)consumed;
+    }
+    return PQUIC_FEC_SOURCE_SYMBOL_HEADER_BYTES + in_symbol;            /* :35 */
+}

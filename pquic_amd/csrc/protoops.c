@@ -10,6 +10,7 @@
  * error code instead of computing.
  */
 #include "pquic_fec_protoops.h"
+#include "pquic_fec_frames.h"
 
 #include <pthread.h>
 #include <stdlib.h>
@@ -199,3 +200,18 @@ static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
 
 protoop_arg_t pquic_fec_rlc_recover(picoquic_cnx_t *cnx) { return recover(cnx, 0); }
 protoop_arg_t pquic_fec_xor_recover(picoquic_cnx_t *cnx) { return recover(cnx, 1); }
+
+/* ---- source-symbol capture ---- */
+static int skip_via_host(void *cnx, const uint8_t *bytes, size_t bytes_max, size_t *consumed, int *pure_ack) {
+    return g_fec_api.skip_frame((picoquic_cnx_t *)cnx, (uint8_t *)bytes, bytes_max, consumed, pure_ack);
+}
+
+protoop_arg_t pquic_fec_packet_payload_to_source_symbol(picoquic_cnx_t *cnx) {
+    if (!g_fec_bound || !g_fec_api.skip_frame) return PQUIC_FEC_ERR_UNBOUND;
+    const uint8_t *payload = (const uint8_t *)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 0);
+    uint8_t *buffer = (uint8_t *)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 1);
+    const uint32_t length = (uint32_t)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 2);
+    const uint64_t pn = (uint64_t)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 3);
+    if (!buffer) return PQUIC_ERROR_MEMORY;                                /* :14-16 */
+    return pquic_fec_payload_to_source_symbol(payload, length, pn, buffer, skip_via_host, cnx);
+}

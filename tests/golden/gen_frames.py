@@ -4,7 +4,9 @@ Expected bytes come from the reference itself, built by `make -C oracle ref`:
   - FEC frame header: write_fec_frame_header / parse_fec_frame_header (plugins/fec/fec.h:175-194);
   - SFPID frame: helper_write_source_fpid_frame (fec_protoops.h:92-100) / parse_sfpid_frame (fec.h);
   - RECOVERED frame: the pluglets protoops/write_simple_recovered_frame.c and
-    protoops/parse_simple_recovered_frame.c, run through get_cnx/set_cnx.
+    protoops/parse_simple_recovered_frame.c, run through get_cnx/set_cnx;
+  - source symbols: the pluglet protoops/packet_payload_to_source_symbol.c, its skip_frame
+    calls answered by the driver's synthetic frame grammar (ref_skip_frame_synthetic).
 Inputs are seeded random values plus hand-made edge cases, stored verbatim.
 
     python tests/golden/gen_frames.py
@@ -32,7 +34,26 @@ def lib():
     L.ref_write_recovered.restype = C.c_long
     L.ref_parse_recovered.argtypes = [u8p, C.c_long, u64p, C.POINTER(C.c_int)]
     L.ref_parse_recovered.restype = C.c_long
+    L.ref_payload_to_source_symbol.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, C.POINTER(C.c_uint32)]
+    L.ref_payload_to_source_symbol.restype = C.c_long
     return L
+
+
+def synthetic_payload(rnd):
+    """A packet payload in the driver's synthetic frame grammar: PADDING runs, ACK (0x02),
+    CRYPTO (0x06), STREAM-like (0x08-0x0f), SFPID (0x29), FEC (0x2a), others; sometimes a
+    truncated last frame."""
+    out = bytearray()
+    for _ in range(rnd.randint(0, 12)):
+        t = rnd.choice([0x00, 0x02, 0x06, 0x08, 0x0A, 0x0F, 0x29, 0x2A, 0x2B, 0x01, 0x1C, 0x30])
+        if t == 0x00:
+            out += bytes(rnd.randint(1, 20))
+        else:
+            n = rnd.choice([0, 1, 5, 20, 60, 200, rnd.randint(0, 255)])
+            out += bytes([t, n]) + bytes(rnd.getrandbits(8) for _ in range(n))
+    if rnd.random() < 0.2 and len(out) > 3:
+        out = out[: rnd.randint(1, len(out))]
+    return bytes(out)
 
 
 def main():
@@ -92,6 +113,18 @@ def main():
         src = (C.c_uint8 * max(len(raw), 1)).from_buffer_copy(raw.ljust(max(len(raw), 1), b"\0"))
         end = L.ref_parse_recovered(src, len(raw), pk, C.byref(n))
         out["recovered_parse"].append({"bytes": h, "consumed": end, "packets": list(pk[: n.value])})
+    rs = random.Random(20261016)  # separate stream: the sections above stay byte-identical
+    out["source_symbol"] = []
+    payloads = [b"", bytes([0x02, 0x03, 1, 2, 3]), bytes(16), bytes([0x08, 2, 7, 7, 0, 0, 0x06, 1, 9])]
+    payloads += [synthetic_payload(rs) for _ in range(120)]
+    for i, pl in enumerate(payloads):
+        pn = rs.getrandbits(64) if i else 0x0102030405060708
+        src = (C.c_uint8 * max(len(pl), 1)).from_buffer_copy(pl.ljust(max(len(pl), 1), b"\0"))
+        buf = (C.c_uint8 * (len(pl) + 16))()
+        sl = C.c_uint32(0)
+        ret = L.ref_payload_to_source_symbol(src, len(pl), pn, buf, C.byref(sl))
+        out["source_symbol"].append({"payload": pl.hex(), "pn": pn, "ret": ret, "symbol": bytes(buf[:ret]).hex(),
+                                     "state_current_symbol_length": sl.value})
     with open(OUT, "w") as f:
         json.dump(out, f, indent=0)
     print("wrote", OUT, {k: len(v) for k, v in out.items()})

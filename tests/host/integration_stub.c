@@ -10,8 +10,18 @@
 #include "uthash.h"
 #include "pquic_fec_protoops.h"
 
+static int fec_skip_frame(picoquic_cnx_t *cnx, uint8_t *bytes, size_t bytes_max, size_t *consumed,
+                          int *pure_ack) {
+    protoop_arg_t outs[PROTOOPARGS_MAX];
+    int ret = (int)protoop_prepare_and_run_noparam(cnx, &PROTOOP_NOPARAM_SKIP_FRAME, outs, bytes, bytes_max,
+                                                   *consumed, *pure_ack);
+    *consumed = (size_t)outs[0];
+    *pure_ack = (int)outs[1];
+    return ret;
+}
+
 void pquic_fec_install(int hip_device) {
-    static const pquic_fec_host_api_t api = {get_cnx, set_cnx, my_malloc, my_free};
+    static const pquic_fec_host_api_t api = {get_cnx, set_cnx, my_malloc, my_free, fec_skip_frame};
     pquic_fec_bind_host(&api, hip_device);
 }
 
@@ -35,4 +45,6 @@ void pquic_fec_install_native(picoquic_cnx_t *cnx) {
     register_noparam_protoop(cnx, &pid_create, pquic_fec_rlc_create_fec_schemes);
     register_noparam_protoop(cnx, &pid_gen, pquic_fec_rlc_generate_repair_symbols);
     register_noparam_protoop(cnx, &pid_rec, pquic_fec_rlc_recover);
+    static protoop_id_t pid_capture = {.id = "packet_payload_to_source_symbol"};
+    register_noparam_protoop(cnx, &pid_capture, pquic_fec_packet_payload_to_source_symbol);
 }

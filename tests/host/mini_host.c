@@ -65,9 +65,34 @@ static protoop_arg_t run_protoop(picoquic_cnx_t *cnx, op_t op, int inputc, const
     return ret;
 }
 
+/* skip_frame stand-in: the synthetic frame grammar of oracle/ref/ref_driver.c
+ * (ref_skip_frame_synthetic): PADDING runs of 0x00, every other type [type][len][len bytes]. */
+static int mh_skip_frame(picoquic_cnx_t *cnx, uint8_t *bytes, size_t bytes_max, size_t *consumed, int *pure_ack) {
+    (void)cnx;
+    *pure_ack = 0;
+    if (bytes_max == 0) { *consumed = 0; return -1; }
+    size_t n;
+    if (bytes[0] == 0x00) {
+        n = 1;
+        while (n < bytes_max && bytes[n] == 0x00) n++;
+    } else {
+        n = bytes_max < 2 ? bytes_max : 2 + (size_t)bytes[1];
+        if (n > bytes_max) n = bytes_max;
+    }
+    *consumed = n;
+    return 0;
+}
+
 int mh_bind(int device) {
-    pquic_fec_host_api_t api = {mh_get_cnx, mh_set_cnx, mh_malloc, mh_free};
+    pquic_fec_host_api_t api = {mh_get_cnx, mh_set_cnx, mh_malloc, mh_free, mh_skip_frame};
     return pquic_fec_bind_host(&api, device);
+}
+
+/* the packet_payload_to_source_symbol protoop with the reference's four inputs */
+long mh_payload_to_source_symbol(const uint8_t *payload, uint32_t len, uint64_t pn, uint8_t *buffer) {
+    picoquic_cnx_t cnx;
+    protoop_arg_t in[4] = {(protoop_arg_t)payload, (protoop_arg_t)buffer, len, pn};
+    return (long)run_protoop(&cnx, pquic_fec_packet_payload_to_source_symbol, 4, in, NULL);
 }
 
 int mh_unbind(void) { return pquic_fec_bind_host(NULL, 0); }

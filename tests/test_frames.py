@@ -108,6 +108,68 @@ def test_source_symbol_header(lib):
     assert bytes(buf).hex() == "10" + "0102030405060708"
 
 
+SKIP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_size_t),
+                      C.POINTER(C.c_int))
+
+
+def synthetic_skip(ctx, bytes_, bytes_max, consumed, pure_ack):
+    """The frame grammar the reference pluglet was driven with (oracle/ref/ref_driver.c
+    ref_skip_frame_synthetic): PADDING runs of 0x00, every other type [type][len][len bytes]."""
+    pure_ack[0] = 0
+    if bytes_max == 0:
+        consumed[0] = 0
+        return -1
+    if bytes_[0] == 0:
+        n = 1
+        while n < bytes_max and bytes_[n] == 0:
+            n += 1
+    else:
+        n = bytes_max if bytes_max < 2 else min(bytes_max, 2 + bytes_[1])
+    consumed[0] = n
+    return 0
+
+
+def test_payload_to_source_symbol(lib, gold):
+    """packet_payload_to_source_symbol.c: symbol bytes and length equal the reference pluglet's
+    on 124 payloads (ACK / PADDING / CRYPTO frames dropped, truncated last frames, empty)."""
+    fn = lib.pquic_fec_payload_to_source_symbol
+    fn.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, SKIP_FN, C.c_void_p]
+    fn.restype = C.c_uint32
+    cb = SKIP_FN(synthetic_skip)
+    for case in gold["source_symbol"]:
+        pl = bytes.fromhex(case["payload"])
+        src = (C.c_uint8 * max(len(pl), 1)).from_buffer_copy(pl.ljust(max(len(pl), 1), b"\0"))
+        buf = (C.c_uint8 * (len(pl) + 16))()
+        n = fn(C.addressof(src), len(pl), case["pn"], C.addressof(buf), cb, None)
+        assert n == case["ret"], case
+        assert bytes(buf[:n]).hex() == case["symbol"], case
+    assert any(len(c["symbol"]) // 2 < 9 + len(c["payload"]) // 2 for c in gold["source_symbol"])
+
+
+def test_payload_to_source_symbol_protoop():
+    """The protoop adapter (inputs through get_cnx, frames through the host's skip_frame) on the
+    same vectors, driven by the picoquic stand-in; a NULL buffer returns PICOQUIC_ERROR_MEMORY."""
+    so = os.path.join(ROOT, "tests", "host", "libminihost.so")
+    if not os.path.exists(so):
+        pytest.skip("mini host not built")
+    M = C.CDLL(so)
+    M.mh_payload_to_source_symbol.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p]
+    M.mh_payload_to_source_symbol.restype = C.c_long
+    M.mh_unbind()
+    assert M.mh_payload_to_source_symbol(None, 0, 0, None) == 0x41B  # unbound
+    assert M.mh_bind(0) == 0
+    with open(GOLD) as f:
+        cases = json.load(f)["source_symbol"]
+    for case in cases:
+        pl = bytes.fromhex(case["payload"])
+        src = (C.c_uint8 * max(len(pl), 1)).from_buffer_copy(pl.ljust(max(len(pl), 1), b"\0"))
+        buf = (C.c_uint8 * (len(pl) + 16))()
+        n = M.mh_payload_to_source_symbol(C.addressof(src), len(pl), case["pn"], C.addressof(buf))
+        assert n == case["ret"] and bytes(buf[:n]).hex() == case["symbol"], case
+    assert M.mh_payload_to_source_symbol(C.addressof(src), 4, 1, None) == 0x405
+    M.mh_unbind()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("nb,r,L,dlen,stride", [(257, 4, 1200, 1200, 1216), (33, 8, 1200, 1000, 1400),
                                                 (5, 16, 9000, 8998, 9016), (64, 1, 8, 3, 20),
