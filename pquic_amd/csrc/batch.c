@@ -2,14 +2,18 @@
  * pquic_amd/csrc/batch.c -- batching adapter for the block FEC framework
  * (include/pquic_fec_batch.h).  Host C, like the framework it serves.
  *
- * Blocks are staged, as they are submitted, into the page-locked rows of an open "job" (one
- * per operation, scheme, k and r): k source rows (+ r repair rows for recover) of `stride`
- * bytes per block, zero-padded like the reference pads to max_length, plus per-block FEC
- * block numbers and presence masks.  A full or overdue job goes to a worker thread that runs
- * it through the engine's host-resident entry points (H2D, kernels, D2H pipelined on HIP
- * streams); finished jobs are completed on the caller's thread in poll / drain with the same
- * finish halves the synchronous operations use (fec_core.c), so a batched block ends in
- * exactly the state the protocol operation would leave it in.
+ * Submission only checks the reference's preconditions and records the block in the open "job"
+ * (one per operation, scheme, k and r).  A full or overdue job goes through a two-stage
+ * pipeline off the caller's thread:
+ *   - stager threads (several jobs at once) copy each block into the job's page-locked rows: k
+ *     source rows (+ r repair rows for recover) of `stride` bytes, zero-padded like the
+ *     reference pads to max_length, plus presence masks;
+ *   - the engine thread runs staged jobs through the host-resident entry points (zero-copy
+ *     kernels on the page-locked rows).
+ * Finished jobs are completed on the caller's thread in poll / drain with the same finish
+ * halves the synchronous operations use (fec_core.c), so a batched block ends in exactly the
+ * state the protocol operation would leave it in.  The caller keeps a block unmodified until
+ * its completion (pquic_fec_batch.h), which is what lets the copy happen late.
  */
 #include "pquic_fec_batch.h"
 
@@ -21,7 +25,7 @@
 #include "fecgpu.h"
 
 enum { OP_GENERATE = 0, OP_RECOVER = 1 };
-enum { MAX_OPEN = 32 };
+enum { MAX_OPEN = 32, MAX_STAGERS = 16, DEFAULT_STAGERS = 2 };
 
 typedef struct {
     picoquic_cnx_t *cnx;
@@ -51,10 +55,12 @@ struct pquic_fec_batcher {
     job_t *open[MAX_OPEN];
     job_t *free_jobs;
     pthread_t worker;
+    pthread_t stager[MAX_STAGERS];
+    int nstagers;
     pthread_mutex_t mu;
-    pthread_cond_t cv_todo, cv_done;
-    job_t *todo_head, *todo_tail, *done_head, *done_tail;
-    int inflight, stop;
+    pthread_cond_t cv_todo, cv_staged, cv_done;
+    job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *done_head, *done_tail;
+    int inflight, stop, stagers_done;
     pquic_fec_batch_stats_t stats;
 };
 
@@ -122,7 +128,21 @@ static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
                                              j->rec);
 }
 
-static void *worker_main(void *arg) {
+/* Copies a job's blocks into its page-locked rows (the stage halves of fec_core.c). */
+static void stage_job(job_t *j) {
+    const uint32_t S = j->stride, k = j->k, r = j->r;
+    for (uint32_t i = 0; i < j->n; i++) {
+        const entry_t *e = &j->ent[i];
+        uint8_t *src = j->src + (size_t)i * k * S;
+        if (j->op == OP_GENERATE)
+            fec_generate_stage(e->fb, src, S);
+        else
+            fec_recover_stage(e->fb, j->xor_scheme, e->maxl, src, j->rep + (size_t)i * r * S, S, j->sp + 2 * (size_t)i,
+                              j->rp + 2 * (size_t)i);
+    }
+}
+
+static void *stager_main(void *arg) {
     pquic_fec_batcher_t *b = arg;
     pthread_mutex_lock(&b->mu);
     for (;;) {
@@ -131,6 +151,29 @@ static void *worker_main(void *arg) {
         job_t *j = b->todo_head;
         b->todo_head = j->next;
         if (!b->todo_head) b->todo_tail = NULL;
+        pthread_mutex_unlock(&b->mu);
+        stage_job(j);
+        pthread_mutex_lock(&b->mu);
+        j->next = NULL;
+        if (b->staged_tail) b->staged_tail->next = j; else b->staged_head = j;
+        b->staged_tail = j;
+        pthread_cond_signal(&b->cv_staged);
+    }
+    b->stagers_done++;
+    pthread_cond_broadcast(&b->cv_staged);
+    pthread_mutex_unlock(&b->mu);
+    return NULL;
+}
+
+static void *worker_main(void *arg) {
+    pquic_fec_batcher_t *b = arg;
+    pthread_mutex_lock(&b->mu);
+    for (;;) {
+        while (!b->staged_head && b->stagers_done < b->nstagers) pthread_cond_wait(&b->cv_staged, &b->mu);
+        if (!b->staged_head) break;  /* every stager has stopped and nothing is left */
+        job_t *j = b->staged_head;
+        b->staged_head = j->next;
+        if (!b->staged_head) b->staged_tail = NULL;
         pthread_mutex_unlock(&b->mu);
         run_engine(b, j);
         pthread_mutex_lock(&b->mu);
@@ -159,8 +202,21 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     }
     pthread_mutex_init(&b->mu, NULL);
     pthread_cond_init(&b->cv_todo, NULL);
+    pthread_cond_init(&b->cv_staged, NULL);
     pthread_cond_init(&b->cv_done, NULL);
-    if (pthread_create(&b->worker, NULL, worker_main, b)) {
+    const char *ns = getenv("PQUIC_FEC_BATCH_STAGERS");  /* copy threads (default 2) */
+    b->nstagers = ns && atoi(ns) > 0 ? atoi(ns) : DEFAULT_STAGERS;
+    if (b->nstagers > MAX_STAGERS) b->nstagers = MAX_STAGERS;
+    int started = 0;
+    for (; started < b->nstagers; started++)
+        if (pthread_create(&b->stager[started], NULL, stager_main, b)) break;
+    if (started < b->nstagers || pthread_create(&b->worker, NULL, worker_main, b)) {
+        pthread_mutex_lock(&b->mu);
+        b->stop = 1;
+        b->nstagers = started;
+        pthread_cond_broadcast(&b->cv_todo);
+        pthread_mutex_unlock(&b->mu);
+        for (int i = 0; i < started; i++) pthread_join(b->stager[i], NULL);
         fecgpu_host_ctx_destroy(b->ctx);
         free(b);
         return NULL;
@@ -245,15 +301,8 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     int slot;
     job_t *j = open_job(b, op, xor_scheme, k, r, &slot);
     if (!j) return -1;
-    const uint32_t i = j->n, S = j->stride;
-    uint8_t *src = j->src + (size_t)i * k * S;
-    if (op == OP_GENERATE) {
-        fec_generate_stage(fb, src, S);
-    } else {
-        fec_recover_stage(fb, xor_scheme, maxl, src, j->rep + (size_t)i * r * S, S, j->sp + 2 * (size_t)i,
-                          j->rp + 2 * (size_t)i);
-    }
-    j->fbn[i] = fb->fec_block_number & 0xffffffu;
+    const uint32_t i = j->n;
+    j->fbn[i] = fb->fec_block_number & 0xffffffu;  /* rows are copied later, by a stager */
     j->ent[i] = (entry_t){cnx, fb, done, user, maxl};
     if (!i) j->t_first = now_us;
     j->n = i + 1;
@@ -338,6 +387,7 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
     b->stop = 1;
     pthread_cond_broadcast(&b->cv_todo);
     pthread_mutex_unlock(&b->mu);
+    for (int i = 0; i < b->nstagers; i++) pthread_join(b->stager[i], NULL);
     pthread_join(b->worker, NULL);
     while (b->free_jobs) {
         job_t *j = b->free_jobs;
@@ -347,6 +397,7 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
     fecgpu_host_ctx_destroy(b->ctx);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->cv_todo);
+    pthread_cond_destroy(&b->cv_staged);
     pthread_cond_destroy(&b->cv_done);
     free(b);
 }

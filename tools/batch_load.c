@@ -19,8 +19,34 @@ struct st_picoquic_cnx_t { int id; };
 
 static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) { (void)c; (void)ak; (void)p; return 0; }
 static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t v) { (void)c; (void)ak; (void)p; (void)v; }
-static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) { (void)c; return malloc(n); }
-static void bl_free(picoquic_cnx_t *c, void *p) { (void)c; free(p); }
+/* The plugin allocator hands out fixed 2100-byte slots from a free list (picoquic/memory.c:72-95,
+ * 181-191); this load generator does the same, so completions cost what they cost in PQUIC
+ * rather than glibc malloc's price.  Larger requests fall back to the heap, tagged. */
+enum { SLOT = 2112 };  /* 2100 B rounded to 64, plus room for the tag */
+typedef union slot_u { union slot_u *next; uint8_t bytes[SLOT]; } slot_u;
+static slot_u *g_free_slots;
+static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
+    (void)c;
+    if (n > SLOT - 16) {
+        uint8_t *p = malloc((size_t)n + 16);
+        if (!p) return NULL;
+        p[0] = 1;
+        return p + 16;
+    }
+    slot_u *s = g_free_slots;
+    if (s) g_free_slots = s->next; else if (!(s = malloc(sizeof *s))) return NULL;
+    s->bytes[0] = 0;
+    return s->bytes + 16;
+}
+static void bl_free(picoquic_cnx_t *c, void *p) {
+    (void)c;
+    if (!p) return;
+    uint8_t *b = (uint8_t *)p - 16;
+    if (b[0]) { free(b); return; }
+    slot_u *s = (slot_u *)b;
+    s->next = g_free_slots;
+    g_free_slots = s;
+}
 
 static uint64_t now_us(void) {
     struct timespec ts;
@@ -43,7 +69,7 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     g_lat[g_nlat++] = now_us() - s->t_submit;
     for (int i = 0; i < fb->total_repair_symbols; i++) {
         pquic_repair_symbol_t *rs = fb->repair_symbols[i];
-        if (rs) { free(rs->data); free(rs); fb->repair_symbols[i] = NULL; }
+        if (rs) { bl_free(NULL, rs->data); bl_free(NULL, rs); fb->repair_symbols[i] = NULL; }
     }
     s->busy = 0;
 }
@@ -57,7 +83,7 @@ static int cmp_u64(const void *a, const void *b) {
  *      [6] blocks completed, [7] mean blocks per batch.  Returns 0 or -1. */
 int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks, unsigned max_delay_us,
            int nstreams, double offered_gib_s, double out[8]) {
-    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free};
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device)) return -1;
     pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
     pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
