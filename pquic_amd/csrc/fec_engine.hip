@@ -333,17 +333,27 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
       V[e * kpad + j] = bit128(m0, m1, j) ? (uint8_t)(unk[e] == j) : X[e * kpad + j];
     }
     __syncthreads();
-    // sort_system (:28-40): position i takes the first row with the largest A[.][i]
-    if (lane == 0) {
-      for (int i = 0; i < n; i++) perm[i] = i;
-      for (int i = 0; i < n; i++) {
-        int mx = i;
-        for (int j = i + 1; j < n; j++)
-          if (A[perm[mx] * empad + i] < A[perm[j] * empad + i]) mx = j;
-        const int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t;
-      }
-    }
+    // sort_system (:28-40): position i takes the first row with the largest A[.][i].  The scan
+    // over rows j >= i is a wave max-reduction of (value << 16 | 0xffff - j), so the largest value
+    // wins and, among equal values, the smallest j -- the reference's strict '<' scan.
+    for (int i = lane; i < n; i += 64) perm[i] = i;
     __syncthreads();
+    for (int i = 0; i < n; i++) {
+      uint32_t key = 0;
+      for (int j = i + lane; j < n; j += 64) {
+        const uint32_t kj = ((uint32_t)A[perm[j] * empad + i] << 16) | (0xffffu - (uint32_t)j);
+        key = kj > key ? kj : key;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)key, off, 64);
+        key = o > key ? o : key;
+      }
+      const int mx = (int)(0xffffu - (key & 0xffffu));
+      __syncthreads();  // every lane has read perm[] before it changes
+      if (lane == 0) { const int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t; }
+      __syncthreads();
+    }
     // forward elimination without re-pivoting (:54-70): row_pk -= (A[pk][i] / A[pi][i]) row_pi for all
     // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below)
     for (int i = 0; i < n - 1; i++) {
