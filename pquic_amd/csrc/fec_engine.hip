@@ -757,6 +757,215 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tiled register plan for systems too large for one lane (configs[4]: k = 64, e = 16): LPB = EM/4
+// lanes per block.  Lane q of a block holds columns 4q..4q+3 of A (one dword per row) and V's
+// columns [q * 4 KDL, (q + 1) * 4 KDL); an A entry another lane needs (pivots, factors, sort keys)
+// comes by ds_bpermute from the lane that owns its column.  The TinyMT32 rows are generated
+// cooperatively (lane q: rows q, q + LPB, ...) into LDS.  Row operations and record layout as
+// k_rlc_plan_reg; records leave as coalesced dwords.  (rlc_fec_scheme_gf256.c:28-115, 134-236)
+// ---------------------------------------------------------------------------------------------
+template <int KDL, int EM>
+__global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                      const uint32_t *fbn, const uint64_t *sp,
+                                                      const uint64_t *rp, uint8_t *ws) {
+  constexpr int LPB = EM / 4;    // lanes per block: one A dword (4 columns) each
+  constexpr int BPW = 64 / LPB;  // blocks per wave
+  constexpr int CW = 4 * KDL;    // V columns per lane
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x, g = lane / LPB, q = lane % LPB, lane0 = g * LPB;
+  const int em = (int)L.em;
+  const int kpad = (int)pad16((uint32_t)k);
+  const uint8_t *EXP = lds, *LOG = lds + 512;
+  uint8_t *CO = lds + 768;                                   // [BPW][EM][kpad] coefficient rows
+  const uint32_t orow = plan_out_row(L.stride);
+  uint8_t *OUTR = CO + (size_t)BPW * EM * kpad;             // [BPW][orow] records
+  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  uint8_t *h = OUTR + (size_t)g * orow;
+  const uint8_t *crow = CO + (size_t)g * EM * kpad;
+  const int c0 = q * CW;
+  const uint64_t kmask = k < 64 ? (1ull << k) - 1 : ~0ull;
+  auto byte_at = [](uint64_t lo, uint64_t hi, int i) -> uint32_t {
+    return (uint32_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xffu);
+  };
+  for (uint64_t base = (uint64_t)blockIdx.x * BPW; base < nblocks; base += (uint64_t)gridDim.x * BPW) {
+    const uint64_t b = base + g;
+    int state = 0, n = 0;  // 0: nothing to do, 1: solve
+    uint64_t miss = 0, U0 = 0, U1 = 0, S0 = 0, S1 = 0;
+    uint32_t f = 0;
+    if (b < nblocks) {
+      const uint64_t s0 = sp[2 * b] & kmask;  // k <= 64
+      uint64_t q0 = rp[2 * b], q1 = rp[2 * b + 1];
+      clip128(q0, q1, r);
+      const int cur_ss = __popcll(s0), cur_rs = __popcll(q0) + __popcll(q1);
+      if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
+        if (q == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
+      } else {
+        state = 1;
+        n = k - cur_ss;
+        miss = ~s0 & kmask;
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          if ((miss >> j) & 1) {
+            if (u < 8) U0 |= (uint64_t)j << (8 * u); else U1 |= (uint64_t)j << (8 * (u - 8));
+            u++;
+          }
+        int e = 0;
+        for (int i = 0; i < r && e < n; i++)
+          if (bit128(q0, q1, i)) {
+            if (e < 8) S0 |= (uint64_t)i << (8 * e); else S1 |= (uint64_t)i << (8 * (e - 8));
+            e++;
+          }
+        f = block_fbn(b, fbn_base, fbn);
+      }
+    }
+    // TinyMT32 rows of the selected repairs (:194-212), lane q: rows q, q + LPB, ...
+    for (int e = q; e < EM; e += LPB) {
+      if (state && e < n) {
+        Tmt t;
+        tmt_init(t, rlc_seed(f, byte_at(S0, S1, e)));
+        uint8_t *row = CO + ((size_t)g * EM + e) * kpad;
+        for (int j = 0; j < k; j++) row[j] = tmt_coef(t);
+      }
+    }
+    __syncthreads();
+    uint32_t A[EM], V[EM][KDL];  // A[e]: columns 4q..4q+3 of row e
+#pragma unroll
+    for (int e = 0; e < EM; e++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; bb++) {
+        const int u = 4 * q + bb;
+        if (state && e < n && u < n) x |= (uint32_t)crow[e * kpad + byte_at(U0, U1, u)] << (8 * bb);
+      }
+      A[e] = x;
+#pragma unroll
+      for (int d = 0; d < KDL; d++) {
+        const int c = c0 + 4 * d;
+        uint32_t y = 0;
+        if (state && e < n && c < k) {
+          y = *reinterpret_cast<const uint32_t *>(crow + e * kpad + c);  // coefficients of present sources
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {
+            const int cc = c + bb;
+            if (cc >= k) y &= ~(0xffu << (8 * bb));
+            else if ((miss >> cc) & 1) {  // unknown column: identity row of its unknown
+              const uint32_t one = (uint32_t)(__popcll(miss & ((1ull << cc) - 1)) == e);
+              y = (y & ~(0xffu << (8 * bb))) | (one << (8 * bb));
+            }
+          }
+        }
+        V[e][d] = y;
+      }
+    }
+    // A[e][i] from the lane owning column i (every lane of the block runs the same code path)
+    auto colA = [&](int e, int i) -> uint32_t {
+      return ((uint32_t)__shfl((int)A[e], lane0 + (i >> 2), 64) >> (8 * (i & 3))) & 0xffu;
+    };
+#pragma unroll
+    for (int i = 0; i < EM; i++) {  // sort_system :28-40 (first maximum wins; rows swapped in place)
+      int mx = i;
+      uint32_t best = colA(i, i);
+#pragma unroll
+      for (int j = i + 1; j < EM; j++) {
+        const uint32_t v = colA(j, i);
+        if (j < n && best < v) { best = v; mx = j; }
+      }
+      if (i < n) {
+#pragma unroll
+        for (int j = i + 1; j < EM; j++) {
+          if (j == mx) {
+            const uint32_t t = A[i]; A[i] = A[j]; A[j] = t;
+#pragma unroll
+            for (int d = 0; d < KDL; d++) { const uint32_t t2 = V[i][d]; V[i][d] = V[j][d]; V[j][d] = t2; }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < EM - 1; i++) {  // elimination without re-pivoting :54-70
+      const uint32_t piv = colA(i, i);
+      const uint32_t lip = 255u - LOG[piv];
+#pragma unroll
+      for (int kk = i + 1; kk < EM; kk++) {
+        const uint32_t a = colA(kk, i);
+        if (i < n - 1 && piv && kk < n && a) {
+          const PermTab T = perm_table(EXP[LOG[a] + lip]);  // a / piv
+          A[kk] ^= gf_mulc(A[i], T);
+#pragma unroll
+          for (int d = 0; d < KDL; d++) V[kk][d] ^= gf_mulc(V[i][d], T);
+        }
+      }
+    }
+    bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
+#pragma unroll
+    for (int i = 0; i < EM; i++) ub |= i < n && colA(i, i) == 0;
+    if (state && ub) {
+      if (q == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
+      state = 0;
+    }
+#pragma unroll
+    for (int i = EM - 1; i >= 0; i--) {  // back substitution :71-114; X_i replaces row i
+#pragma unroll
+      for (int u = i + 1; u < EM; u++) {
+        const uint32_t a = colA(i, u);
+        if (state && i < n && u < n && a) {
+          const PermTab T = perm_table(a);
+#pragma unroll
+          for (int d = 0; d < KDL; d++) V[i][d] ^= gf_mulc(V[u][d], T);
+        }
+      }
+      const uint32_t dg = colA(i, i);
+      if (state && i < n) {
+        const PermTab T = perm_table(EXP[255u - LOG[dg]]);  // 1 / diagonal
+#pragma unroll
+        for (int d = 0; d < KDL; d++) V[i][d] = gf_mulc(V[i][d], T);
+      }
+    }
+    if (state) {
+#pragma unroll
+      for (int i = 0; i < EM; i++) {
+        if (i < n) {
+          uint8_t *D = h + L.off_D + i * k;
+#pragma unroll
+          for (int d = 0; d < KDL; d++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++)
+              if (c0 + 4 * d + bb < k) D[c0 + 4 * d + bb] = (uint8_t)(V[i][d] >> (8 * bb));
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {  // dependency flags of the columns this lane owns
+            const int u = 4 * q + bb;
+            if (u < n) h[L.off_dep + i * em + u] = (u > i) && ((A[i] >> (8 * bb)) & 0xffu) != 0;
+          }
+          if (q == 0) {
+            h[L.off_nz + i] = 0;
+            h[L.off_unk + i] = (uint8_t)byte_at(U0, U1, i);
+            h[L.off_sel + i] = (uint8_t)byte_at(S0, S1, i);
+          }
+        }
+      }
+      if (q == 0) {
+        int u = 0;
+        for (int j = 0; j < k; j++)
+          h[L.off_slot + j] = ((miss >> j) & 1) ? (uint8_t)(0x80 | byte_at(S0, S1, u++)) : (uint8_t)j;
+        h[0] = FECGPU_BLOCK_RECOVERED;
+        h[1] = (uint8_t)n;
+      }
+    }
+    __syncthreads();
+    const uint32_t nrows = nblocks - base < BPW ? (uint32_t)(nblocks - base) : (uint32_t)BPW;
+    const uint32_t rdw = L.stride / 4, odw = orow / 4;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
+    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(OUTR);
+    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
+      const uint32_t row = x / rdw;
+      dst[x] = srcw[row * odw + (x - row * rdw)];
+    }
+    __syncthreads();
+  }
+}
+
 template <int RT, int W>
 __global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
                                                     const uint32_t *__restrict__ rep, uint64_t nblocks,
@@ -1623,10 +1832,11 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const size_t lane_lds = plan_lane_lds(k, r);
-  // FECGPU_PLAN=reg|lane|wave overrides the size rule (A/B experiments, cross-checks in the tests);
+  // FECGPU_PLAN=reg|tile|lane|wave overrides the size rule (A/B experiments, cross-checks in the tests);
   // read per call so a test process can compare the plan kernels on the same inputs
   const char *pe = getenv("FECGPU_PLAN");
-  const int force = pe && !strcmp(pe, "wave") ? 1 : pe && !strcmp(pe, "lane") ? 2 : pe && !strcmp(pe, "reg") ? 3 : 0;
+  const int force = pe && !strcmp(pe, "wave") ? 1 : pe && !strcmp(pe, "lane") ? 2 : pe && !strcmp(pe, "reg") ? 3
+                  : pe && !strcmp(pe, "tile") ? 4 : 0;
   const uint32_t em = ws_layout(k, r).em;
   if ((force == 0 || force == 3) && k <= 32 && em <= 8) {
     const size_t reg_lds = 768 + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
@@ -1639,6 +1849,23 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
     else if (em <= 4) FEC_PLAN_REG(8, 4);
     else FEC_PLAN_REG(8, 8);
 #undef FEC_PLAN_REG
+    HIPCHK(hipGetLastError());
+    return FECGPU_OK;
+  }
+  if ((force == 0 || force == 4) && k <= 64 && em <= 16) {  // FECGPU_PLAN=tile
+    constexpr int BPW = 16, EM = 16;  // k_rlc_plan_tile<4, 16>: 4 lanes per block
+    const size_t tile_lds = 768 + (size_t)BPW * EM * pad16(k) + (size_t)BPW * plan_out_row(ws_layout(k, r).stride);
+    if (tile_lds > 65536) {
+      static bool raised = false;
+      if (!raised) {
+        HIPCHK(hipFuncSetAttribute((const void *)k_rlc_plan_tile<4, 16>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        raised = true;
+      }
+    }
+    const uint64_t groups = (nblocks + BPW - 1) / BPW;
+    hipLaunchKernelGGL((k_rlc_plan_tile<4, 16>), dim3(grid_for(groups)), dim3(64), tile_lds, s, nblocks,
+                       (int)k, (int)r, fbn_base, fbn, src_present, rep_present, ws);
     HIPCHK(hipGetLastError());
     return FECGPU_OK;
   }

@@ -418,11 +418,13 @@ def _ws_fields(ws, k, r, n_blocks):
 
 
 @pytest.mark.parametrize("k,r,nb", [(1, 1, 64), (4, 1, 300), (16, 4, 2000), (12, 6, 700), (16, 8, 500),
-                                    (30, 3, 400), (32, 8, 600), (9, 9, 300)])
+                                    (30, 3, 400), (32, 8, 600), (9, 9, 300), (64, 16, 300), (40, 12, 200),
+                                    (61, 16, 100), (20, 16, 150)])
 def test_plan_kernels_agree(eng, k, r, nb):
-    """The three plan kernels (register lane-per-block, LDS lane-per-block, wave-per-block)
-    write identical decode records -- same unknowns, repair selection, solution rows D,
-    dependency flags, and the same reference-crash verdicts -- on random erasure patterns."""
+    """The plan kernels (register lane-per-block, tiled register, LDS lane-per-block,
+    wave-per-block) write identical decode records -- same unknowns, repair selection, solution
+    rows D, dependency flags, and the same reference-crash verdicts -- on random erasure
+    patterns.  Kernels whose size limits exclude (k, r) are skipped."""
     import os
     rng = np.random.default_rng(k * 1000 + r)
     sp = np.zeros((nb, 2), np.uint64)
@@ -438,7 +440,10 @@ def test_plan_kernels_agree(eng, k, r, nb):
     res = {}
     old = os.environ.get("FECGPU_PLAN")
     try:
-        for kind in ("reg", "lane", "wave"):
+        em = min(k, r)
+        kinds = [x for x, ok in (("reg", k <= 32 and em <= 8), ("tile", k <= 64 and em <= 16), ("lane", True),
+                                 ("wave", True)) if ok]
+        for kind in kinds:
             os.environ["FECGPU_PLAN"] = kind
             ws = eng.alloc_workspace(nb, k, r)
             ws.fill_(0xEE)
@@ -450,9 +455,10 @@ def test_plan_kernels_agree(eng, k, r, nb):
             os.environ.pop("FECGPU_PLAN", None)
         else:
             os.environ["FECGPU_PLAN"] = old
-    assert res["reg"] == res["lane"]
-    assert res["reg"] == res["wave"]
-    sts = {t[0] for t in res["reg"]}
+    first = res[kinds[0]]
+    for kind in kinds[1:]:
+        assert res[kind] == first, kind
+    sts = {t[0] for t in first}
     assert DEC_RECOVERED in sts
 
 
