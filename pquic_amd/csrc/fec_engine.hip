@@ -1476,12 +1476,12 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
         miss = m1 ? 127 - __clzll(m1) : 63 - __clzll(m0);  // LAST missing index (:54-58)
       }
     }
-    if (st == FECGPU_BLOCK_RECOVERED) {
-      V a = rep[b * (uint64_t)Lv + c];
+    if (st == FECGPU_BLOCK_RECOVERED) {  // streaming rows: non-temporal like the encode
+      V a = __builtin_nontemporal_load(rep + b * (uint64_t)Lv + c);
       const V *p = src + b * (uint64_t)k * Lv + c;
       for (int j = 0; j < k; j++)
-        if (j != miss) a = vxor(a, p[(uint64_t)j * Lv]);
-      src[(b * (uint64_t)k + miss) * Lv + c] = a;
+        if (j != miss) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
+      __builtin_nontemporal_store(a, src + (b * (uint64_t)k + miss) * Lv + c);
     }
     if (c == 0) {
       status[b] = (uint8_t)st;

@@ -37,6 +37,7 @@ def setup(k, r, nb, e, L):
     eng.rlc_encode(src, rep, k, r, L)
     sp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
     sp[:, 0] = (((1 << k) - 1) & ~((1 << e) - 1)) if k < 63 else -(1 << e)
+    sp[1::2, 0] = (((1 << k) - 1) & ~((1 << e) << 1)) if k < 63 else sp[1::2, 0]  # vary the erased slot
     rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
     rp[:, 0] = (1 << r) - 1
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -49,6 +50,8 @@ cases = []
 CASES = [(16, 4, 1 << 20, "enc", 1200), (16, 4, 1 << 20, "dec", 1200), (32, 8, 1 << 20, "enc", 1200)]
 if "--wide" in sys.argv:  # also the r >= 8 decode and configs[4] (jumbo symbols)
     CASES += [(32, 8, 1 << 19, "dec", 1200), (64, 16, 1 << 15, "enc", 9000), (64, 16, 1 << 15, "dec", 9000)]
+if "--xor" in sys.argv:  # the XOR scheme (configs[0]'s) at GPU scale
+    CASES += [(4, 1, 1 << 22, "xenc", 1200), (4, 1, 1 << 22, "xdec", 1200)]
 for (k, r, nb, mode, L) in CASES:
     bufs = setup(k, r, nb, min(k, r), L)
     cases.append((f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L, bufs))
@@ -58,6 +61,10 @@ def run(case, eng):
     _, k, r, nb, mode, L, (src, rep, sp, rp, st, rec, ws) = case
     if mode == "enc":
         eng.rlc_encode(src, rep, k, r, L)
+    elif mode == "xenc":
+        eng.xor_encode(src, rep, k, L)
+    elif mode == "xdec":
+        eng.xor_decode(src, rep, sp, rp, st, rec, k, L)
     else:
         eng.rlc_decode(src, rep, sp, rp, st, rec, k, r, L, workspace=ws)
 
