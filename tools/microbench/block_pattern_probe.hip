@@ -11,31 +11,40 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int K = 16, R = 4, L = 1200;
+#ifndef PK
+#define PK 16
+#define PR 4
+#define PL 1200
+#endif
+constexpr int K = PK, R = PR, L = PL;  // -DPK=32 -DPR=8 for configs[3]'s rows
 
 // wave per group of G blocks; ilv: group q = blocks q, q + NG, ...; else qG .. qG + G - 1
-template <int G, bool ILV, bool NTS>
+// WIDE: lane l holds 16-B pieces l and l + 64 (64 + 11 lanes per 1200-B row) instead of l and l + 38
+template <int G, bool ILV, bool NTS, bool WIDE = false>
 __global__ __launch_bounds__(64) void enc_pattern(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                   uint64_t nblocks) {
   const int lane = threadIdx.x;
-  if (lane >= 38) return;
-  const uint32_t o0 = 16 * lane, o1 = 16 * (lane + 38);
-  const bool ok1 = lane + 38 < 75;
+  constexpr int A = WIDE ? 64 : (L / 16 + 1) / 2;  // lanes of the first piece row
+  if (lane >= A) return;
+  const uint32_t o0 = 16 * lane, o1 = 16 * (lane + A);
+  const bool ok1 = lane + A < L / 16;
   const uint64_t NG = (nblocks + G - 1) / G;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
     for (int g = 0; g < G; g++) {
       const uint64_t b = ILV ? q + g * NG : q * G + g;
       if (b >= nblocks) break;
       const uint8_t *sb = src + b * K * L;
-      u32x4 a0[K], a1[K];
-#pragma unroll
-      for (int j = 0; j < K; j++) {  // all k rows in flight (the asm keeps P = 8 deep)
-        a0[j] = *(const u32x4 *)(sb + j * L + o0);
-        a1[j] = ok1 ? *(const u32x4 *)(sb + j * L + o1) : (u32x4)0;
-      }
       u32x4 x0 = 0, x1 = 0;
+      for (int j0 = 0; j0 < K; j0 += 8) {  // 8 rows in flight at a time (the asm keeps P = 4..8)
+        u32x4 a0[8], a1[8];
 #pragma unroll
-      for (int j = 0; j < K; j++) { x0 ^= a0[j]; x1 ^= a1[j]; }
+        for (int j = 0; j < 8; j++) {
+          a0[j] = j0 + j < K ? *(const u32x4 *)(sb + (j0 + j) * L + o0) : (u32x4)0;
+          a1[j] = (ok1 && j0 + j < K) ? *(const u32x4 *)(sb + (j0 + j) * L + o1) : (u32x4)0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) { x0 ^= a0[j]; x1 ^= a1[j]; }
+      }
       uint8_t *rb = rep + b * R * L;
 #pragma unroll
       for (int i = 0; i < R; i++) {
@@ -67,15 +76,17 @@ __global__ __launch_bounds__(64) void enc_pattern_persist(const uint8_t *__restr
       const uint64_t b = base + g * W + blockIdx.x;
       if (b >= nblocks) break;
       const uint8_t *sb = src + b * K * L;
-      u32x4 a0[K], a1[K];
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        a0[j] = *(const u32x4 *)(sb + j * L + o0);
-        a1[j] = ok1 ? *(const u32x4 *)(sb + j * L + o1) : (u32x4)0;
-      }
       u32x4 x0 = 0, x1 = 0;
+      for (int j0 = 0; j0 < K; j0 += 8) {
+        u32x4 a0[8], a1[8];
 #pragma unroll
-      for (int j = 0; j < K; j++) { x0 ^= a0[j]; x1 ^= a1[j]; }
+        for (int j = 0; j < 8; j++) {
+          a0[j] = j0 + j < K ? *(const u32x4 *)(sb + (j0 + j) * L + o0) : (u32x4)0;
+          a1[j] = (ok1 && j0 + j < K) ? *(const u32x4 *)(sb + (j0 + j) * L + o1) : (u32x4)0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) { x0 ^= a0[j]; x1 ^= a1[j]; }
+      }
       uint8_t *rb = rep + b * R * L;
 #pragma unroll
       for (int i = 0; i < R; i++) {
@@ -89,7 +100,7 @@ __global__ __launch_bounds__(64) void enc_pattern_persist(const uint8_t *__restr
 int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const uint64_t nb = 1 << 20;
+  const uint64_t nb = (uint64_t)(1 << 20) * 16 / K;  // ~20 GB of sources
   uint8_t *src, *rep;
   CK(hipMalloc(&src, nb * K * L)); CK(hipMalloc(&rep, nb * R * L));
   CK(hipMemset(src, 3, nb * K * L)); CK(hipMemset(rep, 0, nb * R * L));
@@ -115,10 +126,15 @@ int main() {
     run(nm, lds, enc_pattern<G, ILV, NTS>, (nb + G - 1) / G);
     RUNP(1, false, true)
     RUNP(4, false, true)
+    RUNP(8, true, true)
     RUNP(16, false, true)
     RUNP(4, true, true)
     RUNP(16, true, true)
     RUNP(16, true, false)
+    snprintf(nm, sizeof nm, "G16 interleaved WIDE lanes %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern<16, true, true, true>, (nb + 15) / 16);
+    snprintf(nm, sizeof nm, "G1 contiguous WIDE lanes %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern<1, false, true, true>, nb);
     if (lds) {
       for (int W : {3072, 2048, 6144}) {
         snprintf(nm, sizeof nm, "G16 persistent W=%d 3 waves/SIMD", W);
