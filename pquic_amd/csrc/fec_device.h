@@ -65,8 +65,8 @@ __device__ __forceinline__ uint32_t rlc_seed(uint32_t fbn, uint32_t i) {
 }
 
 // ---------------------------------------------------------------- GF(2^8) scalar ------
-__device__ __forceinline__ uint32_t gf_xtime(uint32_t a) {
-  return ((a << 1) ^ ((a & 0x80u) ? 0x1du : 0u)) & 0xffu;
+__device__ __forceinline__ uint32_t gf_xtime(uint32_t a) {  // a < 256
+  return (a << 1) ^ ((a >> 7) * 0x11du);  // the carry's 0x100 cancels bit 8 of a << 1
 }
 
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
@@ -95,33 +95,26 @@ __device__ __forceinline__ uint32_t gf_inv(uint32_t a) {
 // Five dwords per coefficient: {T0lo, T0hi, T1lo, T1hi} and T2.
 struct PermTab { uint4 t01; uint32_t t2; };
 
+__device__ __forceinline__ uint32_t bcast8(uint32_t x) {  // byte 0 of x in all four bytes
+  return __builtin_amdgcn_perm(0u, x, 0x00000000u);
+}
+
+// The 4-entry half tables {0, a, b, a^b} packed in one dword.
+__device__ __forceinline__ uint32_t pair_table(uint32_t a, uint32_t b) {
+  return (a << 8) | (b << 16) | ((a ^ b) << 24);
+}
+
 __device__ __forceinline__ PermTab perm_table(uint32_t c) {
   uint32_t p[8];
   p[0] = c;
 #pragma unroll
   for (int i = 1; i < 8; i++) p[i] = gf_xtime(p[i - 1]);  // c * 2^i
-  auto prod3 = [&](uint32_t x, int base) {                 // c * (x << base), x < 8
-    uint32_t v = 0;
-    if (x & 1) v ^= p[base];
-    if (x & 2) v ^= p[base + 1];
-    if (x & 4) v ^= p[base + 2];
-    return v;
-  };
+  // t01: bytes x = 0..7 of c * x[2:0] (dwords 0-1) and c * (x << 3) (dwords 2-3); the upper
+  // half of an 8-entry table is the lower half XOR the product of its top bit
   PermTab t;
-  uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (uint32_t x = 0; x < 8; x++) {
-    w[x >> 2] |= prod3(x, 0) << (8 * (x & 3));
-    w[2 + (x >> 2)] |= prod3(x, 3) << (8 * (x & 3));
-  }
-  t.t01 = make_uint4(w[0], w[1], w[2], w[3]);
-  uint32_t t2 = 0;
-#pragma unroll
-  for (uint32_t x = 0; x < 4; x++) {
-    uint32_t v = ((x & 1) ? p[6] : 0u) ^ ((x & 2) ? p[7] : 0u);
-    t2 |= v << (8 * x);
-  }
-  t.t2 = t2;
+  const uint32_t lo0 = pair_table(p[0], p[1]), lo3 = pair_table(p[3], p[4]);
+  t.t01 = make_uint4(lo0, lo0 ^ bcast8(p[2]), lo3, lo3 ^ bcast8(p[5]));
+  t.t2 = pair_table(p[6], p[7]);  // c * (x << 6), x < 4
   return t;
 }
 

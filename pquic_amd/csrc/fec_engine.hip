@@ -1421,13 +1421,9 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
     default: FN<16, 4>(__VA_ARGS__); break;                                        \
   }
 
-static bool use_perm_path() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("FECGPU_DATAPATH");
-    v = (e && strcmp(e, "perm") == 0) ? 1 : 0;
-  }
-  return v == 1;
+static bool use_perm_path() {  // FECGPU_DATAPATH=perm: the v_perm data path (A/B; read per call)
+  const char *e = getenv("FECGPU_DATAPATH");
+  return e && strcmp(e, "perm") == 0;
 }
 
 // =============================================================================================

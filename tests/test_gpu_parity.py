@@ -612,3 +612,40 @@ def test_roundtrip_k32_e8(eng, oracle):
         assert st_h[b] == stb[0], b
     del src, rep, work
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 300), (32, 8, 1200, 100), (7, 5, 2052, 60), (64, 16, 9000, 6)])
+def test_perm_datapath_vs_oracle(eng, oracle, k, r, L, nb):
+    """The v_perm data path (FECGPU_DATAPATH=perm, kept for A/B against the bitsliced one) gives
+    the same encode and decode bytes as the oracle."""
+    import os
+    rng = np.random.default_rng(k + 7 * r)
+    src_h = synth_bytes(nb * k * L, 3 + k).reshape(nb, k, L)
+    old = os.environ.get("FECGPU_DATAPATH")
+    os.environ["FECGPU_DATAPATH"] = "perm"
+    try:
+        src = to_dev(src_h)
+        rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
+        eng.rlc_encode(src, rep, k, r, L, fbn_base=41)
+        torch.cuda.synchronize()
+        rep_h = rep.cpu().numpy()
+        assert np.array_equal(rep_h, oracle.rlc_encode_batch(src_h, r, 41))
+        sp = np.zeros((nb, 2), np.uint64)
+        rp = np.zeros((nb, 2), np.uint64)
+        for b in range(nb):
+            e = int(rng.integers(0, min(k, r) + 1))
+            miss = set(rng.choice(k, e, replace=False).tolist())
+            sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+            rp[b] = masks_from_lists(1, r, [list(range(r))])[0]
+        work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=41)
+    finally:
+        if old is None:
+            os.environ.pop("FECGPU_DATAPATH", None)
+        else:
+            os.environ["FECGPU_DATAPATH"] = old
+    ref = work.copy()
+    st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, 41)
+    assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)
+    for b in range(nb):
+        for j in bits(rec[b], k):
+            assert np.array_equal(got[b, j], src_h[b, j])
