@@ -20,7 +20,7 @@ constexpr int K = PK, R = PR, L = PL;  // -DPK=32 -DPR=8 for configs[3]'s rows
 
 // wave per group of G blocks; ilv: group q = blocks q, q + NG, ...; else qG .. qG + G - 1
 // WIDE: lane l holds 16-B pieces l and l + 64 (64 + 11 lanes per 1200-B row) instead of l and l + 38
-template <int G, bool ILV, bool NTS, bool WIDE = false>
+template <int G, bool ILV, bool NTS, bool WIDE = false, bool NTL = false>
 __global__ __launch_bounds__(64) void enc_pattern(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                   uint64_t nblocks) {
   const int lane = threadIdx.x;
@@ -39,8 +39,9 @@ __global__ __launch_bounds__(64) void enc_pattern(const uint8_t *__restrict__ sr
         u32x4 a0[8], a1[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-          a0[j] = j0 + j < K ? *(const u32x4 *)(sb + (j0 + j) * L + o0) : (u32x4)0;
-          a1[j] = (ok1 && j0 + j < K) ? *(const u32x4 *)(sb + (j0 + j) * L + o1) : (u32x4)0;
+          const u32x4 *p0 = (const u32x4 *)(sb + (j0 + j) * L + o0), *p1 = (const u32x4 *)(sb + (j0 + j) * L + o1);
+          a0[j] = j0 + j < K ? (NTL ? __builtin_nontemporal_load(p0) : *p0) : (u32x4)0;
+          a1[j] = (ok1 && j0 + j < K) ? (NTL ? __builtin_nontemporal_load(p1) : *p1) : (u32x4)0;
         }
 #pragma unroll
         for (int j = 0; j < 8; j++) { x0 ^= a0[j]; x1 ^= a1[j]; }
@@ -97,6 +98,45 @@ __global__ __launch_bounds__(64) void enc_pattern_persist(const uint8_t *__restr
   }
 }
 
+// LIN: the same bytes, but each wave-instruction reads 1 KiB of the block's contiguous k x L
+// source region in order (lane l, instruction m: bytes 1024 m + 16 l), and writes the r x L repair
+// region the same way: every access is a run of whole 128-B lines except at region ends.  (A real
+// kernel would need an LDS transpose to get column-aligned symbols back; this measures whether the
+// denser shape is worth one.)
+template <int G, bool ILV, bool NTL = true>
+__global__ __launch_bounds__(64) void enc_pattern_lin(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                      uint64_t nblocks) {
+  const int lane = threadIdx.x;
+  constexpr int NP = K * L / 16, NI = (NP + 63) / 64;  // 16-B pieces, instructions per block
+  constexpr int RP = R * L / 16, RI = (RP + 63) / 64;
+  const uint64_t NG = (nblocks + G - 1) / G;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    for (int g = 0; g < G; g++) {
+      const uint64_t b = ILV ? q + g * NG : q * G + g;
+      if (b >= nblocks) break;
+      const uint8_t *sb = src + b * K * L;
+      u32x4 x = 0;
+      for (int m0 = 0; m0 < NI; m0 += 8) {
+        u32x4 a[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+          const int pc = (m0 + m) * 64 + lane;
+          const u32x4 *pp = (const u32x4 *)(sb + 16 * pc);
+          a[m] = (m0 + m < NI && pc < NP) ? (NTL ? __builtin_nontemporal_load(pp) : *pp) : (u32x4)0;
+        }
+#pragma unroll
+        for (int m = 0; m < 8; m++) x ^= a[m];
+      }
+      uint8_t *rb = rep + b * R * L;
+#pragma unroll
+      for (int m = 0; m < RI; m++) {
+        const int pc = m * 64 + lane;
+        if (pc < RP) __builtin_nontemporal_store(x + (uint32_t)m, (u32x4 *)(rb + 16 * pc));
+      }
+    }
+  }
+}
+
 int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -135,6 +175,19 @@ int main() {
     run(nm, lds, enc_pattern<16, true, true, true>, (nb + 15) / 16);
     snprintf(nm, sizeof nm, "G1 contiguous WIDE lanes %s", lds ? "3 waves/SIMD" : "max occupancy");
     run(nm, lds, enc_pattern<1, false, true, true>, nb);
+    snprintf(nm, sizeof nm, "G1 contiguous LIN %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern_lin<1, false>, nb);
+    snprintf(nm, sizeof nm, "G4 interleaved LIN %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern_lin<4, true>, (nb + 3) / 4);
+    snprintf(nm, sizeof nm, "G16 interleaved LIN %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern_lin<16, true>, (nb + 15) / 16);
+    snprintf(nm, sizeof nm, "G16 interleaved LIN ld-default %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern_lin<16, true, false>, (nb + 15) / 16);
+    snprintf(nm, sizeof nm, "G16 interleaved nt loads %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern<16, true, true, false, true>, (nb + 15) / 16);
+    snprintf(nm, sizeof nm, "G1 contiguous nt loads %s", lds ? "3 waves/SIMD" : "max occupancy");
+    run(nm, lds, enc_pattern<1, false, true, false, true>, nb);
+    if (getenv("LIN_ONLY")) continue;
     if (lds) {
       for (int W : {3072, 2048, 6144}) {
         snprintf(nm, sizeof nm, "G16 persistent W=%d 3 waves/SIMD", W);
