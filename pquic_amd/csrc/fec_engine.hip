@@ -1421,6 +1421,33 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
     default: FN<16, 4>(__VA_ARGS__); break;                                        \
   }
 
+// The case tails build jump targets from the table's upper address bits and a 16-bit offset, so
+// the table must sit on a 64 KiB boundary at run time (the code object asks for it: .p2align 16).
+// Checked once per device, on a private stream, before the first bitsliced launch; a misplaced
+// table fails the call instead of jumping into the wrong code.
+static std::atomic<int> g_tab_state[64];  // 0 unknown, 1 checked, -1 misaligned
+static int bs_table_check() {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return set_err(FECGPU_ERR_NO_DEVICE, "%s", "device index out of range");
+  int st = g_tab_state[dev].load();
+  if (st == 0) {
+    uint64_t *d = nullptr, h = 0;
+    hipStream_t ps;
+    HIPCHK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&d, sizeof(uint64_t)));
+    hipLaunchKernelGGL(fec_bs_case_table_addr, dim3(1), dim3(64), 0, ps, d);
+    HIPCHK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, ps));
+    HIPCHK(hipStreamSynchronize(ps));
+    HIPCHK(hipFree(d));
+    HIPCHK(hipStreamDestroy(ps));
+    st = (h != 0 && (h & 0xFFFF) == 0) ? 1 : -1;
+    g_tab_state[dev].store(st);
+  }
+  if (st < 0) return set_err(FECGPU_ERR_HIP, "%s", "GF(256) case table is not 64 KiB-aligned in device memory");
+  return FECGPU_OK;
+}
+
 static bool use_perm_path() {  // FECGPU_DATAPATH=perm: the v_perm data path (A/B; read per call)
   const char *e = getenv("FECGPU_DATAPATH");
   return e && strcmp(e, "perm") == 0;
@@ -1706,7 +1733,12 @@ int fecgpu_init(int device) {
   HIPCHK(hipGetDeviceProperties(&p, device));
   if (strncmp(p.gcnArchName, "gfx950", 6) != 0)
     return set_err(FECGPU_ERR_NO_DEVICE, "device is %s, engine is built for gfx950", p.gcnArchName);
-  return FECGPU_OK;
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  if (cur != device) HIPCHK(hipSetDevice(device));
+  const int rc = bs_table_check();
+  if (cur != device) HIPCHK(hipSetDevice(cur));
+  return rc;
 }
 
 void fecgpu_get_stats(fecgpu_stats_t *out) {
@@ -1752,6 +1784,7 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
                       cfg, fbn_base, fbn, r0, s)
     }
   } else {
+    if (int rc2 = bs_table_check()) return rc2;
     const BsCfg cfg = pick_bs_cfg((int)symbol_size);
     const EncTile et = pick_enc_tile(r);
     const int rt = et.rt;
@@ -1771,6 +1804,7 @@ int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t st
   int rc = check_common(symbols, rep, nwindows, k, r, symbol_size);
   if (rc || nwindows == 0 || r == 0) return rc;
   if (step == 0) return set_err(FECGPU_ERR_INVALID, "%s", "window step must be >= 1");
+  if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const int rt = pick_rt(r);
   for (int r0 = 0; r0 < (int)r; r0 += rt) {
@@ -1929,6 +1963,7 @@ static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64
     HIPCHK(hipGetLastError());
     return launch_finalize(nblocks, k, r, status, recovered, ws, s);
   }
+  if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const bool fused = (int)L.em <= rt;  // one pass covers every unknown of every block
   for (int r0 = 0; r0 < (int)L.em; r0 += rt) {

@@ -14,13 +14,14 @@ How a lane computes  acc_i += c_ij * S_j  over GF(2^8)/0x11D for 32 bytes at a t
   v_bitop3_b32 (3-input XOR):  acc_o ^= TL[row_o & 15] ^ TH[row_o >> 4].
   A coefficient therefore costs at most 8 full-rate VALU ops per 32 bytes.
 * Dispatch.  The 8 register indices depend on the wave-uniform coefficient c, so the code
-  is selected per coefficient from a shared table of 256 cases (88 bytes each, 32 KiB-aligned,
+  is selected per coefficient from a shared table of 256 cases (80 bytes each, 64 KiB-aligned,
   entry 0 a return stub).  The case code names the accumulator planes as v0..v7;
   s_set_gpr_idx_on(SRC0,DST) relocates them to repair i's accumulators (ACC_BASE + 8 i), while
   the table operands (SRC1/SRC2) stay absolute.  Cases are CHAINED: the wrapper stages each
   source's coefficients as 16-bit case offsets ((c + 1) * 88, 0 = end), four to a 64-bit SGPR
   queue; the caller enters the first case with s_swappc_b64, and every case's tail advances M0
-  by 8, shifts the queue and jumps straight to the next case (the zero field lands on the stub,
+  by 8, shifts the queue, packs the next field under TAB's address bits and jumps straight to
+  the next case (3 SALU + the branch) (the zero field lands on the stub,
   which returns).  One taken branch per coefficient instead of a call and a return; tiles with
   fewer live repairs (rt < RT) end their chain early.
 * Output.  The same three exchange rounds are an involution, so applying them to the
@@ -47,12 +48,12 @@ COPTR = 66
 INPTR = 67   # decode only
 OUTPTR = 68  # decode only
 DATA_BASE = 68  # encode; decode data buffers start at 70 (tuples must start on an even VGPR)
-CASE_BYTES = 88  # <= 8 VOP3 (64 B) + the 20-byte chain tail; table entry 0 is the return stub
+CASE_BYTES = 80  # <= 8 VOP3 (64 B) + the 16-byte chain tail; table entry 0 is the return stub
 # stage-0 destinations (scratch, overwritten by the combos), stage-2 destinations (planes)
 XS = [TL[3], TL[5], TL[6], TL[7], TH[3], TH[5], TH[6], TH[7]]
 PL = [TL[1], TL[2], TL[4], TL[8], TH[1], TH[2], TH[4], TH[8]]
 # SGPRs owned by the asm bodies
-S_TAB, S_TGT, S_RET, S_T, S_J = 60, 62, 64, 66, 67
+S_TAB, S_TGT, S_RET, S_TABHI, S_J = 60, 62, 64, 66, 67  # S_TABHI = TAB.lo >> 16
 S_C = [68, 69, 70, 71]  # coefficient-field dwords of the current source (readfirstlane of CO)
 S_CQ = 84        # chain queue: the remaining 16-bit case offsets of the running chain (shared with
                  # the decode epilogue's exec save, which never overlaps a chain)
@@ -148,7 +149,7 @@ def v(n):
 
 
 def emit_table():
-    lines = ['  .text', '  .p2align 15', '  .globl fec_bs_case_table', '  .hidden fec_bs_case_table', 'fec_bs_case_table:']
+    lines = ['  .text', '  .p2align 16', '  .globl fec_bs_case_table', '  .hidden fec_bs_case_table', 'fec_bs_case_table:']
     # entry 0: the chain's end (a zero field) returns to the caller
     lines.append(f"  s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
     lines.append(f"  .org fec_bs_case_table + {CASE_BYTES}")
@@ -164,8 +165,7 @@ def emit_table():
         # chain tail: next repair's accumulators, next 16-bit case offset, jump (entry 0 returns)
         body += [f"s_add_u32 m0, m0, 8",
                  f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
-                 f"s_pack_ll_b32_b16 s{S_T}, s{S_CQ}, 0",
-                 f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}",
+                 f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}",
                  f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
         lines += ["  " + b for b in body]
         lines.append(f"  .org fec_bs_case_table + {CASE_BYTES * (c + 2)}")
@@ -262,7 +262,10 @@ def body(mode: str, RT: int, VEC: int, P: int):
     a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
     a(f"s_add_u32 s{S_TAB}, s{S_TAB}, fec_bs_case_table@rel32@lo+4")
     a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, fec_bs_case_table@rel32@hi+12")
-    # the table is one 32 KiB-aligned block: every target shares TAB's high word
+    # the table is 64 KiB-aligned and 20 KiB long: a target is TAB's upper 48 bits with the case
+    # offset as its low 16 (s_pack_ll of the queue field and TAB.lo >> 16); the engine checks the
+    # alignment on the device before the first launch (fec_bs_case_table_addr)
+    a(f"s_lshr_b32 s{S_TABHI}, s{S_TAB}, 16")
     a(f"s_mov_b32 s{S_TGT + 1}, s{S_TAB + 1}")
     a(f"s_getpc_b64 s[{S_EPI}:{S_EPI + 1}]")
     a(".Lepipc_%=:")
@@ -349,8 +352,7 @@ def body(mode: str, RT: int, VEC: int, P: int):
                 for w in range(4):
                     a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
             a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
-            a(f"s_pack_ll_b32_b16 s{S_T}, s{S_CQ}, 0")
-            a(f"s_add_u32 s{S_TGT}, s{S_TAB}, s{S_T}")
+            a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
             if ch % 2 == 0:  # chain 1 continues M0 where chain 0 left it (4 cases later)
                 a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
             a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
@@ -512,6 +514,19 @@ def main():
              '    "s_endpgm\\n"']
     parts += [f'    "{ln}\\n"' for ln in emit_table()]
     parts += ['    "  s_endpgm\\n");', "}", ""]
+    parts += ["// The table's runtime address (the case tails build targets as TAB.hi:TAB.lo[31:16]:offset,",
+              "// which needs 64 KiB alignment): the engine checks it once per device before any launch.",
+              "__global__ void fec_bs_case_table_addr(uint64_t *out) {",
+              "  uint32_t lo, hi;",
+              "  asm volatile(",
+              '    "s_getpc_b64 s[60:61]\\n"',
+              '    "s_add_u32 s60, s60, fec_bs_case_table@rel32@lo+4\\n"',
+              '    "s_addc_u32 s61, s61, fec_bs_case_table@rel32@hi+12\\n"',
+              '    "s_mov_b32 %0, s60\\n"',
+              '    "s_mov_b32 %1, s61\\n"',
+              '    : "=s"(lo), "=s"(hi) : : "s60", "s61");',
+              "  if (threadIdx.x == 0) out[0] = ((uint64_t)hi << 32) | lo;",
+              "}", ""]
     tops = {}
     for mode in ("enc", "dec"):
         for RT, VEC in CONFIGS:
