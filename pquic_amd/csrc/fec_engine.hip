@@ -1460,35 +1460,41 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <typename V>
 __device__ __forceinline__ V vxor(V a, V b) { return a ^ b; }
 
-template <typename V>
+// One thread per 16-B (or 4-B) column piece of a block.  KC > 0: k fixed at compile time, so
+// the k row loads are issued back to back; I: 32-bit index arithmetic when nblocks * Lv < 2^32
+// (a 64-bit division per piece is most of the non-memory work otherwise).
+template <typename V, int KC, typename I>
 __global__ __launch_bounds__(256) void k_xor_encode(const V *__restrict__ src, V *__restrict__ rep,
-                                                    uint64_t nblocks, int k, int Lv) {
-  const uint64_t total = nblocks * (uint64_t)Lv;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t b = t / (uint64_t)Lv, c = t - b * (uint64_t)Lv;
-    const V *p = src + b * (uint64_t)k * Lv + c;
+                                                    uint64_t nblocks, int k_rt, int Lv_rt) {
+  const int k = KC ? KC : k_rt;
+  const I Lv = (I)Lv_rt, total = (I)(nblocks * (uint64_t)Lv_rt);
+  for (I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x; t < total; t += (I)gridDim.x * (I)blockDim.x) {
+    const I b = t / Lv, c = t - b * Lv;
+    const V *p = src + (uint64_t)b * (uint64_t)k * (uint64_t)Lv + c;
     V a = __builtin_nontemporal_load(p);
-    for (int j = 1; j < k; j++) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
-    __builtin_nontemporal_store(a, rep + b * (uint64_t)Lv + c);
+#pragma unroll
+    for (int j = 1; j < (KC ? KC : 1); j++) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
+    if (!KC)
+      for (int j = 1; j < k; j++) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
+    __builtin_nontemporal_store(a, rep + (uint64_t)b * Lv + c);
   }
 }
 
 // xor_fec_scheme.c:41-74.  status: RECOVERED when exactly the preconditions hold and the
 // repair is present; REF_UB when they hold with the repair absent (NULL dereference).
-template <typename V>
+template <typename V, int KC, typename I>
 __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V *__restrict__ rep,
-                                                    uint64_t nblocks, int k, int Lv,
+                                                    uint64_t nblocks, int k_rt, int Lv_rt,
                                                     const uint64_t *sp, const uint64_t *rp,
                                                     uint8_t *status, uint64_t *recovered) {
-  const uint64_t total = nblocks * (uint64_t)Lv;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t b = t / (uint64_t)Lv, c = t - b * (uint64_t)Lv;
-    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1];
+  const int k = KC ? KC : k_rt;
+  const I Lv = (I)Lv_rt, total = (I)(nblocks * (uint64_t)Lv_rt);
+  for (I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x; t < total; t += (I)gridDim.x * (I)blockDim.x) {
+    const I b = t / Lv, c = t - b * Lv;
+    uint64_t s0 = sp[2 * (uint64_t)b], s1 = sp[2 * (uint64_t)b + 1];
     if (k < 64) { s0 &= (1ull << k) - 1; s1 = 0; } else if (k < 128) s1 &= (1ull << (k - 64)) - 1;
     const int cur_ss = __popcll(s0) + __popcll(s1);
-    const int cur_rs = (int)(rp[2 * b] & 1);
+    const int cur_rs = (int)(rp[2 * (uint64_t)b] & 1);
     int st = FECGPU_BLOCK_NOTHING, miss = -1;
     if (cur_ss + cur_rs == k) {
       if (!cur_rs) st = FECGPU_BLOCK_REF_UB;
@@ -1500,18 +1506,58 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
       }
     }
     if (st == FECGPU_BLOCK_RECOVERED) {  // streaming rows: non-temporal like the encode
-      V a = __builtin_nontemporal_load(rep + b * (uint64_t)Lv + c);
-      const V *p = src + b * (uint64_t)k * Lv + c;
-      for (int j = 0; j < k; j++)
-        if (j != miss) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
-      __builtin_nontemporal_store(a, src + (b * (uint64_t)k + miss) * Lv + c);
+      const V *p = src + (uint64_t)b * (uint64_t)k * Lv + c;
+      V a = __builtin_nontemporal_load(rep + (uint64_t)b * Lv + c);
+      if (KC) {  // exactly one source is missing: the k - 1 present rows, loads back to back
+#pragma unroll
+        for (int jj = 0; jj < (KC ? KC - 1 : 1); jj++)
+          a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)(jj + (jj >= miss)) * Lv));
+      } else {
+        for (int j = 0; j < k; j++)
+          if (j != miss) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
+      }
+      __builtin_nontemporal_store(a, src + ((uint64_t)b * k + miss) * Lv + c);
     }
     if (c == 0) {
       status[b] = (uint8_t)st;
-      recovered[2 * b] = (st == FECGPU_BLOCK_RECOVERED && miss < 64) ? 1ull << miss : 0;
-      recovered[2 * b + 1] = (st == FECGPU_BLOCK_RECOVERED && miss >= 64) ? 1ull << (miss - 64) : 0;
+      recovered[2 * (uint64_t)b] = (st == FECGPU_BLOCK_RECOVERED && miss < 64) ? 1ull << miss : 0;
+      recovered[2 * (uint64_t)b + 1] = (st == FECGPU_BLOCK_RECOVERED && miss >= 64) ? 1ull << (miss - 64) : 0;
     }
   }
+}
+
+// k = 2..8 and 16 get a compile-time row count; other k take the runtime loop.
+struct XorEnc {
+  template <typename V, int KC, typename I, typename... A>
+  static void go(uint32_t grid, hipStream_t s, A... a) {
+    hipLaunchKernelGGL((k_xor_encode<V, KC, I>), dim3(grid), dim3(256), 0, s, a...);
+  }
+};
+struct XorDec {
+  template <typename V, int KC, typename I, typename... A>
+  static void go(uint32_t grid, hipStream_t s, A... a) {
+    hipLaunchKernelGGL((k_xor_decode<V, KC, I>), dim3(grid), dim3(256), 0, s, a...);
+  }
+};
+template <typename V, typename OP, typename I, typename... A>
+static void xor_dispatch_k(uint32_t k, uint32_t grid, hipStream_t s, A... a) {
+  switch (k) {
+    case 2: OP::template go<V, 2, I>(grid, s, a...); break;
+    case 3: OP::template go<V, 3, I>(grid, s, a...); break;
+    case 4: OP::template go<V, 4, I>(grid, s, a...); break;
+    case 5: OP::template go<V, 5, I>(grid, s, a...); break;
+    case 6: OP::template go<V, 6, I>(grid, s, a...); break;
+    case 8: OP::template go<V, 8, I>(grid, s, a...); break;
+    case 16: OP::template go<V, 16, I>(grid, s, a...); break;
+    default: OP::template go<V, 0, I>(grid, s, a...); break;
+  }
+}
+template <typename V, typename OP, typename... A>
+static void xor_dispatch(uint32_t k, uint64_t total, uint32_t grid, hipStream_t s, A... a) {
+  const char *e = getenv("FECGPU_XOR_GENERIC");  // A/B: the runtime-k, 64-bit-index kernel
+  if (e && atoi(e)) return xor_dispatch_k<V, OP, uint64_t>(0, grid, s, a...);
+  if (total < (1ull << 32) - (uint64_t)grid * 256) xor_dispatch_k<V, OP, uint32_t>(k, grid, s, a...);
+  else xor_dispatch_k<V, OP, uint64_t>(k, grid, s, a...);
 }
 
 // FEC frames for batched repair symbols (the block framework's get_repair_payload_from_queue +
@@ -1827,11 +1873,9 @@ int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   const uint64_t total = nblocks * (uint64_t)Lv;
   const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
   if (v4)
-    hipLaunchKernelGGL(k_xor_encode<u32x4>, dim3(grid), dim3(256), 0, s, (const u32x4 *)src, (u32x4 *)rep,
-                       nblocks, (int)k, Lv);
+    xor_dispatch<u32x4, XorEnc>(k, total, grid, s, (const u32x4 *)src, (u32x4 *)rep, nblocks, (int)k, Lv);
   else
-    hipLaunchKernelGGL(k_xor_encode<uint32_t>, dim3(grid), dim3(256), 0, s, (const uint32_t *)src,
-                       (uint32_t *)rep, nblocks, (int)k, Lv);
+    xor_dispatch<uint32_t, XorEnc>(k, total, grid, s, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, Lv);
   HIPCHK(hipGetLastError());
   g_stats[0]++;
   g_stats[1] += nblocks;
@@ -2018,12 +2062,11 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   const uint64_t total = nblocks * (uint64_t)Lv;
   const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
   if (v4)
-    hipLaunchKernelGGL(k_xor_decode<u32x4>, dim3(grid), dim3(256), 0, s, (u32x4 *)src, (const u32x4 *)rep,
-                       nblocks, (int)k, Lv, src_present, rep_present, status, recovered);
+    xor_dispatch<u32x4, XorDec>(k, total, grid, s, (u32x4 *)src, (const u32x4 *)rep, nblocks, (int)k, Lv,
+                                src_present, rep_present, status, recovered);
   else
-    hipLaunchKernelGGL(k_xor_decode<uint32_t>, dim3(grid), dim3(256), 0, s, (uint32_t *)src,
-                       (const uint32_t *)rep, nblocks, (int)k, Lv, src_present, rep_present, status,
-                       recovered);
+    xor_dispatch<uint32_t, XorDec>(k, total, grid, s, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k,
+                                   Lv, src_present, rep_present, status, recovered);
   HIPCHK(hipGetLastError());
   g_stats[2]++;
   g_stats[3] += nblocks;
