@@ -1556,8 +1556,11 @@ template <typename V, typename OP, typename... A>
 static void xor_dispatch(uint32_t k, uint64_t total, uint32_t grid, hipStream_t s, A... a) {
   const char *e = getenv("FECGPU_XOR_GENERIC");  // A/B: the runtime-k, 64-bit-index kernel
   if (e && atoi(e)) return xor_dispatch_k<V, OP, uint64_t>(0, grid, s, a...);
-  if (total < (1ull << 32) - (uint64_t)grid * 256) xor_dispatch_k<V, OP, uint32_t>(k, grid, s, a...);
-  else xor_dispatch_k<V, OP, uint64_t>(k, grid, s, a...);
+  const char *w = getenv("FECGPU_XOR_IDX64");  // tests: the 64-bit-index instantiations at small sizes
+  if (total < (1ull << 32) - (uint64_t)grid * 256 && !(w && atoi(w)))
+    xor_dispatch_k<V, OP, uint32_t>(k, grid, s, a...);
+  else
+    xor_dispatch_k<V, OP, uint64_t>(k, grid, s, a...);
 }
 
 // FEC frames for batched repair symbols (the block framework's get_repair_payload_from_queue +

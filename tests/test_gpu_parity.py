@@ -238,9 +238,15 @@ def test_decode_zero_symbol_propagation(eng, oracle):
             assert np.array_equal(got[b, j], src_h[b, j])
 
 
-def test_xor_vs_oracle(eng, oracle):
+@pytest.mark.parametrize("knob", [None, "FECGPU_XOR_GENERIC", "FECGPU_XOR_IDX64"])
+def test_xor_vs_oracle(eng, oracle, knob, monkeypatch):
+    """XOR encode/recover vs the oracle: the k-specialised kernels (k = 2..8, 16; 16-B and 4-B
+    pieces), the runtime-k kernel, and the 64-bit-index instantiations."""
+    if knob:
+        monkeypatch.setenv(knob, "1")
     rng = np.random.default_rng(9)
-    for k, L, nb in [(4, 1200, 1000), (1, 4, 10), (7, 36, 300), (100, 64, 20), (128, 16, 9)]:
+    for k, L, nb in [(4, 1200, 1000), (1, 4, 10), (7, 36, 300), (100, 64, 20), (128, 16, 9), (2, 1216, 50),
+                     (3, 48, 70), (5, 1200, 40), (6, 20, 33), (8, 36, 64), (16, 1200, 30), (16, 4, 17)]:
         src_h = synth_bytes(nb * k * L, k).reshape(nb, k, L)
         rep = torch.empty((nb, 1, L), dtype=torch.uint8, device=DEV)
         eng.xor_encode(to_dev(src_h), rep, k, L)
