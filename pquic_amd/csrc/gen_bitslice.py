@@ -45,8 +45,9 @@ TH = {n: T_BASE + 15 + n - 1 for n in range(1, 16)}     # v47..v61
 TMP = [62, 63, 64, 65]
 CO = TMP  # coefficient fields: read into the transpose temporaries once the transpose is done
 COPTR = 66
-INPTR = 67   # decode only
+INPTR = 67   # decode only: next entry of the input-address table
 OUTPTR = 68  # decode only
+NADDR = 70   # decode only: the next source's address, read from the table one source ahead
 DATA_BASE = 68  # encode; decode data buffers start at 70 (tuples must start on an even VGPR)
 CASE_BYTES = 80  # <= 8 VOP3 (64 B) + the 16-byte chain tail; table entry 0 is the return stub
 # stage-0 destinations (scratch, overwritten by the combos), stage-2 destinations (planes)
@@ -281,6 +282,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
     else:
         a(f"v_mov_b32 v{INPTR}, %[intab]")
+        a(f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}")  # source 0's address
+        a(f"v_add_u32 v{INPTR}, 8, v{INPTR}")
         a(f"v_mov_b32 v{OUTPTR}, %[outtab]")
     a(f"s_mov_b32 s{S_S}, 0")
     a(f"s_mov_b32 s{S_J}, 0")
@@ -290,11 +293,13 @@ def body(mode: str, RT: int, VEC: int, P: int):
     def load_source(buf):
         out = []
         if mode == "dec":
-            out += [f"ds_read_b64 v[{TMP[0]}:{TMP[1]}], v{INPTR}",
-                    f"v_add_u32 v{INPTR}, 8, v{INPTR}",
-                    "s_waitcnt lgkmcnt(0)",
-                    f"v_readfirstlane_b32 s{S_CUR}, v{TMP[0]}",
-                    f"v_readfirstlane_b32 s{S_CUR + 1}, v{TMP[1]}"]
+            # this source's address was read one source ago (nothing else of the LDS queue is
+            # outstanding here, so the wait is free); then fetch the next one
+            out += ["s_waitcnt lgkmcnt(0)",
+                    f"v_readfirstlane_b32 s{S_CUR}, v{NADDR}",
+                    f"v_readfirstlane_b32 s{S_CUR + 1}, v{NADDR + 1}",
+                    f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}",
+                    f"v_add_u32 v{INPTR}, 8, v{INPTR}"]
         for q in range(NP):
             out += [f"s_mov_b64 exec, %[vm{q}]",
                     f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
@@ -459,7 +464,7 @@ DEC_REC_NZ = 144
 
 
 def data_base(mode: str) -> int:
-    return DATA_BASE if mode == "enc" else OUTPTR + 2  # tuples must start on an even VGPR
+    return DATA_BASE if mode == "enc" else NADDR + 2  # tuples must start on an even VGPR
 
 
 def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
