@@ -326,6 +326,10 @@ def body(mode: str, RT: int, VEC: int, P: int):
     dsr = "ds_read_b64" if csb == 8 else "ds_read_b128"
     ndw = min(4, csb // 4)
     nch = max(1, RT // 4)  # chains of up to 4 cases (one 64-bit queue each)
+    # the common path of every source step falls through: the prefetch-less tail steps and the
+    # block-end epilogue calls are out of line (after the loop), so a step costs no taken branch
+    # besides its case chains
+    ool = []
     for b in range(P):
         nb = (b + P - 1) % P
         a(f".Lbody{b}_%=:")
@@ -334,10 +338,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_cbranch_scc0 .Lnopf{b}_%=")
         L.extend(load_source(nb))
         a(f"s_waitcnt vmcnt({NP * (P - 1)})")
-        a(f"s_branch .Lpf{b}_%=")
-        a(f".Lnopf{b}_%=:")
-        a("s_waitcnt vmcnt(0)")
         a(f".Lpf{b}_%=:")
+        ool += [f".Lnopf{b}_%=:", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
         L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
         # the coefficient fields land in the (now free) transpose temporaries under the combos
         a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
@@ -365,13 +367,14 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_add_u32 s{S_S}, s{S_S}, 1")
         a(f"s_add_u32 s{S_J}, s{S_J}, 1")
         a(f"s_cmp_eq_u32 s{S_J}, %[k]")
-        a(f"s_cbranch_scc0 .Lnoepi{b}_%=")
-        a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]")
-        a(f"s_mov_b32 s{S_J}, 0")
+        a(f"s_cbranch_scc1 .Lepicall{b}_%=")
         a(f".Lnoepi{b}_%=:")
         a(f"s_cmp_lt_u32 s{S_S}, %[nsrc]")
         a(f"s_cbranch_scc0 .Lexit_%=")
+        ool += [f".Lepicall{b}_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
+                f"s_mov_b32 s{S_J}, 0", f"s_branch .Lnoepi{b}_%="]
     a(f"s_branch .Lbody0_%=")
+    L.extend(ool)
 
     # ---- per-block epilogue subroutine ----
     a(".Lepi_%=:")

@@ -77,7 +77,8 @@ def test_encode_golden(eng):
 
 @pytest.mark.parametrize("k,r,L,nb", [(1, 1, 4, 7), (3, 2, 12, 33), (16, 4, 1200, 257), (32, 8, 1200, 129),
                                       (64, 16, 9000, 9), (100, 20, 1200, 5), (128, 128, 64, 3),
-                                      (7, 5, 2052, 17), (20, 3, 4096, 11), (5, 17, 300, 13)])
+                                      (7, 5, 2052, 17), (20, 3, 4096, 11), (5, 17, 300, 13),
+                                      (3, 2, 65532, 3), (16, 4, 1204, 65)])  # largest symbol; L % 16 == 4
 def test_encode_vs_oracle(eng, oracle, k, r, L, nb):
     src_h = synth_bytes(nb * k * L, 1000 + k * r).reshape(nb, k, L)
     src = to_dev(src_h)
@@ -182,7 +183,7 @@ def test_decode_golden(eng):
 @pytest.mark.parametrize("k,r,L,nb,emax", [(4, 1, 1200, 300, 1), (16, 4, 1200, 500, 4), (32, 8, 1200, 200, 8),
                                            (8, 8, 40, 600, 8), (64, 16, 9000, 12, 16), (100, 30, 64, 40, 30),
                                            (128, 128, 8, 6, 128), (10, 3, 4, 200, 3), (12, 6, 2100, 300, 6),
-                                           (40, 20, 4100, 30, 20)])
+                                           (40, 20, 4100, 30, 20), (4, 3, 65532, 8, 3), (16, 4, 1204, 200, 4)])
 def test_decode_vs_oracle(eng, oracle, k, r, L, nb, emax):
     rng = np.random.default_rng(k * 131 + r)
     src_h = synth_bytes(nb * k * L, 77 + k).reshape(nb, k, L)
