@@ -1145,15 +1145,22 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
   else BS_CALL_DEC(16);
 }
 
-// blocks per group: 64 / RT coefficient lanes per block, bounded by the LDS budget
-__host__ __device__ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes) {
+// Blocks per group: at most 64 / RT (one coefficient lane per (block, repair)), bounded by the LDS
+// budget.  Defaults measured in-process (profiles/r01_ab_group.log, two boxes): encode tiles of 4
+// repairs stream groups of 4 blocks (k16 r4 -2.6..-3.1 % against 16); symbols wider than one
+// column chunk (L > 2 KiB) go one block per group (k64 r16 L9000 encode -2.3 %, decode -8.3 %:
+// the chunk passes then revisit one block's rows); everything else keeps 64 / RT.
+// FECGPU_GROUP=N replaces the defaults with a plain cap (A/B experiments).
+static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, bool enc, int nchunks) {
   int g = 64 / RT;
-#ifndef __HIP_DEVICE_COMPILE__
-  if (const char *e = getenv("FECGPU_GROUP")) {  // A/B experiments: cap the blocks per group
+  if (const char *e = getenv("FECGPU_GROUP")) {
     const int cap = atoi(e);
     while (g > 1 && g > cap) g >>= 1;
+  } else if (nchunks > 1) {
+    g = 1;
+  } else if (enc && RT == 4) {
+    g = 4;
   }
-#endif
   while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
   return g;
 }
@@ -1391,7 +1398,7 @@ template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                              hipStream_t s) {
-  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0) : 1;
+  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks) : 1;
   const size_t lds = (size_t)W * G * k * FEC_BS_COEF_ROW_BYTES(RT);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
@@ -1402,7 +1409,7 @@ template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                               uint8_t *dst) {
-  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80);
+  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks);
   const size_t lds = RecoverLds<RT>::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
