@@ -1146,10 +1146,12 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
 }
 
 // Blocks per group: at most 64 / RT (one coefficient lane per (block, repair)), bounded by the LDS
-// budget.  Defaults measured in-process (profiles/r01_ab_group.log, two boxes): encode tiles of 4
-// repairs stream groups of 4 blocks (k16 r4 -2.6..-3.1 % against 16); symbols wider than one
-// column chunk (L > 2 KiB) go one block per group (k64 r16 L9000 encode -2.3 %, decode -8.3 %:
-// the chunk passes then revisit one block's rows); everything else keeps 64 / RT.
+// budget.  Defaults measured in-process (profiles/r01_ab_group.log, three boxes):
+// - encode tiles of 4 repairs: groups of 4 blocks (k16 r4 -2.6..-3.1 % against 16);
+// - decode tiles of 4: groups of 8 (k16 e4 -0.8..-1 %);
+// - symbols wider than one column chunk (L > 2 KiB): one block per group (k64 r16 L9000 encode
+//   -2.3 %, decode -8.3 %: the chunk passes then revisit one block's rows);
+// - everything else: 64 / RT.
 // FECGPU_GROUP=N replaces the defaults with a plain cap (A/B experiments).
 static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, bool enc, int nchunks) {
   int g = 64 / RT;
@@ -1158,8 +1160,8 @@ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, 
     while (g > 1 && g > cap) g >>= 1;
   } else if (nchunks > 1) {
     g = 1;
-  } else if (enc && RT == 4) {
-    g = 4;
+  } else if (RT == 4) {
+    g = enc ? 4 : 8;
   }
   while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
   return g;
