@@ -1624,56 +1624,57 @@ __global__ void k_write_repair_frames(const uint32_t *__restrict__ rep, uint64_t
   }
 }
 
-// Fast path (16-B aligned rows and slots): one wave per frame, a lane per 16-B output chunk;
-// chunk c holds payload bytes 16c-14 .. 16c+1 = source dwords 4c-4 .. 4c shifted by 2 bytes.
+// Fast path (16-B aligned rows and slots): a thread per 16-B output chunk over all frames, so the
+// frame slots are written as one contiguous run (a wave per frame left 52 of its 128 lane slots
+// idle on 1216-B slots).  Chunk c of a frame holds payload bytes 16c-14 .. 16c+1 = source dwords
+// 4c-4 .. 4c shifted by 2 bytes; chunk 0 is the header.  I: 32-bit chunk indices when they fit.
+template <typename I>
 __global__ __launch_bounds__(256) void k_write_repair_frames16(const uint32_t *__restrict__ rep, uint64_t nframes,
                                                                uint32_t r, uint32_t Lw, uint32_t len,
                                                                uint32_t fbn_base, const uint32_t *fbn, uint32_t nss,
                                                                uint32_t nrs, uint32_t *__restrict__ frames,
                                                                uint32_t fw) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  const uint32_t nchunks = fw / 4;
-  for (uint64_t f = wave; f < nframes; f += nw) {
-    const uint32_t *row = rep + f * (uint64_t)Lw;
-    u32x4 *out = reinterpret_cast<u32x4 *>(frames + f * fw);
-    for (uint32_t c = lane; c < nchunks; c += 64) {
-      u32x4 o;
-      if (c == 0) {
-        const uint64_t b = f / r;
-        const uint32_t i = (uint32_t)(f - b * r);
-        const uint32_t fb = fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
-        const uint64_t raw = ((uint64_t)fb << 8) | i;
-        uint32_t wv[4];
-        for (int w = 0; w < 4; w++) {
-          uint32_t v = 0;
-          for (int q = 0; q < 4; q++) {
-            const int ob = 4 * w + q;
-            const uint32_t byte = ob < 14 ? frame_header_byte(ob, len, raw, nss, nrs) : (row[0] >> (8 * (ob - 14))) & 0xff;
-            v |= byte << (8 * q);
-          }
-          wv[w] = v;
+  const I nchunks = (I)(fw / 4), total = (I)(nframes * (fw / 4));
+  u32x4 *out = reinterpret_cast<u32x4 *>(frames);
+  for (I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x; t < total; t += (I)gridDim.x * (I)blockDim.x) {
+    const I f = t / nchunks;
+    const uint32_t c = (uint32_t)(t - f * nchunks);
+    const uint32_t *row = rep + (uint64_t)f * Lw;
+    u32x4 o;
+    if (c == 0) {
+      const uint64_t b = (uint64_t)f / r;
+      const uint32_t i = (uint32_t)((uint64_t)f - b * r);
+      const uint32_t fb = fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
+      const uint64_t raw = ((uint64_t)fb << 8) | i;
+      uint32_t wv[4];
+      for (int w = 0; w < 4; w++) {
+        uint32_t v = 0;
+        for (int q = 0; q < 4; q++) {
+          const int ob = 4 * w + q;
+          const uint32_t byte = ob < 14 ? frame_header_byte(ob, len, raw, nss, nrs) : (row[0] >> (8 * (ob - 14))) & 0xff;
+          v |= byte << (8 * q);
         }
-        o = u32x4{wv[0], wv[1], wv[2], wv[3]};
-      } else {
-        const uint32_t d0 = 4 * (c - 1);
-        const u32x4 a = d0 + 3 < Lw ? *reinterpret_cast<const u32x4 *>(row + d0) : u32x4{0, 0, 0, 0};
-        const uint32_t e = d0 + 4 < Lw ? row[d0 + 4] : 0u;
-        o = u32x4{__builtin_amdgcn_alignbyte(a.y, a.x, 2), __builtin_amdgcn_alignbyte(a.z, a.y, 2),
-                  __builtin_amdgcn_alignbyte(a.w, a.z, 2), __builtin_amdgcn_alignbyte(e, a.w, 2)};
+        wv[w] = v;
       }
-      const int valid = (int)(14 + len) - 16 * (int)c;  // zero the slot past the frame's end
-      if (valid < 16) {
-        uint32_t m[4];
-        for (int w = 0; w < 4; w++) {
-          const int vb = valid - 4 * w;
-          m[w] = vb <= 0 ? 0u : vb >= 4 ? 0xffffffffu : (1u << (8 * vb)) - 1u;
-        }
-        o = u32x4{o.x & m[0], o.y & m[1], o.z & m[2], o.w & m[3]};
-      }
-      __builtin_nontemporal_store(o, out + c);
+      o = u32x4{wv[0], wv[1], wv[2], wv[3]};
+    } else {
+      const uint32_t d0 = 4 * (c - 1);
+      const u32x4 a = d0 + 3 < Lw ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(row + d0))
+                                  : u32x4{0, 0, 0, 0};
+      const uint32_t e = d0 + 4 < Lw ? row[d0 + 4] : 0u;
+      o = u32x4{__builtin_amdgcn_alignbyte(a.y, a.x, 2), __builtin_amdgcn_alignbyte(a.z, a.y, 2),
+                __builtin_amdgcn_alignbyte(a.w, a.z, 2), __builtin_amdgcn_alignbyte(e, a.w, 2)};
     }
+    const int valid = (int)(14 + len) - 16 * (int)c;  // zero the slot past the frame's end
+    if (valid < 16) {
+      uint32_t m[4];
+      for (int w = 0; w < 4; w++) {
+        const int vb = valid - 4 * w;
+        m[w] = vb <= 0 ? 0u : vb >= 4 ? 0xffffffffu : (1u << (8 * vb)) - 1u;
+      }
+      o = u32x4{o.x & m[0], o.y & m[1], o.z & m[2], o.w & m[3]};
+    }
+    __builtin_nontemporal_store(o, out + t);
   }
 }
 
@@ -2095,11 +2096,16 @@ int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, ui
   if (!nblocks || !r) return FECGPU_OK;
   const uint64_t nf = nblocks * r, total = nf * (frame_stride / 4);
   if (symbol_size % 16 == 0 && frame_stride % 16 == 0 && ((uintptr_t)rep | (uintptr_t)frames) % 16 == 0) {
-    const uint64_t wg = (nf + 3) / 4;  // 4 waves (frames) per workgroup
+    const uint64_t chunks = nf * (frame_stride / 16), wg = (chunks + 255) / 256;
     const uint32_t grid = (uint32_t)(wg < (1u << 20) ? wg : (1u << 20));
-    hipLaunchKernelGGL(k_write_repair_frames16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint32_t *)rep,
-                       nf, r, symbol_size / 4, (uint32_t)data_length, fbn_base, fbn, (uint32_t)nss, (uint32_t)nrs,
-                       (uint32_t *)frames, frame_stride / 4);
+    if (chunks < (1ull << 32) - (uint64_t)grid * 256)
+      hipLaunchKernelGGL(k_write_repair_frames16<uint32_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                         (const uint32_t *)rep, nf, r, symbol_size / 4, (uint32_t)data_length, fbn_base, fbn,
+                         (uint32_t)nss, (uint32_t)nrs, (uint32_t *)frames, frame_stride / 4);
+    else
+      hipLaunchKernelGGL(k_write_repair_frames16<uint64_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                         (const uint32_t *)rep, nf, r, symbol_size / 4, (uint32_t)data_length, fbn_base, fbn,
+                         (uint32_t)nss, (uint32_t)nrs, (uint32_t *)frames, frame_stride / 4);
   } else {
     const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
     hipLaunchKernelGGL(k_write_repair_frames, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint32_t *)rep,
