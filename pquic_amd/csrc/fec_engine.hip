@@ -437,6 +437,20 @@ __host__ __device__ static inline uint32_t lane_arena_bytes(uint32_t k, uint32_t
 // 64 workspace records are contiguous in HBM.
 __host__ __device__ static inline uint32_t plan_out_row(uint32_t stride) { return stride + 4; }
 
+// Records staged in LDS (rows of odw dwords, padded against bank conflicts) leave as coalesced
+// dwords of rows of rdw.  Lane positions advance by 64 dwords per step without a division.
+__device__ __forceinline__ void copy_records(uint32_t *dst, const uint32_t *src, uint32_t nrows, uint32_t rdw,
+                                             uint32_t odw, int lane) {
+  const uint32_t drow = 64u / rdw, dcol = 64u - drow * rdw;  // dcol < rdw
+  uint32_t row = (uint32_t)lane / rdw, col = (uint32_t)lane - row * rdw;
+  for (uint32_t x = lane; x < nrows * rdw; x += 64) {
+    dst[x] = src[row * odw + col];
+    row += drow;
+    col += dcol;
+    if (col >= rdw) { col -= rdw; row++; }
+  }
+}
+
 __host__ __device__ static inline size_t plan_lane_lds(uint32_t k, uint32_t r) {
   return 768 + 64 * (size_t)lane_arena_bytes(k, r) + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
 }
@@ -562,13 +576,8 @@ __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, i
       } while (0);
     __syncthreads();
     const uint32_t nrows = nblocks - base < 64 ? (uint32_t)(nblocks - base) : 64u;
-    const uint32_t rdw = L.stride / 4, odw = orow / 4;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
-    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(obase);
-    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
-      const uint32_t row = x / rdw;
-      dst[x] = srcw[row * odw + (x - row * rdw)];
-    }
+    copy_records(reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride),
+                 reinterpret_cast<const uint32_t *>(obase), nrows, L.stride / 4, orow / 4, lane);
     __syncthreads();
   }
 #undef AR
@@ -727,9 +736,15 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
       for (int i = 0; i < EM; i++) {
         if (i < n) {
           uint8_t *D = h + L.off_D + i * k;
+          if ((k & 3) == 0) {  // D + 4d is 4-byte aligned: the packed V row as dwords
 #pragma unroll
-          for (int j = 0; j < 4 * KD; j++)
-            if (j < k) D[j] = (uint8_t)(V[i][j >> 2] >> (8 * (j & 3)));
+            for (int d = 0; d < KD; d++)
+              if (4 * d < k) reinterpret_cast<uint32_t *>(D)[d] = V[i][d];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4 * KD; j++)
+              if (j < k) D[j] = (uint8_t)(V[i][j >> 2] >> (8 * (j & 3)));
+          }
           for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && col8(A[i], u) != 0;
           h[L.off_nz + i] = 0;
           h[L.off_unk + i] = (uint8_t)col8(U, i);
@@ -746,13 +761,8 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
     } while (0);
     __syncthreads();
     const uint32_t nrows = nblocks - base < 64 ? (uint32_t)(nblocks - base) : 64u;
-    const uint32_t rdw = L.stride / 4, odw = orow / 4;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
-    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(lds + 768);
-    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
-      const uint32_t row = x / rdw;
-      dst[x] = srcw[row * odw + (x - row * rdw)];
-    }
+    copy_records(reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride),
+                 reinterpret_cast<const uint32_t *>(lds + 768), nrows, L.stride / 4, orow / 4, lane);
     __syncthreads();
   }
 }
@@ -955,13 +965,8 @@ __global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, i
     }
     __syncthreads();
     const uint32_t nrows = nblocks - base < BPW ? (uint32_t)(nblocks - base) : (uint32_t)BPW;
-    const uint32_t rdw = L.stride / 4, odw = orow / 4;
-    uint32_t *dst = reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride);
-    const uint32_t *srcw = reinterpret_cast<const uint32_t *>(OUTR);
-    for (uint32_t x = lane; x < nrows * rdw; x += 64) {
-      const uint32_t row = x / rdw;
-      dst[x] = srcw[row * odw + (x - row * rdw)];
-    }
+    copy_records(reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride),
+                 reinterpret_cast<const uint32_t *>(OUTR), nrows, L.stride / 4, orow / 4, lane);
     __syncthreads();
   }
 }
