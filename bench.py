@@ -26,10 +26,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HB
 # measured on MI355X (profiles/r01_copy_style_probe.log, tools/microbench/copy_style_probe.hip): the best
 # plain-streaming rates -- one-shot float4 copy (1:1) and a one-shot 4:1 read:write mix (nt loads and
 # stores); and the FEC data path's own access pattern with trivial compute
-# (profiles/r01_block_pattern_probe.log: k16 r4 rows, one wave per interleaved group of 16 blocks)
+# (profiles/r01_block_pattern_probe.log: k16 r4 rows, one wave per interleaved group of 4 blocks --
+# the encode's default group -- at 3 waves/SIMD; groups of 16 measured 5438-5476 on that box)
 MEASURED_COPY_GBS = 6282.0
 MEASURED_MIX41_GBS = 6440.0
-PATTERN_CEILING_GBS = 5479.0
+PATTERN_CEILING_GBS = 5564.0
 METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 
 
