@@ -472,8 +472,8 @@ def data_base(mode: str) -> int:
 
 def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     """Register prefetch depth P (source rows in flight per wave).  Prefer 3 waves/SIMD
-    (<= 168 VGPRs) when that still leaves P >= PMIN3; otherwise take everything up to 256
-    VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63.
+    (<= 168 VGPRs) when that still leaves P >= PMIN3 (4 for encode, 2 for decode); otherwise
+    take everything up to 256 VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63.
     The decode wrapper keeps ~14 more VGPRs live across the asm than the asm's own window
     (measured with -Rpass-analysis=kernel-resource-usage), so its budgets carry a margin --
     without it the recover kernels tip over a VGPR granule and lose a wave per SIMD."""
@@ -488,7 +488,10 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     if forced:  # A/B: VGPR limit for this tile size
         return max([P for P in range(2, 33) if fits(P, int(forced) - margin)] or [2])
     p3 = max([P for P in range(2, 33) if fits(P, budget3)] or [0])
-    if p3 >= int(os.environ.get("FEC_GEN_PMIN3", "4")):
+    # decode takes 3 waves/SIMD even at P = 2: RT=8 at 3 waves and P=2 ran 14.7 % faster than at 2
+    # waves and P=12 (profiles/r01_ab_prefetch.log); encode keeps P >= 4 (its RT=8 tile fits P=4)
+    pmin3 = int(os.environ.get("FEC_GEN_PMIN3", "2" if mode == "dec" else "4"))
+    if p3 >= pmin3:
         return min(p3, int(os.environ.get("FEC_GEN_PMAX", "8")))
     return max([P for P in range(2, 33) if fits(P, budget2)] or [2])
 
