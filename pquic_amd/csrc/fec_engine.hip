@@ -1816,18 +1816,11 @@ void fecgpu_get_stats(fecgpu_stats_t *out) {
 // FECGPU_ENC_TILE="RT,W" overrides (A/B experiments).
 struct EncTile { int rt, waves; };
 static EncTile pick_enc_tile(uint32_t r) {
-  static int ort = -1, ow = -1;
-  if (ort < 0) {
-    ort = 0;
-    if (const char *e = getenv("FECGPU_ENC_TILE")) {
-      int a = 0, b = 0;
-      if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4) {
-        ort = a;
-        ow = b;
-      }
-    }
+  if (const char *e = getenv("FECGPU_ENC_TILE")) {  // read per call (in-process A/B)
+    int a = 0, b = 0;
+    if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4)
+      return {a, b};
   }
-  if (ort > 0) return {ort, ow};
   // measured (profiles/r01_tile_ab.log): splitting repairs over waves repeats the transpose and
   // table work per wave and loses more VALU than the occupancy gains (k32r8 4x2: +34 %,
   // k64r16 8x2: +10 %), so one wave carries up to 16 repairs

@@ -20,7 +20,15 @@ reps = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--reps=")), 
 variants = []
 for spec in args or ["base"]:
     name, _, env = spec.partition(":")
-    variants.append((name, dict(kv.split("=", 1) for kv in env.split(",") if kv)))
+    kvs = {}
+    last = None
+    for piece in env.split(","):  # a piece without "=" continues the previous value ("A=8,2")
+        if "=" in piece:
+            last, v = piece.split("=", 1)
+            kvs[last] = v
+        elif piece and last:
+            kvs[last] += "," + piece
+    variants.append((name, kvs))
 knobs = sorted({k for _, e in variants for k in e if k != "LIB"})
 
 eng0 = Engine(0)
