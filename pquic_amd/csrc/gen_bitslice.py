@@ -300,10 +300,10 @@ def body(mode: str, RT: int, VEC: int, P: int):
                     f"v_readfirstlane_b32 s{S_CUR + 1}, v{NADDR + 1}",
                     f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}",
                     f"v_add_u32 v{INPTR}, 8, v{INPTR}"]
+        # no exec switching: a lane's piece past the chunk end has offset 0 (BsLanes), so its load
+        # stays inside the row, and its bytes never reach memory (the stores are masked)
         for q in range(NP):
-            out += [f"s_mov_b64 exec, %[vm{q}]",
-                    f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
-        out.append(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+            out.append(f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@")
         if mode == "enc":
             # next row of this block, or -- after its k-th row -- the first row of the group's next
             # block, which starts bstep blocks further on (interleaved groups: %[sdlo/hi] = delta)
