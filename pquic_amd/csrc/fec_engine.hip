@@ -1101,14 +1101,14 @@ struct BsLanes {
 #define BS_CALL_ENC(RT)                                                                             \
   do {                                                                                              \
     if constexpr (VEC == 16)                                                                        \
-      bs_enc_r##RT##_v16(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.vm[0], \
+      bs_enc_r##RT##_v16(sp, rpp, L, rslo, rshi, sdl, ll, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.vm[0], \
                          ln.vm[1]);                                                                \
     else if constexpr (VEC == 8)                                                                    \
-      bs_enc_r##RT##_v8(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
+      bs_enc_r##RT##_v8(sp, rpp, L, rslo, rshi, sdl, ll, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
                         ln.off[3],                                                                  \
                         ln.vm[0], ln.vm[1], ln.vm[2], ln.vm[3]);                                    \
     else                                                                                            \
-      bs_enc_r##RT##_v4(sp, rpp, L, rslo, rshi, sdlo, sdhi, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
+      bs_enc_r##RT##_v4(sp, rpp, L, rslo, rshi, sdl, ll, nsrc, k, rt, ca, ln.off[0], ln.off[1], ln.off[2], \
                         ln.off[3],                                                                  \
                         ln.off[4], ln.off[5], ln.off[6], ln.off[7], ln.vm[0], ln.vm[1], ln.vm[2],   \
                         ln.vm[3], ln.vm[4], ln.vm[5], ln.vm[6], ln.vm[7]);                          \
@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void bs_enc_call(uint64_t sp, uint64_t rpp, uint32_t 
                                             uint32_t nsrc, uint32_t k, uint32_t rt, uint32_t ca,
                                             const BsLanes<VEC> &ln) {
   const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
-  const uint32_t sdlo = (uint32_t)sdelta, sdhi = (uint32_t)(sdelta >> 32);
+  const uint64_t sdl = sdelta + L, ll = L;  // source pointer steps: after a block's k-th row / otherwise
   if constexpr (RT == 1) BS_CALL_ENC(1);
   else if constexpr (RT == 2) BS_CALL_ENC(2);
   else if constexpr (RT == 4) BS_CALL_ENC(4);

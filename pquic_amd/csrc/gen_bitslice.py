@@ -306,15 +306,14 @@ def body(mode: str, RT: int, VEC: int, P: int):
             out.append(f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@")
         if mode == "enc":
             # next row of this block, or -- after its k-th row -- the first row of the group's next
-            # block, which starts bstep blocks further on (interleaved groups: %[sdlo/hi] = delta)
-            out += [f"s_add_u32 s{S_CUR}, s{S_CUR}, %[L]", f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, 0",
-                    f"s_add_u32 s{S_JL}, s{S_JL}, 1",
+            # block, which starts bstep blocks further on: one 64-bit select between the two steps
+            # (%[ll] = L, %[sdl] = L + delta), through the chain queue (idle while loads issue)
+            out += [f"s_add_u32 s{S_JL}, s{S_JL}, 1",
                     f"s_cmp_eq_u32 s{S_JL}, %[k]",
-                    f"s_cselect_b32 s{S_DJ}, %[sdlo], 0",
-                    f"s_cselect_b32 s{S_DJ + 1}, %[sdhi], 0",
+                    f"s_cselect_b64 s[{S_CQ}:{S_CQ + 1}], %[sdl], %[ll]",
                     f"s_cselect_b32 s{S_JL}, 0, s{S_JL}",
-                    f"s_add_u32 s{S_CUR}, s{S_CUR}, s{S_DJ}",
-                    f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_DJ + 1}"]
+                    f"s_add_u32 s{S_CUR}, s{S_CUR}, s{S_CQ}",
+                    f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_CQ + 1}"]
         return out
 
     for q in range(P - 1):  # prologue: sources 0 .. P-2
@@ -445,9 +444,9 @@ def emit_function(mode, RT, VEC, P):
     vms = ", ".join(f"uint64_t vm{q}" for q in range(NP))
     if mode == "enc":
         sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rslo, "
-               f"uint32_t rshi, uint32_t sdlo, uint32_t sdhi, "
+               f"uint32_t rshi, uint64_t sdl, uint64_t ll, "
                f"uint32_t nsrc, uint32_t k, uint32_t rt, uint32_t coef, {offs}, {vms})")
-        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rslo] "s"(rslo)', '[rshi] "s"(rshi)', '[sdlo] "s"(sdlo)', '[sdhi] "s"(sdhi)', '[rt] "s"(rt)']
+        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rslo] "s"(rslo)', '[rshi] "s"(rshi)', '[sdl] "s"(sdl)', '[ll] "s"(ll)', '[rt] "s"(rt)']
     else:
         sig = (f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, uint32_t nsrc, "
                f"uint32_t k, uint32_t coef, {offs}, {vms})")
