@@ -285,8 +285,13 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}")  # source 0's address
         a(f"v_add_u32 v{INPTR}, 8, v{INPTR}")
         a(f"v_mov_b32 v{OUTPTR}, %[outtab]")
-    a(f"s_mov_b32 s{S_S}, 0")
-    a(f"s_mov_b32 s{S_J}, 0")
+    # count-down loop counters, tested by the borrow of s_sub_u32 (no compares in the loop):
+    # S_S = sources left after this one, S_J = sources left in this block after this one,
+    # S_T2 = prefetches left (max(0, nsrc - (P - 1)))
+    a(f"s_sub_u32 s{S_S}, %[nsrc], 1")
+    a(f"s_sub_u32 s{S_J}, %[k], 1")
+    a(f"s_sub_u32 s{S_T2}, %[nsrc], {P - 1}")
+    a(f"s_cselect_b32 s{S_T2}, 0, s{S_T2}")
     if mode == "enc":
         a(f"s_mov_b32 s{S_JL}, 0")
 
@@ -332,13 +337,12 @@ def body(mode: str, RT: int, VEC: int, P: int):
     for b in range(P):
         nb = (b + P - 1) % P
         a(f".Lbody{b}_%=:")
-        a(f"s_add_u32 s{S_T2}, s{S_S}, {P - 1}")
-        a(f"s_cmp_lt_u32 s{S_T2}, %[nsrc]")
-        a(f"s_cbranch_scc0 .Lnopf{b}_%=")
+        a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
+        a(f"s_cbranch_scc1 .Lnopf{b}_%=")
         L.extend(load_source(nb))
         a(f"s_waitcnt vmcnt({NP * (P - 1)})")
         a(f".Lpf{b}_%=:")
-        ool += [f".Lnopf{b}_%=:", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
+        ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
         L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
         # the coefficient fields land in the (now free) transpose temporaries under the combos
         a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
@@ -363,15 +367,13 @@ def body(mode: str, RT: int, VEC: int, P: int):
                 a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
             a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
         a("s_set_gpr_idx_off")
-        a(f"s_add_u32 s{S_S}, s{S_S}, 1")
-        a(f"s_add_u32 s{S_J}, s{S_J}, 1")
-        a(f"s_cmp_eq_u32 s{S_J}, %[k]")
+        a(f"s_sub_u32 s{S_J}, s{S_J}, 1")
         a(f"s_cbranch_scc1 .Lepicall{b}_%=")
         a(f".Lnoepi{b}_%=:")
-        a(f"s_cmp_lt_u32 s{S_S}, %[nsrc]")
-        a(f"s_cbranch_scc0 .Lexit_%=")
+        a(f"s_sub_u32 s{S_S}, s{S_S}, 1")
+        a(f"s_cbranch_scc1 .Lexit_%=")
         ool += [f".Lepicall{b}_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
-                f"s_mov_b32 s{S_J}, 0", f"s_branch .Lnoepi{b}_%="]
+                f"s_sub_u32 s{S_J}, %[k], 1", f"s_branch .Lnoepi{b}_%="]
     a(f"s_branch .Lbody0_%=")
     L.extend(ool)
 
