@@ -84,6 +84,18 @@ def make_erasures(torch, nb, k, e, seed, dev):
     return sp.to(dev), miss
 
 
+def check_recovered(torch, dst, src, ok, miss, nb, k, L, what):
+    """Decode gate: in every recovered block, the rows written for the erased symbols equal the
+    originals (recovered rows go to their own buffer, src's layout; only erased rows are written)."""
+    e = miss.shape[1]
+    miss = miss.to(src.device)
+    for c0 in range(0, nb, 1 << 16):  # chunked: no full-size temporaries
+        c1 = min(nb, c0 + (1 << 16))
+        b = torch.arange(c0, c1, device=src.device)
+        rows = (b.unsqueeze(1) * k + miss[c0:c1]).reshape(-1)[ok[c0:c1].repeat_interleave(e)]
+        assert bool((dst.view(nb * k, L)[rows] == src.view(nb * k, L)[rows]).all()), what
+
+
 def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     """One BASELINE config as a side leg: RLC encode, then decode with e random erasures,
     device-resident, per-kernel event timing; decode correctness gated on the output."""
@@ -99,27 +111,25 @@ def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
     rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
     ws = eng.alloc_workspace(nb, k, r)
+    rec_rows = torch.empty_like(src)  # recovered symbols (new buffers, as fec_recover allocates them)
     stream = torch.cuda.current_stream(dev)
     eng.rlc_encode(src, rep, k, r, L)
-    eng.rlc_decode(work, rep, sp, rp, st, rec, k, r, L, workspace=ws)
+    eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, dst=rec_rows)
     torch.cuda.synchronize()
     ok = st == 0
-    for c0 in range(0, nb, 1 << 14):
-        c1 = min(nb, c0 + (1 << 14))
-        okc = ok[c0:c1]
-        assert bool((work[c0:c1][okc] == src[c0:c1][okc]).all()), f"k{k} r{r} decode did not restore the sources"
+    check_recovered(torch, rec_rows, src, ok, miss, nb, k, L, f"k{k} r{r} decode did not restore the sources")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     t = [0.0, 0.0, 0.0]
     for _ in range(reps):
         ev[0].record(stream)
         eng.rlc_encode(src, rep, k, r, L)
-        eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, events=ev[1:])
+        eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, events=ev[1:], dst=rec_rows)
         torch.cuda.synchronize()
         for i in range(3):
             t[i] += ev[i].elapsed_time(ev[i + 1]) / reps
     n_rec = int(ok.sum())
     enc_b, app_b = (k + r) * L * nb, (k + e) * L * n_rec
-    del src, rep, work, ws
+    del src, rep, work, ws, rec_rows
     torch.cuda.empty_cache()
     pay = nb * k * L / 2**30
     return {"blocks": nb, "k": k, "r": r, "L": L, "erasures": e, "encode_ms": round(t[0], 3),
@@ -321,11 +331,15 @@ def main():
     status = torch.empty(nb, dtype=torch.uint8, device=dev)
     recovered = torch.empty((nb, 2), dtype=torch.int64, device=dev)
     ws = eng.alloc_workspace(nb, k, r)
-    # decode input: the received block (erased slots hold stale bytes); copied once, and the
-    # recovered symbols are rewritten in place by every decode pass
+    # decode input: the received block (erased slots hold stale bytes), copied once.  The recovered
+    # symbols go to their own buffer -- the reference's fec_recover allocates new source symbols
+    # rather than writing into the received block (rlc_fec_scheme_gf256.c:218-236) -- which also
+    # keeps the writes out of the rows being read (in place measured 5 % slower,
+    # profiles/r01_ab_apply_to.log)
     work.copy_(src)
     idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
     work.view(nb * k, L)[idx] = 0xA5
+    rec_rows = torch.empty_like(src)
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
@@ -333,17 +347,14 @@ def main():
             ev[0].record(stream)
         eng.rlc_encode(src, rep, k, r, L, fbn_base=fbn_base)
         eng.rlc_decode_stages(work, rep, sp, rp, status, recovered, k, r, L, nb, ws, fbn_base=fbn_base,
-                              events=ev[1:] if ev else None)
+                              events=ev[1:] if ev else None, dst=rec_rows)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness gate on the benchmarked data: every recovered block equals the original
+    # correctness gate on the benchmarked data: every recovered block's erased rows equal the originals
     ok = status == 0
-    for c0 in range(0, nb, 1 << 16):  # chunked: no full-size temporaries
-        c1 = min(nb, c0 + (1 << 16))
-        okc = ok[c0:c1]
-        assert bool((work[c0:c1][okc] == src[c0:c1][okc]).all()), "decode did not restore the sources"
+    check_recovered(torch, rec_rows, src, ok, miss, nb, k, L, "decode did not restore the sources")
     n_rec = int(ok.sum())
     n_ub = int((status == 2).sum())
 
@@ -385,7 +396,7 @@ def main():
                               "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
                               "ref_ub_blocks": n_ub, "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)},
     }
-    del work, ws
+    del work, ws, rec_rows
     if not args.no_legs and not args.no_pcie and world == 1:
         legs.update(pcie_legs(torch, args, dev))
         legs.update(batching_legs(dev.index or 0, args))
@@ -459,6 +470,7 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "RLC-GF(256) encode k=16 r=4 + decode 4 erasures, 1200B symbols",
                           "k": k, "r": r, "erasures": e, "symbol_bytes": L, "blocks_per_gpu": nb,
+                          "decode_output": "recovered symbols into their own buffer (as fec_recover allocates them)",
                           "parallelism": f"independent FEC blocks, {world} GPU(s), no collective"},
                "roofline": roof, "cpu_baseline": cpu, "legs": legs}
         print(json.dumps(out))

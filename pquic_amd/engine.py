@@ -158,9 +158,10 @@ class Engine:
         return status, recovered
 
     def rlc_decode_stages(self, src, rep, src_present, rep_present, status, recovered, k, r, L, nblocks,
-                          workspace, fbn_base=0, stream=None, events=None):
+                          workspace, fbn_base=0, stream=None, events=None, dst=None):
         """fecgpu_rlc_decode as its two stages (plan, apply); events[i] (if given) recorded before
-        stage i and events[2] after the last, on the launch stream."""
+        stage i and events[2] after the last, on the launch stream.  dst: write the recovered rows
+        there (src's layout, fecgpu_rlc_decode_apply_to) instead of into src."""
         st = self._stream(stream)
         torch_stream = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         rec = (lambda i: events[i].record(torch_stream)) if events else (lambda i: None)
@@ -169,9 +170,14 @@ class Engine:
                                                     _addr(rep_present), _addr(workspace), workspace.numel(), st),
                     "fecgpu_rlc_decode_plan")
         rec(1)
-        self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
-                                                     _addr(recovered), _addr(workspace), workspace.numel(), st),
-                    "fecgpu_rlc_decode_apply")
+        if dst is None:
+            self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
+                                                         _addr(recovered), _addr(workspace), workspace.numel(), st),
+                        "fecgpu_rlc_decode_apply")
+        else:
+            self._check(self.lib.fecgpu_rlc_decode_apply_to(_addr(src), _addr(rep), _addr(dst), nblocks, k, r, L,
+                                                            _addr(status), _addr(recovered), _addr(workspace),
+                                                            workspace.numel(), st), "fecgpu_rlc_decode_apply_to")
         rec(2)
         return status, recovered
 

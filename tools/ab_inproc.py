@@ -55,12 +55,15 @@ def setup(k, r, nb, e, L):
 
 
 cases = []
+DST = torch.empty(((1 << 20), 16, 1200), dtype=torch.uint8, device=dev) if "--apply-to" in sys.argv else None
 FRAMES = torch.empty(((1 << 20) * 4 * 1216,), dtype=torch.uint8, device=dev) if "--frames" in sys.argv else None
 CASES = [(16, 4, 1 << 20, "enc", 1200), (16, 4, 1 << 20, "dec", 1200), (32, 8, 1 << 20, "enc", 1200)]
 if "--wide" in sys.argv:  # also the r >= 8 decode and configs[4] (jumbo symbols)
     CASES += [(32, 8, 1 << 19, "dec", 1200), (64, 16, 1 << 15, "enc", 9000), (64, 16, 1 << 15, "dec", 9000)]
 if "--xor" in sys.argv:  # the XOR scheme (configs[0]'s) at GPU scale
     CASES += [(4, 1, 1 << 22, "xenc", 1200), (4, 1, 1 << 22, "xdec", 1200)]
+if "--apply-to" in sys.argv:  # decode with the recovered rows written to a separate buffer
+    CASES += [(16, 4, 1 << 20, "decto", 1200)]
 if "--frames" in sys.argv:  # repair symbols -> FEC frames in 1216-B slots (the bench's frames leg)
     CASES += [(16, 4, 1 << 20, "frames", 1200)]
 for (k, r, nb, mode, L) in CASES:
@@ -76,6 +79,9 @@ def run(case, eng):
         eng.xor_encode(src, rep, k, L)
     elif mode == "xdec":
         eng.xor_decode(src, rep, sp, rp, st, rec, k, L)
+    elif mode == "decto":
+        eng.rlc_decode_plan(sp, rp, k, r, nb, ws)
+        eng.rlc_decode_apply_to(src, rep, DST, st, rec, k, r, L, nb, ws)
     elif mode == "frames":
         eng.write_repair_frames(rep, FRAMES, nb, r, L, L, 1216, k, r)
     else:
