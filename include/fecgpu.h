@@ -112,6 +112,23 @@ int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint
                                uint64_t *recovered, void *workspace, size_t workspace_bytes,
                                void *stream);
 
+/* RLC decode with the coefficients of every received repair seeded by its own FPID, as the
+ * reference does (get_coefs(..., rs->repair_fec_payload_id.source_fpid.raw, ...),
+ * rlc_fec_scheme_gf256.c:200): rep_seed[b * r + i] is the low 32 bits of the FPID of the repair
+ * in slot i of block b (entries of absent repairs are ignored).  This is the general form: the
+ * block framework's repairs carry (fbn << 8) | i, which is what fecgpu_rlc_decode assumes, but
+ * the sliding-window framework's blocks are numbered by their window start while their repairs
+ * carry block number 0 (window_framework_receiver.h:60-86, window_framework_sender.h:239-243).
+ * Recovered FPIDs are the caller's business (the host adapters stamp (fec_block_number << 8) + j,
+ * :222). */
+int fecgpu_rlc_decode_plan_seeded(uint64_t nblocks, uint32_t k, uint32_t r, const uint32_t *rep_seed,
+                                  const uint64_t *src_present, const uint64_t *rep_present, void *workspace,
+                                  size_t workspace_bytes, void *stream);
+int fecgpu_rlc_decode_seeded(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                             uint32_t symbol_size, const uint32_t *rep_seed, const uint64_t *src_present,
+                             const uint64_t *rep_present, uint8_t *status, uint64_t *recovered, void *workspace,
+                             size_t workspace_bytes, void *stream);
+
 /* XOR decode (r == 1), same conventions. */
 int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
                       uint32_t symbol_size, const uint64_t *src_present,
@@ -137,6 +154,11 @@ int fecgpu_rlc_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
                            uint32_t k, uint32_t r, uint32_t symbol_size, uint32_t fbn_base,
                            const uint32_t *fbn, const uint64_t *src_present,
                            const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
+/* host-resident fecgpu_rlc_decode_seeded: rep_seed is a host array [nblocks][r] */
+int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,
+                                  uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed,
+                                  const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                                  uint64_t *recovered);
 int fecgpu_xor_encode_host(fecgpu_host_ctx_t *ctx, const void *src, void *rep, uint64_t nblocks,
                            uint32_t k, uint32_t symbol_size);
 int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,
@@ -162,6 +184,15 @@ void fecgpu_host_free(void *p);
 /* Synthetic payload generator (bench/tests): byte o of dst = byte (o mod 8) of
  * splitmix64(seed + (o/8 + 1) * 0x9e3779b97f4a7c15), o counted from `offset`. */
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream);
+
+/* Experiment knobs (A/B runs, cross-checks of alternative kernels in the tests).  Every knob has
+ * a measured default; the environment variable named in DESIGN.md §6.1 seeds it ONCE per process
+ * (first engine call), after which only these calls change it.  Names: "datapath_perm" (0/1),
+ * "plan" (0 auto, 1 wave, 2 lane, 3 reg, 4 tile), "interleave" (0/1), "group" (0 = defaults, else
+ * a cap on blocks per group), "enc_tile_rt" / "enc_tile_waves" (0 = default tiling), "xor_generic",
+ * "xor_idx64", "zc_read" (0/1).  Returns FECGPU_OK or FECGPU_ERR_INVALID for an unknown name. */
+int fecgpu_set_knob(const char *name, int value);
+int fecgpu_get_knob(const char *name, int *value);
 
 /* Per-process counters, the analogue of the reference's per-pluglet count/time
  * (picoquic/ubpf.c:302-319 under DEBUG_PLUGIN_EXECUTION_TIME). */

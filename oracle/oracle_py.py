@@ -205,7 +205,7 @@ class Reference:
         L.ref_encode.argtypes = [C.c_int, C.c_uint32, C.c_int, C.c_int, _u8p, _u16p, C.c_int, _u8p,
                                  C.c_int, _u64p, _u16p]
         L.ref_decode.argtypes = [C.c_int, C.c_uint32, C.c_int, C.c_int, _u8p, _u16p, _u8p, C.c_int,
-                                 _u8p, _u16p, _u8p, _u64p, C.c_int, _u8p, _u16p, _u8p, C.c_int]
+                                 _u8p, _u16p, _u8p, _u64p, C.c_int, _u8p, _u16p, _u8p, C.c_int, _u32p]
         L.ref_rlc_encode_batch.argtypes = [_u8p, _u8p, C.c_uint64, C.c_int, C.c_int, C.c_int,
                                            C.c_uint32]
         L.ref_layout.argtypes = [_u64p]
@@ -242,7 +242,9 @@ class Reference:
                                   _ptr(rep), stride, _ptr(fp, _u64p), _ptr(rl, _u16p))
         return ret, [rep[i, : rl[i]].copy() for i in range(r)], [int(x) for x in fp[:r]]
 
-    def decode_block(self, xor: bool, fbn: int, srcs: list, reps: list, rep_fpids: list):
+    def decode_block(self, xor: bool, fbn: int, srcs: list, reps: list, rep_fpids: list,
+                     with_fpids: bool = False):
+        """Returns (ret, {j: bytes}) or, with_fpids, (ret, {j: bytes}, {j: recovered source FPID})."""
         k, r = len(srcs), len(reps)
         stride = max([len(s) for s in srcs + reps if s is not None] + [1])
         sb = np.zeros((k, stride), np.uint8)
@@ -266,10 +268,14 @@ class Reference:
         out = np.zeros((k, stride), np.uint8)
         ol = np.zeros(k, np.uint16)
         rec = np.zeros(k, np.uint8)
+        ofp = np.zeros(k, np.uint32)
         ret = self.lib.ref_decode(int(xor), fbn, k, r, _ptr(sb), _ptr(sl, _u16p), _ptr(spres), stride,
                                   _ptr(rb), _ptr(rl, _u16p), _ptr(rpres), _ptr(fp, _u64p), stride,
-                                  _ptr(out), _ptr(ol, _u16p), _ptr(rec), stride)
-        return ret, {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}
+                                  _ptr(out), _ptr(ol, _u16p), _ptr(rec), stride, _ptr(ofp, _u32p))
+        got = {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}
+        if with_fpids:
+            return ret, got, {j: int(ofp[j]) for j in range(k) if rec[j]}
+        return ret, got
 
     def rlc_encode_batch(self, src: np.ndarray, r: int, fbn_base: int = 0):
         nb, k, L = src.shape

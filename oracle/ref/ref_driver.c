@@ -134,14 +134,15 @@ int ref_encode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
 /* Recover one block in a child process.
  * src / rep: dense [k][stride] / [r][stride]; presence bytes per symbol.
  * rep_fpid: raw repair FPIDs (the seed is its low 32 bits, rlc_fec_scheme_gf256.c:200).
- * out: [k][out_stride]; recovered[j] = 1 when the pluglet inserted source j.
+ * out: [k][out_stride]; recovered[j] = 1 when the pluglet inserted source j, out_fpid[j] (may
+ * be NULL) its source FPID raw value.
  * Returns the pluglet's return code, or -1000 - signal when the child died. */
 int ref_decode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
                const uint16_t *src_len, const uint8_t *src_present, int src_stride,
                const uint8_t *rep, const uint16_t *rep_len, const uint8_t *rep_present,
                const uint64_t *rep_fpid, int rep_stride, uint8_t *out, uint16_t *out_len,
-               uint8_t *recovered, int out_stride) {
-    size_t shm_len = (size_t)k * out_stride + (size_t)k * 3 + 64;
+               uint8_t *recovered, int out_stride, uint32_t *out_fpid) {
+    size_t shm_len = (size_t)k * out_stride + (size_t)k * 7 + 64;
     uint8_t *shm = mmap(NULL, shm_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (shm == MAP_FAILED) return -2000;
     memset(shm, 0, shm_len);
@@ -175,12 +176,14 @@ int ref_decode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
         int32_t *hdr = (int32_t *)shm;
         hdr[0] = ret;
         uint8_t *rec = shm + 64, *lens = rec + k, *data = lens + 2 * (size_t)k;
+        uint8_t *fps = data + (size_t)k * out_stride;
         for (int j = 0; j < k; j++) {
             source_symbol_t *ss = fb->source_symbols[j];
             if (ss && ss != before[j]) {
                 rec[j] = 1;
                 uint16_t L = ss->data_length;
                 memcpy(lens + 2 * j, &L, 2);
+                memcpy(fps + 4 * j, &ss->source_fec_payload_id.raw, 4);
                 memcpy(data + (size_t)j * out_stride, ss->data, L > out_stride ? out_stride : L);
             }
         }
@@ -192,9 +195,11 @@ int ref_decode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
     if (WIFEXITED(status) && WEXITSTATUS(status) == 0) {
         ret = ((int32_t *)shm)[0];
         uint8_t *rec = shm + 64, *lens = rec + k, *data = lens + 2 * (size_t)k;
+        uint8_t *fps = data + (size_t)k * out_stride;
         for (int j = 0; j < k; j++) {
             recovered[j] = rec[j];
             memcpy(&out_len[j], lens + 2 * j, 2);
+            if (out_fpid) memcpy(&out_fpid[j], fps + 4 * j, 4);
             if (rec[j]) memcpy(out + (size_t)j * out_stride, data + (size_t)j * out_stride, out_len[j]);
         }
     } else {
@@ -382,4 +387,145 @@ long ref_payload_to_source_symbol(const uint8_t *payload, uint32_t len, uint64_t
     long ret = (long)ref_packet_payload_to_source_symbol(NULL);
     *state_len = g_state.current_symbol_length;
     return ret;
+}
+
+/* ---- CPU baseline: the reference pluglets themselves on every host core --------------------------
+ * bench.py's cpu_baseline leg ("kind": "reference").  The driver keeps its protoop arguments in
+ * globals (g_in / g_out above), so the workers are fork()ed processes, one per core, each running
+ * a contiguous share of the sample: RLC encode of its blocks (rlc_fec_scheme_generate_gf256.c:24-77,
+ * block numbers fbn_base + b), then RLC decode of the same blocks with the erasures of sp[]
+ * (rlc_fec_scheme_gf256.c:134-251; recovered symbols are allocated by the pluglet and freed here,
+ * as the framework frees them).  Blocks flagged in skip[] are patterns on which the reference
+ * dereferences x[-1] (flagged by the caller's screen): they are encoded but not
+ * decoded.  The workers start together on a shared flag; out[0] = wall seconds from the start to
+ * the last worker's exit, out[1] = the slowest worker's own compute seconds, out[2] = blocks
+ * decoded.  Returns 0, or -1 if a worker failed. */
+#include <time.h>
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static long ref_work_range(const uint8_t *src, uint8_t *rep, uint64_t b0, uint64_t b1, int k, int r, int L,
+                           uint32_t fbn_base, const uint64_t *sp, const uint8_t *skip) {
+    source_symbol_t ss[256];
+    repair_symbol_t rs[256];
+    long decoded = 0;
+    for (uint64_t b = b0; b < b1; b++) {  /* encode */
+        fec_block_t fb;
+        memset(&fb, 0, sizeof fb);
+        fb.fec_block_number = (uint32_t)((fbn_base + b) & 0xffffff);
+        fb.total_source_symbols = (uint8_t)k;
+        fb.total_repair_symbols = (uint8_t)r;
+        fb.current_source_symbols = (uint8_t)k;
+        for (int j = 0; j < k; j++) {
+            memset(&ss[j], 0, sizeof ss[j]);
+            ss[j].data = (uint8_t *)src + (b * k + j) * (size_t)L;
+            ss[j].data_length = (uint16_t)L;
+            fb.source_symbols[j] = &ss[j];
+        }
+        g_in[0] = (protoop_arg_t)&fb;
+        g_in[1] = (protoop_arg_t)scheme();
+        if (rlc_encode(NULL) != 0) return -1;
+        for (int i = 0; i < r; i++) {
+            memcpy(rep + ((b - b0) * r + i) * (size_t)L, fb.repair_symbols[i]->data, L);
+            my_free(NULL, fb.repair_symbols[i]->data);
+            my_free(NULL, fb.repair_symbols[i]);
+        }
+    }
+    for (uint64_t b = b0; b < b1; b++) {  /* decode */
+        if (skip[b]) continue;
+        fec_block_t fb;
+        memset(&fb, 0, sizeof fb);
+        const uint32_t fbn = (uint32_t)((fbn_base + b) & 0xffffff);
+        fb.fec_block_number = fbn;
+        fb.total_source_symbols = (uint8_t)k;
+        fb.total_repair_symbols = (uint8_t)r;
+        for (int j = 0; j < k; j++)
+            if ((sp[2 * b + (j >> 6)] >> (j & 63)) & 1) {
+                memset(&ss[j], 0, sizeof ss[j]);
+                ss[j].data = (uint8_t *)src + (b * k + j) * (size_t)L;
+                ss[j].data_length = (uint16_t)L;
+                fb.source_symbols[j] = &ss[j];
+                fb.current_source_symbols++;
+            }
+        for (int i = 0; i < r; i++) {
+            memset(&rs[i], 0, sizeof rs[i]);
+            rs[i].repair_fec_payload_id.raw = ((uint64_t)fbn << 8) | (uint64_t)i;
+            rs[i].data = rep + ((b - b0) * r + i) * (size_t)L;
+            rs[i].data_length = (uint16_t)L;
+            fb.repair_symbols[i] = &rs[i];
+            fb.current_repair_symbols++;
+        }
+        source_symbol_t *before[MAX_SYMBOLS_PER_FEC_BLOCK];
+        memcpy(before, fb.source_symbols, sizeof before);
+        g_in[0] = (protoop_arg_t)&fb;
+        g_in[1] = (protoop_arg_t)scheme();
+        if (rlc_decode(NULL) != 0) return -1;
+        for (int j = 0; j < k; j++)
+            if (fb.source_symbols[j] && fb.source_symbols[j] != before[j]) {
+                my_free(NULL, fb.source_symbols[j]->data);
+                my_free(NULL, fb.source_symbols[j]);
+            }
+        decoded++;
+    }
+    return decoded;
+}
+
+int ref_cpu_baseline(int nworkers, const uint8_t *src, uint64_t nblocks, int k, int r, int L, uint32_t fbn_base,
+                     const uint64_t *sp, const uint8_t *skip, int passes, double *out) {
+    if (nworkers < 1 || nworkers > 4096 || !scheme()) return -1;
+    size_t shm_len = 64 + (size_t)nworkers * 16;
+    uint8_t *shm = mmap(NULL, shm_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (shm == MAP_FAILED) return -1;
+    memset(shm, 0, shm_len);
+    volatile int *go = (volatile int *)shm;
+    double *wt = (double *)(shm + 64);
+    long *wd = (long *)(shm + 64 + (size_t)nworkers * 8);
+    pid_t *pids = calloc((size_t)nworkers, sizeof *pids);
+    int started = 0;
+    for (; started < nworkers; started++) {
+        pid_t pid = fork();
+        if (pid < 0) break;
+        if (pid == 0) {
+            const uint64_t b0 = nblocks * (uint64_t)started / (uint64_t)nworkers;
+            const uint64_t b1 = nblocks * (uint64_t)(started + 1) / (uint64_t)nworkers;
+            uint8_t *rep = malloc((b1 - b0 + 1) * (size_t)r * L);
+            while (!*go) { }
+            const double t0 = now_s();
+            long dec = 0;
+            for (int p = 0; p < passes && dec >= 0; p++) {
+                const long d = ref_work_range(src, rep, b0, b1, k, r, L, fbn_base, sp, skip);
+                dec = d < 0 ? -1 : dec + d;
+            }
+            wt[started] = now_s() - t0;
+            wd[started] = dec;
+            _exit(dec < 0 ? 1 : 0);
+        }
+        pids[started] = pid;
+    }
+    __sync_synchronize();
+    const double t0 = now_s();
+    *go = 1;
+    int ok = started == nworkers;
+    for (int i = 0; i < started; i++) {
+        int status = 0;
+        waitpid(pids[i], &status, 0);
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) ok = 0;
+    }
+    const double wall = now_s() - t0;
+    double mx = 0;
+    long dec = 0;
+    for (int i = 0; i < started; i++) {
+        if (wt[i] > mx) mx = wt[i];
+        dec += wd[i];
+    }
+    out[0] = wall;
+    out[1] = mx;
+    out[2] = (double)dec;
+    free(pids);
+    munmap(shm, shm_len);
+    return ok ? 0 : -1;
 }

@@ -41,7 +41,9 @@ typedef struct job {
     uint32_t k, r, n, cap, stride;
     size_t src_bytes, rep_bytes;   /* allocated pinned sizes */
     uint8_t *src, *rep, *st;       /* pinned */
-    uint32_t *fbn;                 /* pinned */
+    uint32_t *fbn;                 /* pinned: block numbers (generate) */
+    uint32_t *seeds;               /* pinned: [cap][r] repair FPID seeds (recover) */
+    size_t seed_bytes;
     uint64_t *sp, *rp, *rec;       /* pinned, 2 words per block */
     entry_t *ent;
     uint64_t t_first;
@@ -70,6 +72,7 @@ static void job_free(job_t *j) {
     fecgpu_host_free(j->rep);
     fecgpu_host_free(j->st);
     fecgpu_host_free(j->fbn);
+    fecgpu_host_free(j->seeds);
     fecgpu_host_free(j->sp);
     free(j->ent);
     free(j);
@@ -78,10 +81,10 @@ static void job_free(job_t *j) {
 /* A job for (op, scheme, k, r), from the free list when one is big enough. */
 static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
     const uint32_t cap = b->cfg.batch_blocks, S = b->stride;
-    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
+    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S, eb = (size_t)cap * (r ? r : 1) * 4;
     job_t **pp = &b->free_jobs;
     for (; *pp; pp = &(*pp)->next)
-        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb) break;
+        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb && (*pp)->seed_bytes >= eb) break;
     job_t *j = *pp;
     if (j) {
         *pp = j->next;
@@ -90,13 +93,15 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         if (!j) return NULL;
         j->src_bytes = sb;
         j->rep_bytes = rb;
+        j->seed_bytes = eb;
+        j->seeds = fecgpu_host_alloc(eb);
         j->src = fecgpu_host_alloc(sb);
         j->rep = fecgpu_host_alloc(rb ? rb : 4);
         j->st = fecgpu_host_alloc(cap);
         j->fbn = fecgpu_host_alloc((size_t)cap * 4);
         j->sp = fecgpu_host_alloc((size_t)cap * 48);  /* sp | rp | rec, 2 words each per block */
         j->ent = calloc(cap, sizeof *j->ent);
-        if (!j->src || !j->rep || !j->st || !j->fbn || !j->sp || !j->ent) {
+        if (!j->src || !j->rep || !j->st || !j->fbn || !j->seeds || !j->sp || !j->ent) {
             job_free(j);
             return NULL;
         }
@@ -124,8 +129,8 @@ static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
     else
         j->rc = j->xor_scheme
                     ? fecgpu_xor_decode_host(c, j->src, j->rep, j->n, j->k, S, j->sp, j->rp, j->st, j->rec)
-                    : fecgpu_rlc_decode_host(c, j->src, j->rep, j->n, j->k, j->r, S, 0, j->fbn, j->sp, j->rp, j->st,
-                                             j->rec);
+                    : fecgpu_rlc_decode_host_seeded(c, j->src, j->rep, j->n, j->k, j->r, S, j->seeds, j->sp, j->rp,
+                                                    j->st, j->rec);
 }
 
 /* Copies a job's blocks into its page-locked rows (the stage halves of fec_core.c). */
@@ -138,7 +143,7 @@ static void stage_job(job_t *j) {
             fec_generate_stage(e->fb, src, S);
         else
             fec_recover_stage(e->fb, j->xor_scheme, e->maxl, src, j->rep + (size_t)i * r * S, S, j->sp + 2 * (size_t)i,
-                              j->rp + 2 * (size_t)i);
+                              j->rp + 2 * (size_t)i, j->seeds + (size_t)i * r);
     }
 }
 
@@ -282,16 +287,18 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     const uint32_t k = fb->total_source_symbols;
     uint32_t r = fb->total_repair_symbols;
     if (op == OP_GENERATE) {
-        if (fec_generate_check(fb, xor_scheme, &maxl)) {  /* the reference returns 1, nothing done */
+        const int chk = fec_generate_check(fb, xor_scheme, &maxl);
+        if (chk) {  /* the reference returns 1, nothing done; totals past 100 slots are an error */
             b->stats.immediate++;
-            done(user, fb, 1);
+            if (chk == FEC_STAGE_REJECT) FEC_STAT_ADD(errors, 1);
+            done(user, fb, chk == FEC_STAGE_REJECT ? PQUIC_FEC_ERR_UNBOUND : 1);
             return 0;
         }
     } else {
         const int chk = fec_recover_check(fb, xor_scheme, &maxl);
         if (chk != FEC_STAGE_OK) {
             b->stats.immediate++;
-            if (chk == FEC_STAGE_REJECT) g_fec_stats.errors++;
+            if (chk == FEC_STAGE_REJECT) FEC_STAT_ADD(errors, 1);
             done(user, fb, chk == FEC_STAGE_REJECT ? PQUIC_FEC_ERR_UNBOUND : (protoop_arg_t)chk);
             return 0;
         }
@@ -336,7 +343,7 @@ static int collect(pquic_fec_batcher_t *b) {
             entry_t *e = &j->ent[i];
             protoop_arg_t ret;
             if (j->rc) {
-                g_fec_stats.errors++;
+                FEC_STAT_ADD(errors, 1);
                 ret = PQUIC_FEC_ERR_UNBOUND;
             } else if (j->op == OP_GENERATE) {
                 ret = fec_generate_finish(e->cnx, e->fb, j->rep + (size_t)i * j->r * S, S, e->maxl);
@@ -344,7 +351,7 @@ static int collect(pquic_fec_batcher_t *b) {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);
             }
-            if (j->op == OP_GENERATE) g_fec_stats.generate_calls++; else g_fec_stats.recover_calls++;
+            if (j->op == OP_GENERATE) FEC_STAT_ADD(generate_calls, 1); else FEC_STAT_ADD(recover_calls, 1);
             e->done(e->user, e->fb, ret);
             n++;
         }

@@ -45,6 +45,9 @@ int fec_generate_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *ma
     /* rlc_fec_scheme_generate_gf256.c:34-39 / xor_fec_scheme_generate.c:45-50 */
     if ((xor_scheme ? r != 1 : r == 0) || k < 1 || fb->current_source_symbols != fb->total_source_symbols)
         return 1;
+    /* fec_block_t holds 100 source and 100 repair pointers (fec.h:8,128-129); the reference would
+     * index past them for larger totals (they are u8 fields the peer controls on the receive side) */
+    if (k > PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK || r > PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK) return FEC_STAGE_REJECT;
     uint16_t m = 0;
     for (int j = 0; j < k; j++)
         if (fb->source_symbols[j] && fb->source_symbols[j]->data_length > m) m = fb->source_symbols[j]->data_length;
@@ -77,10 +80,11 @@ protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, co
 }
 
 int fec_recover_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *maxl) {
-    const int r = fb->total_repair_symbols;
+    const int k = fb->total_source_symbols, r = fb->total_repair_symbols;
     if (xor_scheme) {
         if (r != 1 || fb->current_source_symbols + fb->current_repair_symbols != fb->total_source_symbols)
             return 1;  /* xor_fec_scheme.c:45-49 */
+        if (k > PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK) return FEC_STAGE_REJECT;
         if (!fb->repair_symbols[0]) return 1;  /* the reference dereferences NULL here (:50-51) */
         *maxl = fb->repair_symbols[0]->data_length;
         return FEC_STAGE_OK;
@@ -88,24 +92,18 @@ int fec_recover_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *max
     if (r == 0 || fb->current_source_symbols == fb->total_source_symbols ||
         fb->current_source_symbols + fb->current_repair_symbols < fb->total_source_symbols)
         return 0;  /* rlc_fec_scheme_gf256.c:140-144 */
+    /* totals beyond the block's 100 symbol slots (fec.h:8): the reference reads past them */
+    if (k > PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK || r > PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK) return FEC_STAGE_REJECT;
     int first = -1;
-    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
-    for (int i = 0; i < r; i++) {
-        const pquic_repair_symbol_t *rs = fb->repair_symbols[i];
-        if (!rs) continue;
-        if (first < 0) first = i;
-        /* the seed is the repair's own FPID (:200); the engine derives it from the block
-         * number and the slot, which the block framework keeps equal
-         * (block_framework_receiver.h:29-56, fec.h:292-299) */
-        if (rs->fpid.f.source_fpid.raw != ((fbn << 8) | (uint32_t)(i & 0xff))) return FEC_STAGE_REJECT;
-    }
+    for (int i = 0; i < r && first < 0; i++)
+        if (fb->repair_symbols[i]) first = i;
     if (first < 0) return 0;
     *maxl = fb->repair_symbols[first]->data_length;  /* :186 */
     return FEC_STAGE_OK;
 }
 
 void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t maxl, uint8_t *src_rows,
-                       uint8_t *rep_rows, uint32_t stride, uint64_t sp[2], uint64_t rp[2]) {
+                       uint8_t *rep_rows, uint32_t stride, uint64_t sp[2], uint64_t rp[2], uint32_t *seeds) {
     const int k = fb->total_source_symbols, r = xor_scheme ? 1 : fb->total_repair_symbols;
     sp[0] = sp[1] = rp[0] = rp[1] = 0;
     for (int j = 0; j < k; j++) {
@@ -129,13 +127,17 @@ void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t max
             rp[i >> 6] |= 1ull << (i & 63);
         }
         memset(row + n, 0, stride - n);
+        /* every equation is seeded by its repair's own FPID (rlc_fec_scheme_gf256.c:200), which the
+         * block framework sets to (fbn << 8) | i and the window framework to (0 << 8) | i in a block
+         * numbered by its window start (window_framework_sender.h:239-243) */
+        if (seeds) seeds[i] = rs ? rs->fpid.f.source_fpid.raw : 0;
     }
 }
 
 protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme, uint8_t status,
                                  const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl) {
     const int k = fb->total_source_symbols;
-    if (status == FECGPU_BLOCK_REF_UB) g_fec_stats.ref_ub_blocks++;
+    if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
     if (!xor_scheme) {
         const uint32_t fbn = fb->fec_block_number & 0xffffffu;
         for (int j = 0; j < k && status == FECGPU_BLOCK_RECOVERED; j++) {  /* :218-236 */
@@ -145,7 +147,7 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
             fb->source_symbols[j] = ss;
             fb->current_source_symbols++;
-            g_fec_stats.recovered_symbols++;
+            FEC_STAT_ADD(recovered_symbols, 1);
         }
         return 0;
     }
@@ -156,7 +158,7 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
         if (!ss) return PQUIC_ERROR_MEMORY;
         memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
         fb->source_symbols[j] = ss;  /* current_source_symbols is NOT incremented (:72) */
-        g_fec_stats.recovered_symbols++;
+        FEC_STAT_ADD(recovered_symbols, 1);
         ret = 0;
     }
     return ret;

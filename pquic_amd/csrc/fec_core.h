@@ -27,6 +27,10 @@ extern pquic_fec_protoop_stats_t g_fec_stats;
 
 static inline uint32_t fec_pad4(uint32_t x) { return (x + 3u) & ~3u; }
 
+/* The adapter counters are shared by the synchronous operations and the batching adapter's
+ * completion path, which may run on different threads. */
+#define FEC_STAT_ADD(field, n) __atomic_fetch_add(&g_fec_stats.field, (uint64_t)(n), __ATOMIC_RELAXED)
+
 /* Generate, before the engine: preconditions of rlc_fec_scheme_generate_gf256.c:34-39 /
  * xor_fec_scheme_generate.c:45-50.  Returns 1 (the reference's "nothing done") when they
  * fail, else 0 with *maxl = max_length (:41-45) and, if src_rows is non-NULL, the k sources
@@ -40,15 +44,17 @@ protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, co
 
 /* Recover, before the engine.  Returns FEC_STAGE_OK when the block goes to the engine;
  * otherwise the value the reference operation returns without doing anything
- * (rlc_fec_scheme_gf256.c:140-144 -> 0; xor_fec_scheme.c:45-51 -> 1), or FEC_STAGE_REJECT
- * for a repair whose FPID does not match its slot (the engine derives coefficients from the
- * block number and slot).  *maxl = the first present repair's length (:186). */
+ * (rlc_fec_scheme_gf256.c:140-144 -> 0; xor_fec_scheme.c:45-51 -> 1), or FEC_STAGE_REJECT for
+ * totals past the block's 100 symbol slots (fec.h:8; the reference reads out of bounds there).
+ * *maxl = the first present repair's length (:186).  fec_generate_check returns FEC_STAGE_REJECT
+ * for the same totals. */
 #define FEC_STAGE_OK (-1)
 #define FEC_STAGE_REJECT (-2)
 int fec_recover_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *maxl);
-/* Rows of `stride` bytes, sources truncated to maxl, zero-padded; presence masks. */
+/* Rows of `stride` bytes, sources truncated to maxl, zero-padded; presence masks; seeds[i] (r
+ * entries, may be NULL) = the TinyMT32 seed of the repair in slot i, its own FPID (:200). */
 void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t maxl, uint8_t *src_rows,
-                       uint8_t *rep_rows, uint32_t stride, uint64_t sp[2], uint64_t rp[2]);
+                       uint8_t *rep_rows, uint32_t stride, uint64_t sp[2], uint64_t rp[2], uint32_t *seeds);
 /* Recover, after the engine: inserts every source the engine marked recovered (maxl bytes
  * from src_rows) with the reference's FPID and counter behaviour (RLC increments
  * current_source_symbols, :230; XOR does not, xor_fec_scheme.c:72).  Returns the

@@ -20,6 +20,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <atomic>
+#include <mutex>
 #include <stdlib.h>
 
 #include "fec_device.h"
@@ -36,6 +37,46 @@ using namespace fecdev;
 
 static thread_local char g_err[256];
 static std::atomic<uint64_t> g_stats[4];
+
+// ---------------------------------------------------------------------------------------------
+// Experiment knobs (A/B runs; the tests cross-check alternative kernels).  The defaults are the
+// measured best.  They are read from the environment ONCE, on first use, so the engine's behaviour
+// cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
+// ---------------------------------------------------------------------------------------------
+enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ, K_N };
+static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
+                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read"};
+enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
+static std::atomic<int> g_knob[K_N];
+static std::once_flag g_knob_once;
+
+static void knobs_from_env() {
+  auto num = [](const char *v, int def) { return v ? atoi(v) : def; };
+  const char *e;
+  g_knob[K_PERM] = (e = getenv("FECGPU_DATAPATH")) && !strcmp(e, "perm");
+  e = getenv("FECGPU_PLAN");
+  g_knob[K_PLAN] = !e ? PLAN_AUTO : !strcmp(e, "wave") ? PLAN_WAVE : !strcmp(e, "lane") ? PLAN_LANE
+                 : !strcmp(e, "reg") ? PLAN_REG : !strcmp(e, "tile") ? PLAN_TILE : PLAN_AUTO;
+  g_knob[K_INTERLEAVE] = num(getenv("FECGPU_INTERLEAVE"), 1) != 0;
+  g_knob[K_GROUP] = num(getenv("FECGPU_GROUP"), 0);  // 0: the measured per-shape defaults
+  int a = 0, b = 0;
+  if ((e = getenv("FECGPU_ENC_TILE")) && sscanf(e, "%d,%d", &a, &b) == 2 &&
+      (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4) {
+    g_knob[K_ENC_RT] = a;
+    g_knob[K_ENC_W] = b;
+  }
+  g_knob[K_XOR_GENERIC] = num(getenv("FECGPU_XOR_GENERIC"), 0) != 0;
+  g_knob[K_XOR_IDX64] = num(getenv("FECGPU_XOR_IDX64"), 0) != 0;
+  g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
+}
+
+static inline int knob(KnobId id) {
+  std::call_once(g_knob_once, knobs_from_env);
+  return g_knob[id].load(std::memory_order_relaxed);
+}
+
+// host_path.hip reads the zero-copy knob through this (library-internal)
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
 
 static int set_err(int code, const char *fmt, const char *what) {
   snprintf(g_err, sizeof g_err, fmt, what);
@@ -74,6 +115,16 @@ __host__ __device__ static inline WsLayout ws_layout(uint32_t k, uint32_t r) {
 
 __device__ __forceinline__ uint32_t block_fbn(uint64_t b, uint32_t fbn_base, const uint32_t *fbn) {
   return fbn ? fbn[b] : (uint32_t)((fbn_base + b) & 0xffffffu);
+}
+
+// TinyMT32 seed of the repair in slot i of block b.  The reference seeds every equation with the
+// repair's own FPID (get_coefs(..., rs->repair_fec_payload_id.source_fpid.raw, ...),
+// rlc_fec_scheme_gf256.c:200): callers that hold received FPIDs pass them as seeds[b * r + i]
+// (the sliding-window framework's repairs carry block number 0 in a block numbered by its window
+// start, window_framework_sender.h:239-243 / window_framework_receiver.h:60-86).  Without seeds
+// the FPID is the block framework's (fbn_b << 8) | i.
+__device__ __forceinline__ uint32_t repair_seed(const uint32_t *seeds, uint64_t b, int r, uint32_t f, uint32_t i) {
+  return seeds ? seeds[b * (uint64_t)r + i] : rlc_seed(f, i);
 }
 
 static uint32_t grid_for(uint64_t units);
@@ -276,7 +327,7 @@ __device__ __forceinline__ void clip128(uint64_t &m0, uint64_t &m1, int n) {
 }
 
 __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r, uint32_t fbn_base,
-                                                 const uint32_t *fbn, const uint64_t *sp,
+                                                 const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
                                                  const uint64_t *rp, uint8_t *ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
@@ -319,7 +370,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
     const uint32_t f = block_fbn(b, fbn_base, fbn);
     for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
       Tmt t;
-      tmt_init(t, rlc_seed(f, (uint32_t)sel[e]));
+      tmt_init(t, repair_seed(seeds, b, r, f, (uint32_t)sel[e]));
       for (int j = 0; j < k; j++) X[e * kpad + j] = tmt_coef(t);
     }
     __syncthreads();
@@ -456,7 +507,7 @@ __host__ __device__ static inline size_t plan_lane_lds(uint32_t k, uint32_t r) {
 }
 
 __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, int r, uint32_t fbn_base,
-                                                      const uint32_t *fbn, const uint64_t *sp,
+                                                      const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
                                                       const uint64_t *rp, uint8_t *ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
@@ -498,7 +549,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, i
       const uint32_t f = block_fbn(b, fbn_base, fbn);
       for (int e = 0; e < n; e++) {  // system rows, :194-212
         Tmt t;
-        tmt_init(t, rlc_seed(f, AR(oS + e)));
+        tmt_init(t, repair_seed(seeds, b, r, f, AR(oS + e)));
         int u = 0;
         for (int j = 0; j < k; j++) {
           uint8_t c = tmt_coef(t);
@@ -607,7 +658,7 @@ __device__ __forceinline__ uint32_t col8(uint64_t row, int i) { return (uint32_t
 
 template <int KD, int EM>
 __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, int r, uint32_t fbn_base,
-                                                     const uint32_t *fbn, const uint64_t *sp,
+                                                     const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
                                                      const uint64_t *rp, uint8_t *ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
@@ -656,7 +707,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
       for (int e = 0; e < EM; e++) {  // system rows, :194-212
         if (e < n) {
           Tmt t;
-          tmt_init(t, rlc_seed(f, col8(S, e)));
+          tmt_init(t, repair_seed(seeds, b, r, f, col8(S, e)));
           int u = 0;
 #pragma unroll
           for (int j = 0; j < 4 * KD; j++) {
@@ -777,7 +828,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
 // ---------------------------------------------------------------------------------------------
 template <int KDL, int EM>
 __global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, int r, uint32_t fbn_base,
-                                                      const uint32_t *fbn, const uint64_t *sp,
+                                                      const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
                                                       const uint64_t *rp, uint8_t *ws) {
   constexpr int LPB = EM / 4;    // lanes per block: one A dword (4 columns) each
   constexpr int BPW = 64 / LPB;  // blocks per wave
@@ -834,7 +885,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, i
     for (int e = q; e < EM; e += LPB) {
       if (state && e < n) {
         Tmt t;
-        tmt_init(t, rlc_seed(f, byte_at(S0, S1, e)));
+        tmt_init(t, repair_seed(seeds, b, r, f, byte_at(S0, S1, e)));
         uint8_t *row = CO + ((size_t)g * EM + e) * kpad;
         for (int j = 0; j < k; j++) row[j] = tmt_coef(t);
       }
@@ -1157,11 +1208,10 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
 // - symbols wider than one column chunk (L > 2 KiB): one block per group (k64 r16 L9000 encode
 //   -2.3 %, decode -8.3 %: the chunk passes then revisit one block's rows);
 // - everything else: 64 / RT.
-// FECGPU_GROUP=N replaces the defaults with a plain cap (A/B experiments).
+// Knob "group" (FECGPU_GROUP=N) replaces the defaults with a plain cap (A/B experiments).
 static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, bool enc, int nchunks) {
   int g = 64 / RT;
-  if (const char *e = getenv("FECGPU_GROUP")) {
-    const int cap = atoi(e);
+  if (const int cap = knob(K_GROUP)) {
     while (g > 1 && g > cap) g >>= 1;
   } else if (nchunks > 1) {
     g = 1;
@@ -1396,10 +1446,7 @@ static BsCfg pick_bs_cfg(int L) {
 // sources as one run of contiguous rows, so overlapping blocks go one per group.
 // Interleaved groups (default): a group's blocks are NG apart, so the resident waves stream
 // neighbouring blocks.  FECGPU_INTERLEAVE=0 restores contiguous groups (A/B experiments).
-static int interleave_groups() {
-  const char *e = getenv("FECGPU_INTERLEAVE");
-  return e ? atoi(e) != 0 : 1;
-}
+static int interleave_groups() { return knob(K_INTERLEAVE); }
 
 template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
@@ -1462,10 +1509,7 @@ static int bs_table_check() {
   return FECGPU_OK;
 }
 
-static bool use_perm_path() {  // FECGPU_DATAPATH=perm: the v_perm data path (A/B; read per call)
-  const char *e = getenv("FECGPU_DATAPATH");
-  return e && strcmp(e, "perm") == 0;
-}
+static bool use_perm_path() { return knob(K_PERM) != 0; }  // the v_perm data path (A/B, tests)
 
 // =============================================================================================
 // XOR scheme
@@ -1568,10 +1612,9 @@ static void xor_dispatch_k(uint32_t k, uint32_t grid, hipStream_t s, A... a) {
 }
 template <typename V, typename OP, typename... A>
 static void xor_dispatch(uint32_t k, uint64_t total, uint32_t grid, hipStream_t s, A... a) {
-  const char *e = getenv("FECGPU_XOR_GENERIC");  // A/B: the runtime-k, 64-bit-index kernel
-  if (e && atoi(e)) return xor_dispatch_k<V, OP, uint64_t>(0, grid, s, a...);
-  const char *w = getenv("FECGPU_XOR_IDX64");  // tests: the 64-bit-index instantiations at small sizes
-  if (total < (1ull << 32) - (uint64_t)grid * 256 && !(w && atoi(w)))
+  if (knob(K_XOR_GENERIC)) return xor_dispatch_k<V, OP, uint64_t>(0, grid, s, a...);  // A/B: runtime k, 64-bit index
+  // knob xor_idx64 (tests): the 64-bit-index instantiations at small sizes
+  if (total < (1ull << 32) - (uint64_t)grid * 256 && !knob(K_XOR_IDX64))
     xor_dispatch_k<V, OP, uint32_t>(k, grid, s, a...);
   else
     xor_dispatch_k<V, OP, uint64_t>(k, grid, s, a...);
@@ -1790,6 +1833,7 @@ const char *fecgpu_version(void) { return FECGPU_VERSION; }
 const char *fecgpu_last_error(void) { return g_err; }
 
 int fecgpu_init(int device) {
+  std::call_once(g_knob_once, knobs_from_env);
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device)
     return set_err(FECGPU_ERR_NO_DEVICE, "%s", "no HIP device");
@@ -1805,6 +1849,26 @@ int fecgpu_init(int device) {
   return rc;
 }
 
+int fecgpu_set_knob(const char *name, int value) {
+  std::call_once(g_knob_once, knobs_from_env);
+  for (int i = 0; i < K_N; i++)
+    if (name && !strcmp(name, kKnobName[i])) {
+      g_knob[i].store(value, std::memory_order_relaxed);
+      return FECGPU_OK;
+    }
+  return set_err(FECGPU_ERR_INVALID, "unknown knob %s", name ? name : "(null)");
+}
+
+int fecgpu_get_knob(const char *name, int *value) {
+  std::call_once(g_knob_once, knobs_from_env);
+  for (int i = 0; i < K_N; i++)
+    if (name && value && !strcmp(name, kKnobName[i])) {
+      *value = g_knob[i].load(std::memory_order_relaxed);
+      return FECGPU_OK;
+    }
+  return set_err(FECGPU_ERR_INVALID, "unknown knob %s", name ? name : "(null)");
+}
+
 void fecgpu_get_stats(fecgpu_stats_t *out) {
   out->encode_calls = g_stats[0].load();
   out->encode_blocks = g_stats[1].load();
@@ -1813,13 +1877,12 @@ void fecgpu_get_stats(fecgpu_stats_t *out) {
 }
 
 // Encode tiling: repairs per wave (RT) and waves per workgroup sharing the source stream.
-// FECGPU_ENC_TILE="RT,W" overrides (A/B experiments).
+// Knobs enc_tile_rt / enc_tile_waves (FECGPU_ENC_TILE="RT,W") override (A/B experiments).
 struct EncTile { int rt, waves; };
 static EncTile pick_enc_tile(uint32_t r) {
-  if (const char *e = getenv("FECGPU_ENC_TILE")) {  // read per call (in-process A/B)
-    int a = 0, b = 0;
-    if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4)
-      return {a, b};
+  if (const int a = knob(K_ENC_RT)) {  // knobs enc_tile_rt / enc_tile_waves (FECGPU_ENC_TILE="RT,W")
+    const int b = knob(K_ENC_W);
+    return {a, b >= 1 && b <= 4 ? b : 1};
   }
   // measured (profiles/r01_tile_ab.log): splitting repairs over waves repeats the transpose and
   // table work per wave and loses more VALU than the occupancy gains (k32r8 4x2: +34 %,
@@ -1907,9 +1970,9 @@ static int decode_args(const void *src, const void *rep, uint64_t nblocks, uint3
   return FECGPU_OK;
 }
 
-int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
-                           const uint64_t *src_present, const uint64_t *rep_present, void *workspace,
-                           size_t workspace_bytes, void *stream) {
+static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
+                            const uint32_t *seeds, const uint64_t *src_present, const uint64_t *rep_present,
+                            void *workspace, size_t workspace_bytes, void *stream) {
   static const uint32_t dummy = 0;
   int rc = decode_args(&dummy, &dummy, nblocks, k, r, 4, src_present, rep_present, &dummy, &dummy, workspace,
                        workspace_bytes);
@@ -1917,18 +1980,16 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
   hipStream_t s = (hipStream_t)stream;
   uint8_t *ws = (uint8_t *)workspace;
   const size_t lane_lds = plan_lane_lds(k, r);
-  // FECGPU_PLAN=reg|tile|lane|wave overrides the size rule (A/B experiments, cross-checks in the tests);
-  // read per call so a test process can compare the plan kernels on the same inputs
-  const char *pe = getenv("FECGPU_PLAN");
-  const int force = pe && !strcmp(pe, "wave") ? 1 : pe && !strcmp(pe, "lane") ? 2 : pe && !strcmp(pe, "reg") ? 3
-                  : pe && !strcmp(pe, "tile") ? 4 : 0;
+  // knob "plan" (FECGPU_PLAN=reg|tile|lane|wave) overrides the size rule (A/B experiments; the tests
+  // compare the plan kernels on the same inputs through fecgpu_set_knob)
+  const int force = knob(K_PLAN);
   const uint32_t em = ws_layout(k, r).em;
   if ((force == 0 || force == 3) && k <= 32 && em <= 8) {
     const size_t reg_lds = 768 + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
     const uint64_t groups = (nblocks + 63) / 64;
 #define FEC_PLAN_REG(KD, EM)                                                                         \
   hipLaunchKernelGGL((k_rlc_plan_reg<KD, EM>), dim3(grid_for(groups)), dim3(64), reg_lds, s, nblocks, \
-                     (int)k, (int)r, fbn_base, fbn, src_present, rep_present, ws)
+                     (int)k, (int)r, fbn_base, fbn, seeds, src_present, rep_present, ws)
     if (k <= 16 && em <= 4) FEC_PLAN_REG(4, 4);
     else if (k <= 16) FEC_PLAN_REG(4, 8);
     else if (em <= 4) FEC_PLAN_REG(8, 4);
@@ -1950,7 +2011,7 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
     }
     const uint64_t groups = (nblocks + BPW - 1) / BPW;
     hipLaunchKernelGGL((k_rlc_plan_tile<4, 16>), dim3(grid_for(groups)), dim3(64), tile_lds, s, nblocks,
-                       (int)k, (int)r, fbn_base, fbn, src_present, rep_present, ws);
+                       (int)k, (int)r, fbn_base, fbn, seeds, src_present, rep_present, ws);
     HIPCHK(hipGetLastError());
     return FECGPU_OK;
   }
@@ -1965,7 +2026,7 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
     }
     const uint64_t groups = (nblocks + 63) / 64;
     hipLaunchKernelGGL(k_rlc_plan_lane, dim3(grid_for(groups)), dim3(64), lane_lds, s, nblocks, (int)k,
-                       (int)r, fbn_base, fbn, src_present, rep_present, ws);
+                       (int)r, fbn_base, fbn, seeds, src_present, rep_present, ws);
   } else {
     const size_t plan_lds = plan_lds_bytes(k, r);
     if (plan_lds > 65536) {
@@ -1976,10 +2037,25 @@ int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fb
       }
     }
     hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
-                       fbn_base, fbn, src_present, rep_present, ws);
+                       fbn_base, fbn, seeds, src_present, rep_present, ws);
   }
   HIPCHK(hipGetLastError());
   return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode_plan(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
+                           const uint64_t *src_present, const uint64_t *rep_present, void *workspace,
+                           size_t workspace_bytes, void *stream) {
+  return decode_plan_impl(nblocks, k, r, fbn_base, fbn, nullptr, src_present, rep_present, workspace,
+                          workspace_bytes, stream);
+}
+
+int fecgpu_rlc_decode_plan_seeded(uint64_t nblocks, uint32_t k, uint32_t r, const uint32_t *rep_seed,
+                                  const uint64_t *src_present, const uint64_t *rep_present, void *workspace,
+                                  size_t workspace_bytes, void *stream) {
+  if (nblocks && r && !rep_seed) return set_err(FECGPU_ERR_INVALID, "%s", "NULL rep_seed");
+  return decode_plan_impl(nblocks, k, r, 0, nullptr, rep_seed, src_present, rep_present, workspace,
+                          workspace_bytes, stream);
 }
 
 static int launch_finalize(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *status, uint64_t *recovered,
@@ -2058,6 +2134,20 @@ int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
                                     workspace_bytes, stream)))
     return rc;
   return FECGPU_OK;
+}
+
+int fecgpu_rlc_decode_seeded(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
+                             uint32_t symbol_size, const uint32_t *rep_seed, const uint64_t *src_present,
+                             const uint64_t *rep_present, uint8_t *status, uint64_t *recovered, void *workspace,
+                             size_t workspace_bytes, void *stream) {
+  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, src_present, rep_present, status, recovered,
+                       workspace, workspace_bytes);
+  if (rc || nblocks == 0) return rc;
+  if ((rc = fecgpu_rlc_decode_plan_seeded(nblocks, k, r, rep_seed, src_present, rep_present, workspace,
+                                          workspace_bytes, stream)))
+    return rc;
+  return fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, status, recovered, workspace,
+                                 workspace_bytes, stream);
 }
 
 int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,

@@ -90,11 +90,9 @@ static uint8_t *mapped_host(const void *p) {
 
 // Page-locked host buffers are read (and written) by the kernels directly over PCIe instead of
 // being staged by copies: measured 49.2 -> 51.0 GiB/s encode, 39.2 -> 50.3 GiB/s decode
-// (k16 r4, 2^18 blocks).  FECGPU_ZC_READ=0 restores the staged copies (A/B).
-static bool zc_read() {
-  const char *e = getenv("FECGPU_ZC_READ");
-  return e ? atoi(e) != 0 : true;
-}
+// (k16 r4, 2^18 blocks).  Knob zc_read = 0 (FECGPU_ZC_READ=0) restores the staged copies (A/B).
+int fecgpu_knob_zc_read(void);  // fec_engine.hip (library-internal, C linkage)
+static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 
 static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t per_block) {
   uint64_t n = c->chunk_bytes / (per_block ? per_block : 1);
@@ -102,10 +100,24 @@ static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t p
   return n < nblocks ? n : nblocks;
 }
 
-static int finish(fecgpu_host_ctx_t *c) {
-  for (int i = 0; i < c->ns; i++) HCHK(hipStreamSynchronize(c->slot[i].st));
-  return FECGPU_OK;
+// Every stream drains before a call returns -- also after an error part-way through a batch: work
+// already queued (copies, and with page-locked buffers kernels writing repairs / recovered rows
+// straight into host memory) must not outlive the call, or it could overwrite buffers the caller
+// reuses (the batching adapter recycles its page-locked rows as soon as a job completes).
+static int finish(fecgpu_host_ctx_t *c, int rc) {
+  for (int i = 0; i < c->ns; i++) {
+    const hipError_t e = hipStreamSynchronize(c->slot[i].st);
+    if (e != hipSuccess && rc == FECGPU_OK) rc = FECGPU_ERR_HIP;
+  }
+  return rc;
 }
+
+// HCHK inside a sub-batch loop: record the error and leave the loop (finish() then drains).
+#define LCHK(x)                               \
+  if ((x) != hipSuccess) {                    \
+    rc = FECGPU_ERR_HIP;                      \
+    break;                                    \
+  }
 
 int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uint64_t nblocks, uint32_t k,
                            uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn) {
@@ -116,30 +128,28 @@ int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   const size_t sb = (size_t)k * L, rb = (size_t)r * L;
   const uint64_t n = sub_batch(c, nblocks, sb);
   uint8_t *zs = zc_read() ? mapped_host(src) : nullptr, *zr = zs ? mapped_host(rep) : nullptr;
-  int si = 0;
+  int si = 0, rc = FECGPU_OK;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
     const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
-    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
-    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
     const uint32_t *df = nullptr;
     if (fbn) {
-      HCHK(grow(&s.d_aux, &s.cap_aux, n * 4));
-      HCHK(hipMemcpyAsync(s.d_aux, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+      LCHK(grow(&s.d_aux, &s.cap_aux, n * 4));
+      LCHK(hipMemcpyAsync(s.d_aux, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
       df = (const uint32_t *)s.d_aux;
     }
+    const uint32_t fb0 = (uint32_t)((fbn_base + b0) & 0xffffffu);
     if (zs && zr) {  // page-locked buffers: the kernel reads sources from / writes repairs to host memory
-      int rc = fecgpu_rlc_encode(zs + b0 * sb, zr + b0 * rb, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu), df,
-                                 s.st);
-      if (rc) return rc;
+      if ((rc = fecgpu_rlc_encode(zs + b0 * sb, zr + b0 * rb, m, k, r, L, fb0, df, s.st))) break;
       continue;
     }
-    HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
-    int rc = fecgpu_rlc_encode(s.d_src, s.d_rep, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu), df, s.st);
-    if (rc) return rc;
-    HCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
+    LCHK(grow(&s.d_src, &s.cap_src, n * sb));
+    LCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+    LCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+    if ((rc = fecgpu_rlc_encode(s.d_src, s.d_rep, m, k, r, L, fb0, df, s.st))) break;
+    LCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
   }
-  return finish(c);
+  return finish(c, rc);
 }
 
 int fecgpu_xor_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uint64_t nblocks, uint32_t k,
@@ -150,90 +160,104 @@ int fecgpu_xor_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   HCHK(hipSetDevice(c->device));
   const size_t sb = (size_t)k * L, rb = L;
   const uint64_t n = sub_batch(c, nblocks, sb);
-  int si = 0;
+  int si = 0, rc = FECGPU_OK;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
     const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
-    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
-    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
-    HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
-    int rc = fecgpu_xor_encode(s.d_src, s.d_rep, m, k, L, s.st);
-    if (rc) return rc;
-    HCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
+    LCHK(grow(&s.d_src, &s.cap_src, n * sb));
+    LCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+    LCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+    if ((rc = fecgpu_xor_encode(s.d_src, s.d_rep, m, k, L, s.st))) break;
+    LCHK(hipMemcpyAsync((uint8_t *)rep + b0 * rb, s.d_rep, m * rb, hipMemcpyDeviceToHost, s.st));
   }
-  return finish(c);
+  return finish(c, rc);
 }
 
-// aux layout per sub-batch: fbn[n] (u32, padded to 16), src_present[n][2], rep_present[n][2],
-// recovered[n][2] (u64), status[n] (u8)
-static size_t aux_bytes(uint64_t n) { return ((n * 4 + 15) & ~(size_t)15) + n * 16 * 3 + n; }
+// aux layout per sub-batch: fbn[n] or rep_seed[n][r] (u32, padded to 16), src_present[n][2],
+// rep_present[n][2], recovered[n][2] (u64), status[n] (u8)
+static size_t aux_bytes(uint64_t n, uint32_t nseed) { return ((n * 4 * nseed + 15) & ~(size_t)15) + n * 16 * 3 + n; }
 
+// seeds: rep_seed[nblocks][r] (per-repair FPID seeds) or nullptr (block numbers from fbn / fbn_base)
 static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep, uint64_t nblocks, uint32_t k,
-                       uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn, const uint64_t *sp,
-                       const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
+                       uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn, const uint32_t *seeds,
+                       const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
   if (!c || !src || !rep || !sp || !rp || !status || !recovered) return FECGPU_ERR_INVALID;
   if (!nblocks) return FECGPU_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HCHK(hipSetDevice(c->device));
   const size_t sb = (size_t)k * L, rb = (size_t)r * L;
+  const uint32_t nseed = seeds ? (r ? r : 1) : 1;
   const uint64_t n = sub_batch(c, nblocks, sb + rb);
   // page-locked src (hipHostMalloc / registered): the apply kernel writes the recovered rows
   // straight into it over PCIe, so nothing but status comes back by copy
   uint8_t *zdst = xr ? nullptr : mapped_host(src);
   const uint8_t *zrep = zdst && zc_read() ? mapped_host(rep) : nullptr;
-  int si = 0;
+  int si = 0, rc = FECGPU_OK;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
     const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
-    HCHK(grow(&s.d_src, &s.cap_src, n * sb));
-    HCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
-    HCHK(grow(&s.d_aux, &s.cap_aux, aux_bytes(n)));
+    LCHK(grow(&s.d_aux, &s.cap_aux, aux_bytes(n, nseed)));
     uint8_t *aux = (uint8_t *)s.d_aux;
-    uint32_t *d_fbn = (uint32_t *)aux;
-    uint64_t *d_sp = (uint64_t *)(aux + ((n * 4 + 15) & ~(size_t)15));
+    uint32_t *d_fbn = (uint32_t *)aux;  // fbn[] or rep_seed[][]
+    uint64_t *d_sp = (uint64_t *)(aux + ((n * 4 * nseed + 15) & ~(size_t)15));
     uint64_t *d_rp = d_sp + 2 * n, *d_rec = d_rp + 2 * n;
     uint8_t *d_st = (uint8_t *)(d_rec + 2 * n);
-    HCHK(hipMemcpyAsync(d_sp, sp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
-    HCHK(hipMemcpyAsync(d_rp, rp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
-    if (fbn) HCHK(hipMemcpyAsync(d_fbn, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
-    const uint8_t *in_src = (const uint8_t *)s.d_src, *in_rep = (const uint8_t *)s.d_rep;
+    LCHK(hipMemcpyAsync(d_sp, sp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+    LCHK(hipMemcpyAsync(d_rp, rp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+    if (seeds && r) {
+      LCHK(hipMemcpyAsync(d_fbn, seeds + b0 * r, m * 4 * r, hipMemcpyHostToDevice, s.st));
+    } else if (fbn) {
+      LCHK(hipMemcpyAsync(d_fbn, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+    }
+    const uint8_t *in_src, *in_rep;
     if (zrep) {
       in_src = zdst + b0 * sb;
       in_rep = zrep + b0 * rb;
     } else {
-      HCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
-      HCHK(hipMemcpyAsync(s.d_rep, (const uint8_t *)rep + b0 * rb, m * rb, hipMemcpyHostToDevice, s.st));
+      LCHK(grow(&s.d_src, &s.cap_src, n * sb));
+      LCHK(grow(&s.d_rep, &s.cap_rep, n * rb));
+      in_src = (const uint8_t *)s.d_src;
+      in_rep = (const uint8_t *)s.d_rep;
+      LCHK(hipMemcpyAsync(s.d_src, (const uint8_t *)src + b0 * sb, m * sb, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync(s.d_rep, (const uint8_t *)rep + b0 * rb, m * rb, hipMemcpyHostToDevice, s.st));
     }
-    int rc;
     if (xr) {
       rc = fecgpu_xor_decode(s.d_src, s.d_rep, m, k, L, d_sp, d_rp, d_st, d_rec, s.st);
     } else {
       const size_t wsb = fecgpu_rlc_decode_workspace(n, k, r);
-      HCHK(grow(&s.d_ws, &s.cap_ws, wsb));
-      rc = fecgpu_rlc_decode_plan(m, k, r, (uint32_t)((fbn_base + b0) & 0xffffffu), fbn ? d_fbn : nullptr, d_sp,
-                                  d_rp, s.d_ws, s.cap_ws, s.st);
+      LCHK(grow(&s.d_ws, &s.cap_ws, wsb));
+      rc = seeds ? fecgpu_rlc_decode_plan_seeded(m, k, r, d_fbn, d_sp, d_rp, s.d_ws, s.cap_ws, s.st)
+                 : fecgpu_rlc_decode_plan(m, k, r, (uint32_t)((fbn_base + b0) & 0xffffffu), fbn ? d_fbn : nullptr,
+                                          d_sp, d_rp, s.d_ws, s.cap_ws, s.st);
       if (!rc)
         rc = fecgpu_rlc_decode_apply_to(in_src, in_rep, zdst ? zdst + b0 * sb : s.d_src, m, k, r, L, d_st, d_rec,
                                         s.d_ws, s.cap_ws, s.st);
     }
-    if (rc) return rc;
-    if (!zdst) HCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
-    HCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
-    HCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
+    if (rc) break;
+    if (!zdst) LCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
+    LCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
+    LCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
   }
-  return finish(c);
+  return finish(c, rc);
 }
 
 int fecgpu_rlc_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
                            uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn,
                            const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
-  return decode_host(c, false, src, rep, nblocks, k, r, L, fbn_base, fbn, sp, rp, status, recovered);
+  return decode_host(c, false, src, rep, nblocks, k, r, L, fbn_base, fbn, nullptr, sp, rp, status, recovered);
+}
+
+int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
+                                  uint32_t r, uint32_t L, const uint32_t *rep_seed, const uint64_t *sp,
+                                  const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
+  if (nblocks && r && !rep_seed) return FECGPU_ERR_INVALID;
+  return decode_host(c, false, src, rep, nblocks, k, r, L, 0, nullptr, rep_seed, sp, rp, status, recovered);
 }
 
 int fecgpu_xor_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
                            uint32_t L, const uint64_t *sp, const uint64_t *rp, uint8_t *status,
                            uint64_t *recovered) {
-  return decode_host(c, true, src, rep, nblocks, k, 1, L, 0, nullptr, sp, rp, status, recovered);
+  return decode_host(c, true, src, rep, nblocks, k, 1, L, 0, nullptr, nullptr, sp, rp, status, recovered);
 }
 
 }  // extern "C"

@@ -60,7 +60,13 @@ int pquic_fec_bind_host(const pquic_fec_host_api_t *api, int device) {
     return g_fec_bound ? 0 : -1;
 }
 
-void pquic_fec_protoop_stats(pquic_fec_protoop_stats_t *out) { *out = g_fec_stats; }
+void pquic_fec_protoop_stats(pquic_fec_protoop_stats_t *out) {
+    out->generate_calls = __atomic_load_n(&g_fec_stats.generate_calls, __ATOMIC_RELAXED);
+    out->recover_calls = __atomic_load_n(&g_fec_stats.recover_calls, __ATOMIC_RELAXED);
+    out->recovered_symbols = __atomic_load_n(&g_fec_stats.recovered_symbols, __ATOMIC_RELAXED);
+    out->ref_ub_blocks = __atomic_load_n(&g_fec_stats.ref_ub_blocks, __ATOMIC_RELAXED);
+    out->errors = __atomic_load_n(&g_fec_stats.errors, __ATOMIC_RELAXED);
+}
 
 int pquic_fec_layout(uint64_t out[8]) {
     out[0] = sizeof(pquic_fec_block_t);
@@ -126,11 +132,16 @@ static protoop_arg_t generate(picoquic_cnx_t *cnx, int xor_scheme) {
     if (!g_fec_bound) return PQUIC_FEC_ERR_UNBOUND;
     pquic_fec_block_t *fb = (pquic_fec_block_t *)(uintptr_t)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 0);
     uint16_t maxl = 0;
-    if (fec_generate_check(fb, xor_scheme, &maxl)) return 1;
+    const int chk = fec_generate_check(fb, xor_scheme, &maxl);
+    if (chk == FEC_STAGE_REJECT) {
+        FEC_STAT_ADD(errors, 1);
+        return PQUIC_FEC_ERR_UNBOUND;
+    }
+    if (chk) return 1;
     const int k = fb->total_source_symbols, r = fb->total_repair_symbols;
     const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     pthread_mutex_lock(&g_mu);
-    g_fec_stats.generate_calls++;
+    FEC_STAT_ADD(generate_calls, 1);
     const uint32_t L = fec_pad4(maxl ? maxl : 1);
     int rc = stage((size_t)k * L, (size_t)r * L);
     fecgpu_host_ctx_t *c = rc ? NULL : ctx();
@@ -143,7 +154,7 @@ static protoop_arg_t generate(picoquic_cnx_t *cnx, int xor_scheme) {
     }
     protoop_arg_t ret;
     if (rc) {
-        g_fec_stats.errors++;
+        FEC_STAT_ADD(errors, 1);
         ret = PQUIC_FEC_ERR_UNBOUND;
     } else {
         ret = fec_generate_finish(cnx, fb, g_rep, L, maxl);
@@ -157,39 +168,40 @@ protoop_arg_t pquic_fec_xor_generate_repair_symbols(picoquic_cnx_t *cnx) { retur
 
 /* ------------------------------------------------------------------ recover */
 
-/* rlc_fec_scheme_gf256.c:134-251 and xor_fec_scheme.c:41-74 */
+/* rlc_fec_scheme_gf256.c:134-251 and xor_fec_scheme.c:41-74.  The RLC equations are seeded by each
+ * received repair's own FPID (:200), so blocks of the block framework ((fbn << 8) | i) and of the
+ * sliding-window framework (block numbered by its window start, repairs (0 << 8) | i) both recover
+ * as the reference does. */
 static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
     if (!g_fec_bound) return PQUIC_FEC_ERR_UNBOUND;
     pquic_fec_block_t *fb = (pquic_fec_block_t *)(uintptr_t)g_fec_api.get_cnx(cnx, PQUIC_AK_CNX_INPUT, 0);
     uint16_t maxl = 0;
     const int chk = fec_recover_check(fb, xor_scheme, &maxl);
     if (chk == FEC_STAGE_REJECT) {
-        pthread_mutex_lock(&g_mu);
-        g_fec_stats.errors++;
-        pthread_mutex_unlock(&g_mu);
+        FEC_STAT_ADD(errors, 1);
         return PQUIC_FEC_ERR_UNBOUND;
     }
     if (chk != FEC_STAGE_OK) return (protoop_arg_t)chk;
     const int k = fb->total_source_symbols, r = xor_scheme ? 1 : fb->total_repair_symbols;
-    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     pthread_mutex_lock(&g_mu);
-    g_fec_stats.recover_calls++;
+    FEC_STAT_ADD(recover_calls, 1);
     const uint32_t L = fec_pad4(maxl ? maxl : 1);
     uint64_t sp[2], rp[2], rec[2] = {0, 0};
+    uint32_t seeds[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
     uint8_t st = FECGPU_BLOCK_NOTHING;
     int rc = stage((size_t)k * L, (size_t)r * L);
     fecgpu_host_ctx_t *c = rc ? NULL : ctx();
     if (c) {
-        fec_recover_stage(fb, xor_scheme, maxl, g_src, g_rep, L, sp, rp);
+        fec_recover_stage(fb, xor_scheme, maxl, g_src, g_rep, L, sp, rp, seeds);
         rc = xor_scheme ? fecgpu_xor_decode_host(c, g_src, g_rep, 1, (uint32_t)k, L, sp, rp, &st, rec)
-                        : fecgpu_rlc_decode_host(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, fbn, NULL, sp, rp,
-                                                 &st, rec);
+                        : fecgpu_rlc_decode_host_seeded(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, seeds, sp,
+                                                        rp, &st, rec);
     } else {
         rc = -1;
     }
     protoop_arg_t ret;
     if (rc) {
-        g_fec_stats.errors++;
+        FEC_STAT_ADD(errors, 1);
         ret = PQUIC_FEC_ERR_UNBOUND;
     } else {
         ret = fec_recover_finish(cnx, fb, xor_scheme, st, rec, g_src, L, maxl);

@@ -50,15 +50,20 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
     L.fecgpu_rlc_decode_plan.argtypes = [u64, u32, u32, u32, v, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_plan_seeded.argtypes = [u64, u32, u32, v, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_seeded.argtypes = [v, v, u64, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply_to.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
+    L.fecgpu_set_knob.argtypes = [C.c_char_p, C.c_int]
+    L.fecgpu_get_knob.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
     L.fecgpu_host_ctx_create.argtypes = [C.c_int, C.c_int, sz]
     L.fecgpu_host_ctx_create.restype = v
     L.fecgpu_host_ctx_destroy.argtypes = [v]
     L.fecgpu_rlc_encode_host.argtypes = [v, v, v, u64, u32, u32, u32, u32, v]
     L.fecgpu_rlc_decode_host.argtypes = [v, v, v, u64, u32, u32, u32, u32, v, v, v, v, v]
+    L.fecgpu_rlc_decode_host_seeded.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, v, v]
     L.fecgpu_xor_encode_host.argtypes = [v, v, v, u64, u32, u32]
     L.fecgpu_xor_decode_host.argtypes = [v, v, v, u64, u32, u32, v, v, v, v]
     if not private:
@@ -103,6 +108,28 @@ class Engine:
     def _check(self, rc, what):
         if rc != OK:
             raise FecGpuError(f"{what} failed ({rc}): {self.err()}")
+
+    def get_knob(self, name: str) -> int:
+        v = C.c_int(0)
+        self._check(self.lib.fecgpu_get_knob(name.encode(), C.byref(v)), f"fecgpu_get_knob({name})")
+        return v.value
+
+    def set_knob(self, name: str, value: int):
+        self._check(self.lib.fecgpu_set_knob(name.encode(), int(value)), f"fecgpu_set_knob({name})")
+
+    def knob(self, name: str, value: int):
+        """Context manager: an experiment knob (fecgpu_set_knob) set for the duration of a block."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = self.get_knob(name)
+            self.set_knob(name, value)
+            try:
+                yield
+            finally:
+                self.set_knob(name, old)
+        return cm()
 
     def stats(self) -> dict:
         s = FecGpuStats()
@@ -155,6 +182,19 @@ class Engine:
             _addr(src), _addr(rep), nb, k, r, L, fbn_base, _addr(fbn), _addr(src_present),
             _addr(rep_present), _addr(status), _addr(recovered), _addr(workspace),
             workspace.numel(), self._stream(stream)), "fecgpu_rlc_decode")
+        return status, recovered
+
+    def rlc_decode_seeded(self, src, rep, rep_seed, src_present, rep_present, status, recovered, k: int, r: int,
+                          L: int, nblocks: int | None = None, workspace=None, stream=None):
+        """fecgpu_rlc_decode_seeded: every received repair's coefficients seeded by its own FPID,
+        rep_seed[b * r + i] (u32 device array) -- the sliding-window framework's blocks."""
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        if workspace is None:
+            workspace = self.alloc_workspace(nb, k, r)
+        self._check(self.lib.fecgpu_rlc_decode_seeded(
+            _addr(src), _addr(rep), nb, k, r, L, _addr(rep_seed), _addr(src_present), _addr(rep_present),
+            _addr(status), _addr(recovered), _addr(workspace), workspace.numel(), self._stream(stream)),
+            "fecgpu_rlc_decode_seeded")
         return status, recovered
 
     def rlc_decode_stages(self, src, rep, src_present, rep_present, status, recovered, k, r, L, nblocks,
@@ -250,3 +290,8 @@ class HostPath:
         self._chk(self.lib.fecgpu_rlc_decode_host(self.ctx, _addr(src), _addr(rep), nblocks, k, r, L, fbn_base,
                                                   None, _addr(sp), _addr(rp), _addr(status), _addr(rec)),
                   "fecgpu_rlc_decode_host")
+
+    def rlc_decode_seeded(self, src, rep, seeds, sp, rp, status, rec, nblocks, k, r, L):
+        self._chk(self.lib.fecgpu_rlc_decode_host_seeded(self.ctx, _addr(src), _addr(rep), nblocks, k, r, L,
+                                                         _addr(seeds), _addr(sp), _addr(rp), _addr(status),
+                                                         _addr(rec)), "fecgpu_rlc_decode_host_seeded")

@@ -225,6 +225,81 @@ def main():
     crashes = sum(c["crashed"] for c in dec_cases)
     print(f"encode cases {len(enc_cases)}, varlen {len(var_cases)}, decode {len(dec_cases)} "
           f"({crashes} reference crashes), zero {len(zero_cases)}, varlen-dec {len(vdec)}")
+    window_cases(R)
+
+
+def window_cases(R):
+    """Sliding-window-shaped blocks (the framework every shipped FEC manifest composes:
+    plugins/fec/fec.plugin:5-8, fec_rlc_gf256_window.plugin:5-8).
+
+    Sender (window_framework_sender.h:209-250): the protected window is a block numbered 0
+    (malloc_fec_block(cnx, 0), :215), so the reference encode seeds repair i with (0 << 8) | i;
+    the repairs then leave with fec_block_number 0, symbol_number i and fec_scheme_specific = the
+    window's first source id (:239-243).
+    Receiver (window_framework_receiver.h:60-86): the block is numbered by that first source id
+    (malloc_fec_block(cnx, source_symbol_id)) and repairs are slotted by symbol_number
+    (fec.h:292-299); fec_recover seeds each equation with the repair's own FPID (:200) and stamps
+    recovered sources (fec_block_number << 8) + j (:222).
+    A few "mixed" blocks carry repairs whose FPID block numbers differ from each other (a peer
+    is free to send them): the reference still seeds each equation by its own FPID."""
+    out = []
+    wrng = np.random.default_rng(4242)
+    shapes = [(5, 1), (5, 2), (10, 3), (16, 4), (25, 5), (30, 5), (30, 10), (32, 8), (8, 8)]
+    for t in range(160):
+        k, r = shapes[t % len(shapes)]
+        xor = r == 1 and t % 2 == 0
+        varlen = t % 4 == 3
+        L = 1200 if t % 3 else int(wrng.integers(1, 400)) * 4
+        dseed = 70000 + t
+        lens = [int(x) for x in wrng.integers(1, L + 1, k)] if varlen else None
+        srcs_full = block_sources(dseed, k, L, lens)
+        start = int(wrng.integers(0, 1 << 32)) if t % 5 else int(wrng.integers((1 << 32) - 64, 1 << 32))
+        mixed = (not xor) and t % 11 == 7
+        if mixed:  # every repair from a different block number: encode each one from its own block
+            seed_fbn = [int(wrng.integers(0, 1 << 24)) for _ in range(r)]
+            reps_full = []
+            for i in range(r):
+                ret, rs, _ = R.encode_block(False, seed_fbn[i], srcs_full, r)
+                assert ret == 0
+                reps_full.append(rs[i])
+        else:
+            seed_fbn = [0] * r
+            ret, reps_full, _ = R.encode_block(xor, 0, srcs_full, r)   # window block number 0
+            assert ret == 0
+        fpids = [((seed_fbn[i] << 8) | i) | (start << 32) for i in range(r)]
+        e = int(wrng.integers(1, min(r, k) + 1)) if not xor else 1
+        src_mask = np.ones(k, bool)
+        src_mask[wrng.choice(k, size=e, replace=False)] = False
+        rep_mask = np.zeros(r, bool)
+        if t % 3 == 0:
+            rep_mask[: min(e, r)] = True
+        else:
+            rep_mask[wrng.choice(r, size=int(wrng.integers(min(e, r), r + 1)), replace=False)] = True
+        srcs = [srcs_full[j] if src_mask[j] else None for j in range(k)]
+        reps = [reps_full[i] if rep_mask[i] else None for i in range(r)]
+        ret, rec, rfp = R.decode_block(xor, start, srcs, reps, fpids, with_fpids=True)
+        d = {"tag": f"window_t{t}", "scheme": "xor" if xor else "rlc", "fbn": start, "k": k, "r": r, "L": L,
+             "data_seed": dseed, "src_len": lens, "mixed_seeds": mixed, "repair_fpid_raw": fpids,
+             "src_missing": [j for j in range(k) if not src_mask[j]],
+             "rep_present": [i for i in range(r) if rep_mask[i]],
+             "ret": ret, "crashed": ret <= -1000,
+             "recovered": {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())},
+             "recovered_len": {str(j): int(len(v)) for j, v in sorted(rec.items())},
+             "recovered_fpid": {str(j): int(f) for j, f in sorted(rfp.items())}}
+        if not d["crashed"]:
+            d["recovered_equals_original"] = all(
+                (v[: len(srcs_full[j])] == srcs_full[j]).all() and not v[len(srcs_full[j]):].any()
+                for j, v in rec.items())
+        out.append(d)
+    with open(os.path.join(OUT, "window_cases.json"), "w") as f:
+        json.dump({"generated_by": "tests/golden/gen_golden.py window_cases (reference fec_recover in fork()ed "
+                                   "child, window-framework-shaped blocks)",
+                   "data": "sources = synth_bytes(k*L, data_seed) reshaped [k][L], truncated to src_len when given; "
+                           "repairs = reference encode of block number 0 (per repair: of block number "
+                           "repair_fpid_raw >> 8 & 0xffffff when mixed_seeds)",
+                   "cases": out}, f)
+    print(f"window cases {len(out)} ({sum(c['crashed'] for c in out)} reference crashes, "
+          f"{sum(bool(c['recovered']) for c in out)} with recoveries)")
 
 
 if __name__ == "__main__":

@@ -155,12 +155,15 @@ long mh_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
 }
 
 /* Receiver side: a block with the given sources / repairs present -> fec_recover.
- * recovered[j] = 1 for every source inserted by the operation; its bytes and length in
- * out[j * stride] / out_len[j]; *cur_ss = current_source_symbols afterwards. */
+ * recovered[j] = 1 for every source inserted by the operation; its bytes, length and source FPID in
+ * out[j * stride] / out_len[j] / out_fpid[j] (out_fpid may be NULL); *cur_ss =
+ * current_source_symbols afterwards.  fbn is the block's own number: the block framework's block
+ * number, or the window framework's first source id (window_framework_receiver.h:60-86); repair
+ * FPIDs are taken as given (rep_fpid). */
 long mh_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
                 const uint8_t *src_present, int src_stride, const uint8_t *rep, const uint16_t *rep_len,
                 const uint8_t *rep_present, const uint64_t *rep_fpid, int rep_stride, uint8_t *out,
-                uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss) {
+                uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss, uint32_t *out_fpid) {
     picoquic_cnx_t cnx;
     protoop_arg_t schemes[2] = {0, 0};
     protoop_arg_t ret = run_protoop(&cnx, op_create(xor_scheme), 0, NULL, schemes);
@@ -193,12 +196,60 @@ long mh_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, 
         pquic_source_symbol_t *ss = fb->source_symbols[j];
         recovered[j] = ss && ss != before[j];
         out_len[j] = recovered[j] ? ss->data_length : 0;
+        if (out_fpid) out_fpid[j] = recovered[j] ? ss->fpid.raw : 0;
         if (recovered[j]) memcpy(out + (size_t)j * out_stride, ss->data, ss->data_length);
     }
     *cur_ss = fb->current_source_symbols;
     if (schemes[0] && !xor_scheme) mh_free(&cnx, (void *)(uintptr_t)schemes[0]);
     free_block(fb);
     return (long)ret;
+}
+
+/* A block whose totals exceed its 100 symbol slots (nss / nrs are u8 fields the peer sets,
+ * block_framework_receiver.h:44-45): only the first 100 slots are populated.  Runs generate
+ * (op 0) or recover (op 1) and returns the operation's value; the adapter must refuse the block
+ * before touching the device (the reference reads past fec_block_t here). */
+long mh_oversized(int xor_scheme, int op, int k_total, int r_total) {
+    picoquic_cnx_t cnx;
+    protoop_arg_t schemes[2] = {0, 0};
+    protoop_arg_t ret = run_protoop(&cnx, op_create(xor_scheme), 0, NULL, schemes);
+    if (ret) return (long)ret;
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    uint8_t data[64];
+    memset(data, 7, sizeof data);
+    fb->fec_block_number = 9;
+    fb->total_source_symbols = (uint8_t)k_total;
+    fb->total_repair_symbols = (uint8_t)r_total;
+    const int ns = op ? 90 : (k_total < PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK ? k_total : PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK);
+    for (int j = 0; j < ns; j++) fb->source_symbols[j] = mk_source(9, j, data, sizeof data);
+    fb->current_source_symbols = (uint8_t)k_total;
+    if (op) {  /* counters that pass the reference's preconditions, so only the slot guard stops it */
+        fb->current_source_symbols = (uint8_t)(k_total - (r_total < 10 ? r_total : 10));
+        for (int i = 0; i < 10 && i < r_total; i++) {
+            pquic_repair_symbol_t *rs = mh_malloc(&cnx, sizeof *rs);
+            memset(rs, 0, sizeof *rs);
+            rs->fpid.raw = (9u << 8) | (uint32_t)i;
+            rs->data = mh_malloc(&cnx, sizeof data);
+            memcpy(rs->data, data, sizeof data);
+            rs->data_length = sizeof data;
+            fb->repair_symbols[i] = rs;
+            fb->current_repair_symbols++;
+        }
+    }
+    protoop_arg_t in[2] = {(protoop_arg_t)(uintptr_t)fb, schemes[op ? 0 : 1]};
+    op_t f = op ? (xor_scheme ? pquic_fec_xor_recover : pquic_fec_rlc_recover)
+                : (xor_scheme ? pquic_fec_xor_generate_repair_symbols : pquic_fec_rlc_generate_repair_symbols);
+    ret = run_protoop(&cnx, f, 2, in, NULL);
+    if (schemes[0] && !xor_scheme) mh_free(&cnx, (void *)(uintptr_t)schemes[0]);
+    free_block(fb);
+    return (long)ret;
+}
+
+void mh_protoop_stats(uint64_t out[5]) {
+    pquic_fec_protoop_stats_t s;
+    pquic_fec_protoop_stats(&s);
+    out[0] = s.generate_calls; out[1] = s.recover_calls; out[2] = s.recovered_symbols;
+    out[3] = s.ref_ub_blocks; out[4] = s.errors;
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -319,12 +370,14 @@ void mh_batch_repairs(long t, uint8_t *rep_out, uint16_t *rep_len, uint64_t *rep
 }
 
 /* recover result: inserted sources of ticket t (as mh_recover reports them) */
-void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss) {
+void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recovered, int out_stride, int *cur_ss,
+                        uint32_t *out_fpid) {
     ticket_t *tk = &g_tickets[t];
     for (int j = 0; j < tk->k; j++) {
         pquic_source_symbol_t *ss = tk->fb->source_symbols[j];
         recovered[j] = ss && ss != tk->before[j];
         out_len[j] = recovered[j] ? ss->data_length : 0;
+        if (out_fpid) out_fpid[j] = recovered[j] ? ss->fpid.raw : 0;
         if (recovered[j]) memcpy(out + (size_t)j * out_stride, ss->data, ss->data_length);
     }
     *cur_ss = tk->fb->current_source_symbols;

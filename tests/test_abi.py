@@ -104,3 +104,23 @@ def test_integration_stub_compiles_against_picoquic(tmp_path):
                         f"-I{os.path.join(ROOT, 'include')}", os.path.join(ROOT, "tests", "host", "integration_stub.c"),
                         "-o", str(tmp_path / "stub.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_oversized_block_rejected_without_device_call():
+    """Totals above the block's 100 symbol slots (nss / nrs come from the peer,
+    block_framework_receiver.h:44-45) are refused before any engine call -- the reference reads
+    past fec_block_t there.  Runs on any host: a refused block never reaches the device, so the
+    operation counters do not move while the error counter does."""
+    import numpy as np
+    mh = C.CDLL(MINIHOST)
+    mh.mh_oversized.restype = C.c_long
+    assert mh.mh_bind(0) == 0
+    st0 = np.zeros(5, np.uint64)
+    mh.mh_protoop_stats(st0.ctypes.data_as(C.POINTER(C.c_uint64)))
+    for xor, op, kt, rt in [(0, 0, 150, 4), (0, 0, 16, 120), (0, 1, 150, 20), (0, 1, 100, 101), (1, 1, 150, 1),
+                            (1, 0, 150, 1)]:
+        assert mh.mh_oversized(xor, op, kt, rt) == 0x41B
+    st1 = np.zeros(5, np.uint64)
+    mh.mh_protoop_stats(st1.ctypes.data_as(C.POINTER(C.c_uint64)))
+    assert st1[0] == st0[0] and st1[1] == st0[1]
+    assert st1[4] == st0[4] + 6

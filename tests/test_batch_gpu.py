@@ -10,7 +10,7 @@ import time
 import numpy as np
 import pytest
 
-from golden_io import decode_sources, encode_inputs, load, load_npz, sha
+from golden_io import decode_sources, encode_inputs, load, load_npz, sha, window_inputs
 from oracle_py import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -34,7 +34,8 @@ class Batch:
                                        C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]
         L.mh_batch_status.argtypes = [C.c_long, C.POINTER(C.c_int)]
         L.mh_batch_repairs.argtypes = [C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
-        L.mh_batch_recovered.argtypes = [C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.mh_batch_recovered.argtypes = [C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int),
+                                         C.c_void_p]
         L.mh_batch_poll.argtypes = [C.c_uint64]
         self.L = L
         assert L.mh_bind(0) == 0
@@ -101,7 +102,10 @@ class Batch:
         ol = np.zeros(k, np.uint16)
         rec = np.zeros(k, np.uint8)
         cur = C.c_int(0)
-        self.L.mh_batch_recovered(t, out.ctypes.data, ol.ctypes.data, rec.ctypes.data, stride, C.byref(cur))
+        ofp = np.zeros(k, np.uint32)
+        self.L.mh_batch_recovered(t, out.ctypes.data, ol.ctypes.data, rec.ctypes.data, stride, C.byref(cur),
+                                  ofp.ctypes.data)
+        self.last_fpids = {j: int(ofp[j]) for j in range(k) if rec[j]}
         return {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}, cur.value
 
     def stats(self):
@@ -262,4 +266,38 @@ def test_batch_mixed_keys_and_symbol_cap():
         pad = [np.pad(s, (0, L - len(s))) for s in srcs]
         want = [o.xor_encode_block(pad)[1]] if xor else o.rlc_encode_block(fbn, pad, r)[1]
         assert all(a.tobytes() == b.tobytes() for a, b in zip(reps, want))
+    bt.close()
+
+
+@pytest.mark.parametrize("batch_blocks", [4, 64])
+def test_batch_recover_window_framework_blocks(batch_blocks):
+    """The batcher on window-framework-shaped blocks (window_cases.json): block numbered by its
+    window start, repairs seeded by their own FPIDs (block number 0, or mixed), mixed in one
+    queue with block-framework blocks of the same (k, r)."""
+    bt = Batch(batch_blocks)
+    o = Oracle()
+    d = load("window_cases.json")
+    jobs = []
+    for i, case in enumerate(d["cases"]):
+        srcs_full, reps_full, fpids = window_inputs(case, o)
+        k, r = case["k"], case["r"]
+        srcs = [None if j in case["src_missing"] else srcs_full[j] for j in range(k)]
+        reps = [reps_full[i2] if i2 in case["rep_present"] else None for i2 in range(r)]
+        jobs.append((case, srcs, bt.recover(case["scheme"] == "xor", case["fbn"], srcs, reps, fpids, now=i)))
+    bt.L.mh_batch_drain()
+    n = 0
+    for case, srcs, t in jobs:
+        ret, calls = bt.status(t)
+        assert calls == 1, case["tag"]
+        rec, cur = bt.recovered(t)
+        if case["crashed"]:
+            assert ret == 0 and rec == {}
+            continue
+        assert ret == case["ret"], case["tag"]
+        assert {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())} == case["recovered"], case["tag"]
+        assert {str(j): f for j, f in bt.last_fpids.items()} == case["recovered_fpid"], case["tag"]
+        present = sum(s is not None for s in srcs)
+        assert cur == (present + len(rec) if case["scheme"] == "rlc" else present)
+        n += 1
+    assert n > 150
     bt.close()

@@ -239,12 +239,16 @@ def test_decode_zero_symbol_propagation(eng, oracle):
             assert np.array_equal(got[b, j], src_h[b, j])
 
 
-@pytest.mark.parametrize("knob", [None, "FECGPU_XOR_GENERIC", "FECGPU_XOR_IDX64"])
-def test_xor_vs_oracle(eng, oracle, knob, monkeypatch):
+@pytest.mark.parametrize("knob", [None, "xor_generic", "xor_idx64"])
+def test_xor_vs_oracle(eng, oracle, knob):
     """XOR encode/recover vs the oracle: the k-specialised kernels (k = 2..8, 16; 16-B and 4-B
     pieces), the runtime-k kernel, and the 64-bit-index instantiations."""
-    if knob:
-        monkeypatch.setenv(knob, "1")
+    import contextlib
+    with eng.knob(knob, 1) if knob else contextlib.nullcontext():
+        _xor_vs_oracle(eng, oracle)
+
+
+def _xor_vs_oracle(eng, oracle):
     rng = np.random.default_rng(9)
     for k, L, nb in [(4, 1200, 1000), (1, 4, 10), (7, 36, 300), (100, 64, 20), (128, 16, 9), (2, 1216, 50),
                      (3, 48, 70), (5, 1200, 40), (6, 20, 33), (8, 36, 64), (16, 1200, 30), (16, 4, 17)]:
@@ -399,6 +403,67 @@ def test_window_decode_vs_oracle(eng, oracle):
     assert (st == DEC_RECOVERED).sum() > nw // 2
 
 
+@pytest.mark.parametrize("k,r,L,nb,plan", [(16, 4, 1200, 300, 0), (30, 5, 1200, 200, 0), (32, 8, 1204, 120, 0),
+                                            (64, 16, 9000, 6, 0), (40, 20, 100, 60, 0), (100, 30, 64, 12, 0),
+                                            (16, 8, 256, 100, 1), (16, 8, 256, 100, 2)])
+def test_decode_seeded_vs_oracle(eng, oracle, k, r, L, nb, plan):
+    """fecgpu_rlc_decode_seeded: each repair's coefficients come from its own FPID
+    (rlc_fec_scheme_gf256.c:200) -- window style (0 << 8) | i, mixed block numbers per repair, and
+    arbitrary 32-bit FPIDs whose symbol number is not the slot -- against the oracle's per-block
+    decode with the same seeds, on every plan kernel the size selects (plan 1 / 2 force the wave and
+    LDS-lane plans)."""
+    rng = np.random.default_rng(k * 7 + r)
+    src_h = synth_bytes(nb * k * L, 500 + k).reshape(nb, k, L)
+    seeds = np.zeros((nb, r), np.uint32)
+    for b in range(nb):
+        style = b % 3
+        for i in range(r):
+            seeds[b, i] = (i if style == 0 else ((int(rng.integers(0, 1 << 24)) << 8) | i) if style == 1
+                           else int(rng.integers(0, 1 << 32)))
+    mul, _ = oracle.gf_tables()
+    rep_h = np.zeros((nb, r, L), np.uint8)
+    for b in range(nb):
+        for i in range(r):
+            c = oracle.coefs(int(seeds[b, i]), k)
+            acc = np.zeros(L, np.uint8)
+            for j in range(k):
+                acc ^= mul[c[j]][src_h[b, j]]
+            rep_h[b, i] = acc
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        e = int(rng.integers(0, min(k, r) + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        nrep = int(rng.integers(max(0, e - 1), r + 1))
+        rp[b] = masks_from_lists(1, r, [rng.choice(r, nrep, replace=False).tolist()])[0]
+    work = src_h.copy()
+    for b in range(nb):
+        for j in range(k):
+            if j not in bits(sp[b], k):
+                work[b, j] = 0xA5
+    w = to_dev(work)
+    st = torch.full((nb,), 0xEE, dtype=torch.uint8, device=DEV)
+    rec = torch.full((nb, 2), -1, dtype=torch.int64, device=DEV)
+    with eng.knob("plan", plan):
+        eng.rlc_decode_seeded(w, to_dev(rep_h), torch.from_numpy(seeds.view(np.int32)).to(DEV), to_dev(sp),
+                              to_dev(rp), st, rec, k, r, L)
+        torch.cuda.synchronize()
+    got, st_h, rec_h = w.cpu().numpy(), st.cpu().numpy(), rec.cpu().numpy().view(np.uint64)
+    n_rec = 0
+    for b in range(nb):
+        srcs = [src_h[b, j] if j in bits(sp[b], k) else None for j in range(k)]
+        reps = [rep_h[b, i] if i in bits(rp[b], r) else None for i in range(r)]
+        want_st, want = oracle.rlc_decode_block(0, srcs, reps, seeds[b])
+        assert st_h[b] == want_st, b
+        assert bits(rec_h[b], k) == sorted(want), b
+        for j, v in want.items():
+            assert np.array_equal(got[b, j], v), (b, j)
+            assert np.array_equal(v, src_h[b, j])
+        n_rec += len(want)
+    assert n_rec > 0
+
+
 def _ws_fields(ws, k, r, n_blocks):
     """Meaningful fields of each decode-plan record (unwritten bytes are scratch)."""
     em = min(k, r)
@@ -432,7 +497,6 @@ def test_plan_kernels_agree(eng, k, r, nb):
     wave-per-block) write identical decode records -- same unknowns, repair selection, solution
     rows D, dependency flags, and the same reference-crash verdicts -- on random erasure
     patterns.  Kernels whose size limits exclude (k, r) are skipped."""
-    import os
     rng = np.random.default_rng(k * 1000 + r)
     sp = np.zeros((nb, 2), np.uint64)
     rp = np.zeros((nb, 2), np.uint64)
@@ -445,23 +509,17 @@ def test_plan_kernels_agree(eng, k, r, nb):
     fbn = torch.from_numpy(rng.integers(0, 1 << 24, nb, dtype=np.int64).astype(np.int32)).to(DEV)
     spd, rpd = to_dev(sp), to_dev(rp)
     res = {}
-    old = os.environ.get("FECGPU_PLAN")
-    try:
-        em = min(k, r)
-        kinds = [x for x, ok in (("reg", k <= 32 and em <= 8), ("tile", k <= 64 and em <= 16), ("lane", True),
-                                 ("wave", True)) if ok]
-        for kind in kinds:
-            os.environ["FECGPU_PLAN"] = kind
+    em = min(k, r)
+    kinds = [x for x, ok in (("reg", k <= 32 and em <= 8), ("tile", k <= 64 and em <= 16), ("lane", True),
+                             ("wave", True)) if ok]
+    plan_id = {"wave": 1, "lane": 2, "reg": 3, "tile": 4}
+    for kind in kinds:
+        with eng.knob("plan", plan_id[kind]):
             ws = eng.alloc_workspace(nb, k, r)
             ws.fill_(0xEE)
             eng.rlc_decode_plan(spd, rpd, k, r, nb, ws, fbn=fbn)
             torch.cuda.synchronize()
             res[kind] = _ws_fields(ws.cpu().numpy(), k, r, nb)
-    finally:
-        if old is None:
-            os.environ.pop("FECGPU_PLAN", None)
-        else:
-            os.environ["FECGPU_PLAN"] = old
     first = res[kinds[0]]
     for kind in kinds[1:]:
         assert res[kind] == first, kind
@@ -623,14 +681,11 @@ def test_roundtrip_k32_e8(eng, oracle):
 
 @pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 300), (32, 8, 1200, 100), (7, 5, 2052, 60), (64, 16, 9000, 6)])
 def test_perm_datapath_vs_oracle(eng, oracle, k, r, L, nb):
-    """The v_perm data path (FECGPU_DATAPATH=perm, kept for A/B against the bitsliced one) gives
+    """The v_perm data path (knob datapath_perm, kept for A/B against the bitsliced one) gives
     the same encode and decode bytes as the oracle."""
-    import os
     rng = np.random.default_rng(k + 7 * r)
     src_h = synth_bytes(nb * k * L, 3 + k).reshape(nb, k, L)
-    old = os.environ.get("FECGPU_DATAPATH")
-    os.environ["FECGPU_DATAPATH"] = "perm"
-    try:
+    with eng.knob("datapath_perm", 1):
         src = to_dev(src_h)
         rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
         eng.rlc_encode(src, rep, k, r, L, fbn_base=41)
@@ -645,11 +700,6 @@ def test_perm_datapath_vs_oracle(eng, oracle, k, r, L, nb):
             sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
             rp[b] = masks_from_lists(1, r, [list(range(r))])[0]
         work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=41)
-    finally:
-        if old is None:
-            os.environ.pop("FECGPU_DATAPATH", None)
-        else:
-            os.environ["FECGPU_DATAPATH"] = old
     ref = work.copy()
     st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, 41)
     assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)

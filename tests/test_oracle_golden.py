@@ -6,7 +6,7 @@ compiled natively (tests/golden/gen_golden.py); nothing here depends on a GPU.
 import numpy as np
 import pytest
 
-from golden_io import decode_sources, encode_inputs, load, load_npz, sha
+from golden_io import decode_sources, encode_inputs, load, load_npz, sha, window_inputs
 from oracle_py import DEC_NOTHING, DEC_RECOVERED, DEC_REF_UB, Oracle
 
 
@@ -169,3 +169,39 @@ def test_decode_batch_roundtrip(oracle):
     assert ok.sum() > nb * 0.9
     assert np.array_equal(work[ok], src[ok])
     assert ((st == DEC_RECOVERED) | (st == DEC_REF_UB)).all()
+
+
+def test_decode_window_framework_blocks(oracle):
+    """Window-framework-shaped blocks (window_cases.json): the block is numbered by its window
+    start, the repairs carry block number 0 (or mixed block numbers) and every equation is seeded
+    by its repair's own FPID (rlc_fec_scheme_gf256.c:200)."""
+    d = load("window_cases.json")
+    seen = set()
+    for case in d["cases"]:
+        srcs_full, reps_full, fpids = window_inputs(case, oracle)
+        k, r = case["k"], case["r"]
+        srcs = [None if j in case["src_missing"] else srcs_full[j] for j in range(k)]
+        reps = [reps_full[i] if i in case["rep_present"] else None for i in range(r)]
+        if case["scheme"] == "xor":
+            st, rec = oracle.xor_decode_block(srcs, reps)
+        else:
+            st, rec = oracle.rlc_decode_block(case["fbn"], srcs, reps, [f & 0xFFFFFFFF for f in fpids])
+        seen.add(st)
+        if case["crashed"]:
+            assert st == DEC_REF_UB, case["tag"]
+            continue
+        assert st != DEC_REF_UB, case["tag"]
+        assert {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())} == case["recovered"], case["tag"]
+        assert {str(j): len(v) for j, v in rec.items()} == case["recovered_len"], case["tag"]
+        fb = case["fbn"]
+        assert {str(j): ((fb << 8) + j) & 0xFFFFFFFF for j in rec} == case["recovered_fpid"], case["tag"]
+    assert DEC_RECOVERED in seen and DEC_REF_UB in seen
+    assert any(c["mixed_seeds"] and c["recovered"] for c in d["cases"])
+    # block-number seeds instead of the FPIDs would NOT reproduce the reference: the gap the
+    # adapter closes (seeding by (window start << 8) | i recovers wrong bytes)
+    case = next(c for c in d["cases"] if c["scheme"] == "rlc" and c["recovered"] and not c["crashed"])
+    srcs_full, reps_full, _ = window_inputs(case, oracle)
+    srcs = [None if j in case["src_missing"] else srcs_full[j] for j in range(case["k"])]
+    reps = [reps_full[i] if i in case["rep_present"] else None for i in range(case["r"])]
+    _, wrong = oracle.rlc_decode_block(case["fbn"], srcs, reps)
+    assert {str(j): sha(v.tobytes()) for j, v in sorted(wrong.items())} != case["recovered"]

@@ -1,5 +1,5 @@
-"""In-process A/B of runtime knobs (environment variables the engine reads per call), so every
-variant runs on the same buffers in the same process: alternates variants for several cycles and
+"""In-process A/B of engine knobs (fecgpu_set_knob; the FECGPU_* environment names are accepted
+and mapped to knob names), so every variant runs on the same buffers in the same process: alternates variants for several cycles and
 prints median kernel times.  Removes the process-to-process variance (buffer placement) that
 dominates whole-bench A/B runs.
 A variant may also name another build of the library: "name:LIB=pquic_amd/lib/variants/X/libpquic_fec.so"
@@ -29,7 +29,30 @@ for spec in args or ["base"]:
         elif piece and last:
             kvs[last] += "," + piece
     variants.append((name, kvs))
-knobs = sorted({k for _, e in variants for k in e if k != "LIB"})
+PLAN = {"wave": 1, "lane": 2, "reg": 3, "tile": 4}
+
+
+def to_knobs(env):
+    """{knob name: int} from a variant's VAR=VAL pairs (knob names or FECGPU_* environment names)."""
+    out = {}
+    for kk, vv in env.items():
+        if kk == "LIB":
+            continue
+        if kk == "FECGPU_ENC_TILE":
+            a, b = vv.split(",")
+            out["enc_tile_rt"], out["enc_tile_waves"] = int(a), int(b)
+        elif kk == "FECGPU_DATAPATH":
+            out["datapath_perm"] = int(vv == "perm")
+        elif kk == "FECGPU_PLAN":
+            out["plan"] = PLAN.get(vv, 0)
+        elif kk.startswith("FECGPU_"):
+            out[kk[len("FECGPU_"):].lower()] = int(vv)
+        else:
+            out[kk] = int(vv)
+    return out
+
+
+knobs = sorted({k for _, e in variants for k in to_knobs(e)})
 
 eng0 = Engine(0)
 engines = {name: (Engine(0, lib_path=e["LIB"]) if "LIB" in e else eng0) for name, e in variants}
@@ -88,14 +111,15 @@ def run(case, eng):
         eng.rlc_decode(src, rep, sp, rp, st, rec, k, r, L, workspace=ws)
 
 
+defaults = {(name, kn): engines[name].get_knob(kn) for name, _ in variants for kn in knobs}
 times = {(v[0], c[0]): [] for v in variants for c in cases}
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 for cyc in range(cycles):
     for name, env in variants:
-        for kn in knobs:
-            os.environ.pop(kn, None)
-        os.environ.update({kk: vv for kk, vv in env.items() if kk != "LIB"})
         e = engines[name]
+        want = to_knobs(env)
+        for kn in knobs:  # unset knobs return to their defaults
+            e.set_knob(kn, want.get(kn, defaults[(name, kn)]))
         for c in cases:
             run(c, e)  # warm
             ev[0].record()
