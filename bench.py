@@ -37,6 +37,9 @@ METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--config", choices=["k16", "k32r8", "k64r16"], default="k16",
+                   help="workload: k16 = the metric's configs[1]+[2] (default); k32r8 = configs[3] "
+                        "(2^24 blocks split over the GPUs); k64r16 = configs[4]")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=1 << 20, help="FEC blocks per GPU")
@@ -179,55 +182,92 @@ def xor_leg(torch, eng, dev, k, L, nb, reps=3):
             "decode_GB_s": round((k + 1) * L * nb / (td * 1e-3) / 1e9, 1)}
 
 
-def cpu_baseline(args, nthreads):
-    """The oracle (CPU restatement, bit-exact with the reference; kind "port") on a bounded
-    sample of the same workload, all threads of this process's CPU share."""
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, bounded by a cgroup CPU quota when one is set
+    (a GPU box shares its host: its affinity mask can list every CPU of the machine while the
+    quota grants a slice of them)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return cores, aff, quota
+
+
+def cpu_baseline(args, ncores):
+    """The reference's own plugins/fec scheme pluglets (rlc_fec_scheme_generate_gf256.c,
+    rlc_fec_scheme_gf256.c compiled natively from the reference sources into
+    oracle/_ref/libfecref.so; kind "reference") on every core of this process's CPU share, one
+    fork()ed worker per core, over a bounded sample of the same workload: RLC encode k=16 r=4 of
+    every block, then decode with 4 erasures.  The reference segfaults on ~1 % of erasure patterns
+    (SURVEY §8a A9); those blocks are screened out of its decode (untimed, by the CPU port) and the
+    value still counts their payload, so the reference number is, if anything, flattering.  The
+    port (oracle/fec_oracle.c, bit-exact) is timed beside it on as many threads; their ratio is
+    reported.  Runs before the process touches the GPU (the workers are forks)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes as C
     import numpy as np
     from oracle_py import Oracle, synth_bytes
     o = Oracle()
     k, r, L, e = args.k, args.r, args.symbol, args.erasures
-
-    def make(nb):
-        src = synth_bytes(nb * k * L, 0x5EEDF3C0).reshape(nb, k, L)
-        rng = np.random.default_rng(1)
-        sp = np.zeros((nb, 2), np.uint64)
-        rp = np.zeros((nb, 2), np.uint64)
-        full = (1 << k) - 1
-        for b in range(nb):
-            m = full
-            for j in rng.choice(k, e, replace=False):
-                m &= ~(1 << int(j))
-            sp[b, 0] = m
-            rp[b, 0] = (1 << r) - 1
-        return src, sp, rp
-
-    def run(src, sp, rp):
+    nb = 1 << 14  # 300 MiB of payload: larger than the host caches
+    src = synth_bytes(nb * k * L, 0x5EEDF3C0).reshape(nb, k, L)
+    rng = np.random.default_rng(1)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    full = (1 << k) - 1
+    for b in range(nb):
+        m = full
+        for j in rng.choice(k, e, replace=False):
+            m &= ~(1 << int(j))
+        sp[b, 0] = m
+        rp[b, 0] = (1 << r) - 1
+    # screen: which patterns the reference survives (the port flags its x[-1] crash exactly)
+    rep0 = o.rlc_encode_batch(src, r, 0, ncores)
+    st, _ = o.rlc_decode_batch(src.copy(), rep0, sp, rp, 0, ncores)
+    skip = (st == 2).astype(np.uint8)
+    del rep0
+    out = {"unit": "GiB/s", "cores": ncores, "kind": "reference"}
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
+    gib_pass = nb * k * L / 2**30
+    if os.path.exists(ref_path):
+        lib = C.CDLL(ref_path)
+        lib.ref_cpu_baseline.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_uint32,
+                                         C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+        res = (C.c_double * 3)()
+        assert lib.ref_cpu_baseline(ncores, src.ctypes.data, nb, k, r, L, 0, sp.ctypes.data, skip.ctypes.data, 1,
+                                    res) == 0, "reference CPU workers failed"
+        passes = max(1, min(200, int(round(args.cpu_seconds / max(res[0], 1e-3)))))
+        assert lib.ref_cpu_baseline(ncores, src.ctypes.data, nb, k, r, L, 0, sp.ctypes.data, skip.ctypes.data,
+                                    passes, res) == 0, "reference CPU workers failed"
+        out["value"] = round(passes * gib_pass / res[0], 4)
+        out["sample"] = (f"{passes} passes x {nb} blocks, k={k} r={r} L={L}: the reference's RLC encode + decode "
+                         f"pluglets (native gcc -O2), {ncores} fork()ed workers, {res[0]:.1f} s wall; "
+                         f"{int(skip.sum())} of {nb} erasure patterns crash the reference and are not decoded")
+    else:  # the reference build is absent: the port stands in (and says so)
+        out["kind"] = "port"
+    # the port on the same sample and thread count (second number, and its ratio to the reference)
+    passes_p, t_total = 0, 0.0
+    while t_total < args.cpu_seconds / 2 and passes_p < 1000:
         work = src.copy()
         t0 = time.perf_counter()
-        rep = o.rlc_encode_batch(work, r, 0, nthreads)
-        o.rlc_decode_batch(work, rep, sp, rp, 0, nthreads)
-        return time.perf_counter() - t0
-
-    # bounded sample: 2^14 blocks (300 MiB of payload), re-run until ~cpu_seconds of CPU work
-    nb = 1 << 14
-    src, sp, rp = make(nb)
-    passes, t_total = 0, 0.0
-    while t_total < args.cpu_seconds and passes < 1000:
-        t_total += run(src, sp, rp)
-        passes += 1
-    gib = passes * nb * k * L / 2**30
-    out = {"value": gib / t_total, "unit": "GiB/s", "cores": nthreads, "kind": "port",
-           "sample": f"{passes} passes x {nb} blocks, k={k} r={r} L={L}: RLC encode + decode with {e} "
-                     f"erasures, oracle/fec_oracle.c -O2, {nthreads} pthreads, {t_total:.1f} s"}
-    ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
-    if os.path.exists(ref_path):  # the reference's own encode pluglet, 1 core (calibration)
-        from oracle_py import Reference
-        R = Reference(ref_path)
-        s1 = src[:1024].copy()
-        t0 = time.perf_counter()
-        R.rlc_encode_batch(s1, r, 0)
-        out["reference_encode_1core_GiB_s"] = round(1024 * k * L / 2**30 / (time.perf_counter() - t0), 4)
+        rep = o.rlc_encode_batch(work, r, 0, ncores)
+        o.rlc_decode_batch(work, rep, sp, rp, 0, ncores)
+        t_total += time.perf_counter() - t0
+        passes_p += 1
+    port = round(passes_p * gib_pass / t_total, 4)
+    out["port"] = {"value": port, "threads": ncores,
+                   "sample": f"{passes_p} passes x {nb} blocks, oracle/fec_oracle.c -O2, {t_total:.1f} s"}
+    if "value" in out:
+        out["port"]["port_over_reference"] = round(port / out["value"], 3)
+    else:
+        out["value"] = port
+        out["sample"] = out["port"]["sample"]
     return out
 
 
@@ -294,6 +334,69 @@ def batching_legs(dev_index, args):
     return legs
 
 
+def hook_latency_legs(dev_index):
+    """Latency of the synchronous drop-in hooks (one block per call, the way the block framework
+    calls fec_generate_repair_symbols / fec_recover; tools/batch_load.c bl_hook_latency) at k16 r4
+    L1200 with 4 erasures, next to the reference pluglets' own time per block on one core of this
+    box (oracle/_ref/libfecref.so, in process)."""
+    import ctypes as C
+    path = os.path.join(ROOT, "tools", "libbatchload.so")
+    if not os.path.exists(path):
+        return {}
+    lib = C.CDLL(path)
+    lib.bl_hook_latency.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.POINTER(C.c_double)]
+    out = (C.c_double * 7)()
+    rc = lib.bl_hook_latency(dev_index, 16, 4, 1200, 4, 2000, out)
+    if rc:
+        return {"sync_hook_k16_r4": {"error": rc}}
+    leg = {"k": 16, "r": 4, "L": 1200, "erasures": 4, "calls": 2000,
+           "generate_us_p50": out[0], "generate_us_p99": out[1], "generate_us_mean": round(out[2], 1),
+           "recover_us_p50": out[3], "recover_us_p99": out[4], "recover_us_mean": round(out[5], 1),
+           "recovered_per_call": out[6]}
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
+    if os.path.exists(ref_path):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+        from oracle_py import Oracle, synth_bytes
+        nb, k, r, L = 2000, 16, 4, 1200
+        src = synth_bytes(nb * k * L, 7).reshape(nb, k, L)
+        sp = np.zeros((nb, 2), np.uint64)
+        for b in range(nb):
+            first = b % (k - 3)
+            sp[b, 0] = ((1 << k) - 1) & ~(0xF << first)
+        rp = np.zeros((nb, 2), np.uint64)
+        rp[:, 0] = (1 << r) - 1
+        o = Oracle()
+        st, _ = o.rlc_decode_batch(src.copy(), o.rlc_encode_batch(src, r, 0, 1), sp, rp, 0, 1)
+        skip = (st == 2).astype(np.uint8)
+        rl = C.CDLL(ref_path)
+        rl.ref_work_serial.restype = C.c_long
+        rl.ref_work_serial.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_void_p,
+                                       C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        te, td = C.c_double(0), C.c_double(0)
+        nd = rl.ref_work_serial(src.ctypes.data, nb, k, r, L, 0, sp.ctypes.data, skip.ctypes.data, C.byref(te),
+                                C.byref(td))
+        if nd > 0:
+            leg["reference_pluglet_us_per_block_1core"] = {"generate": round(te.value / nb * 1e6, 1),
+                                                           "recover": round(td.value / nd * 1e6, 1)}
+    return {"sync_hook_k16_r4": leg}
+
+
+# Workloads (BASELINE.json configs).  The default is the metric's own configuration (configs[1] +
+# configs[2]: k16 r4 encode then 4-erasure decode, 2^20 blocks per GPU).  The others are the
+# configs that name 8 GPUs, for multi-GPU runs: configs[3] (k32 r8 encode, 2^24 blocks sharded over
+# the GPUs, strong scaling) and configs[4] (k64 r16 L9000 encode + 16-erasure decode, 2^16 blocks
+# per GPU).
+CONFIGS = {
+    "k16": {"k": 16, "r": 4, "e": 4, "L": 1200, "per_rank": 1 << 20, "scaling": "weak",
+            "workload": "RLC-GF(256) encode k=16 r=4 + decode 4 erasures, 1200B symbols (configs[1]+[2])"},
+    "k32r8": {"k": 32, "r": 8, "e": 0, "L": 1200, "total": 1 << 24, "resident": 1 << 21, "scaling": "strong",
+              "workload": "RLC-GF(256) encode k=32 r=8, 1200B symbols, 2^24 blocks split over the GPUs (configs[3])"},
+    "k64r16": {"k": 64, "r": 16, "e": 16, "L": 9000, "per_rank": 1 << 16, "scaling": "weak",
+               "workload": "RLC-GF(256) encode k=64 r=16 + decode 16 erasures, 9000B symbols (configs[4])"},
+}
+
+
 def main():
     args = parse()
     import torch
@@ -313,97 +416,138 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
+    cfg = dict(CONFIGS[args.config])
+    if args.config == "k16":  # the legacy flags still shape the default workload
+        cfg.update(k=args.k, r=args.r, e=args.erasures, L=args.symbol, per_rank=args.blocks)
+    k, r, e, L = cfg["k"], cfg["r"], cfg["e"], cfg["L"]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == "k16":
+        # before any HIP call: the reference's workers are fork()ed from this process
+        ncores, aff, quota = host_cpu_share()
+        cpu = cpu_baseline(args, ncores)
+        cpu["host"] = {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     eng = Engine(local)
 
-    from pquic_amd.shard import fbn_base_of, weak_range
-    nb, k, r, L, e = args.blocks, args.k, args.r, args.symbol, args.erasures
-    g0, _ = weak_range(nb, rank)  # this rank's global block range (weak scaling)
-    fbn_base = fbn_base_of(g0)
+    from pquic_amd.shard import fbn_base_of, shard_range, weak_range
+    if cfg["scaling"] == "weak":
+        g0, g1 = weak_range(cfg["per_rank"], rank)  # this rank's global block range
+    else:
+        g0, g1 = shard_range(cfg["total"], world, rank)
+    share = g1 - g0                                  # blocks this rank codes per step
+    nb = min(share, cfg.get("resident", share))      # blocks resident in HBM
+    passes = (share + nb - 1) // nb if nb else 0     # a share larger than HBM runs in passes
     src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
     eng.synth_fill(src, src.numel(), 0x5EEDF3C0, g0 * k * L)
     rep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
-    work = torch.empty_like(src)
-    sp, miss = make_erasures(torch, nb, k, e, 11 + rank, dev)
-    rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
-    rp[:, 0] = (1 << r) - 1
-    status = torch.empty(nb, dtype=torch.uint8, device=dev)
-    recovered = torch.empty((nb, 2), dtype=torch.int64, device=dev)
-    ws = eng.alloc_workspace(nb, k, r)
-    # decode input: the received block (erased slots hold stale bytes), copied once.  The recovered
-    # symbols go to their own buffer -- the reference's fec_recover allocates new source symbols
-    # rather than writing into the received block (rlc_fec_scheme_gf256.c:218-236) -- which also
-    # keeps the writes out of the rows being read (in place measured 5 % slower,
-    # profiles/r01_ab_apply_to.log)
-    work.copy_(src)
-    idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
-    work.view(nb * k, L)[idx] = 0xA5
-    rec_rows = torch.empty_like(src)
+    if e:
+        work = torch.empty_like(src)
+        sp, miss = make_erasures(torch, nb, k, e, 11 + rank, dev)
+        rp = torch.zeros((nb, 2), dtype=torch.int64, device=dev)
+        rp[:, 0] = (1 << r) - 1 if r < 64 else -1
+        status = torch.empty(nb, dtype=torch.uint8, device=dev)
+        recovered = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+        ws = eng.alloc_workspace(nb, k, r)
+        # decode input: the received block (erased slots hold stale bytes), copied once.  The recovered
+        # symbols go to their own buffer -- the reference's fec_recover allocates new source symbols
+        # rather than writing into the received block (rlc_fec_scheme_gf256.c:218-236) -- which also
+        # keeps the writes out of the rows being read (in place measured 5 % slower,
+        # profiles/r01_ab_apply_to.log)
+        work.copy_(src)
+        idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
+        work.view(nb * k, L)[idx] = 0xA5
+        rec_rows = torch.empty_like(src)
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        eng.rlc_encode(src, rep, k, r, L, fbn_base=fbn_base)
-        eng.rlc_decode_stages(work, rep, sp, rp, status, recovered, k, r, L, nb, ws, fbn_base=fbn_base,
-                              events=ev[1:] if ev else None, dst=rec_rows)
+        for p in range(passes):
+            m = min(nb, share - p * nb)
+            fb = fbn_base_of(g0 + p * nb)
+            if ev and p == 0:
+                ev[0].record(stream)
+            eng.rlc_encode(src, rep, k, r, L, nblocks=m, fbn_base=fb)
+            if e:
+                eng.rlc_decode_stages(work, rep, sp, rp, status, recovered, k, r, L, m, ws, fbn_base=fb,
+                                      events=ev[1:] if ev and p == 0 else None, dst=rec_rows)
+            elif ev and p == 0:
+                ev[1].record(stream)
+                ev[2].record(stream)
+                ev[3].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness gate on the benchmarked data: every recovered block's erased rows equal the originals
-    ok = status == 0
-    check_recovered(torch, rec_rows, src, ok, miss, nb, k, L, "decode did not restore the sources")
-    n_rec = int(ok.sum())
-    n_ub = int((status == 2).sum())
+    n_rec = n_ub = 0
+    if e:  # correctness gate on the benchmarked data: every recovered block's erased rows equal the originals
+        ok = status == 0
+        if passes == 1:
+            check_recovered(torch, rec_rows, src, ok, miss, nb, k, L, "decode did not restore the sources")
+        n_rec = int(ok.sum())
+        n_ub = int((status == 2).sum())
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(evs[s])
+    for s_ in range(args.steps):
+        step(evs[s_])
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     seg = [sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / args.steps for i in range(3)]
-    enc_ms, plan_ms, apply_ms = seg  # apply includes the zero/undetermined rule (fused for e <= 16)
+    enc_ms, plan_ms, apply_ms = seg  # first pass of a step; apply includes the zero/undetermined rule
     dec_ms = plan_ms + apply_ms
+    per_rank = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        tr = torch.tensor([t_rank], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        allr = [torch.zeros_like(tr) for _ in range(world)]
+        dist.all_gather(allr, tr)
+        per_rank = [round(float(x.item()) / args.steps * 1e3, 3) for x in allr]
 
-    payload = nb * k * L  # per GPU per step
-    value = world * payload * args.steps / elapsed / 2**30
+    total_blocks = world * share if cfg["scaling"] == "weak" else cfg["total"]
+    value = total_blocks * k * L * args.steps / elapsed / 2**30
+    payload = nb * k * L  # resident blocks (one pass)
     enc_bytes = (k + r) * L * nb                 # read k sources, write r repairs per block
     app_bytes = (k + e) * L * n_rec              # read k received symbols, write e per recovered block
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
-    app_gbs = app_bytes / (apply_ms * 1e-3) / 1e9
-
+    app_gbs = app_bytes / (apply_ms * 1e-3) / 1e9 if e else 0.0
+    tag = f"k{k}_r{r}" + ("" if L == 1200 else f"_L{L}")
+    rt = 16 if r >= 16 else 8 if r >= 8 else 4 if r >= 4 else 2 if r >= 2 else 1
+    vec = 16 if L >= 16 else 8 if L % 8 == 0 else 4
+    ert = 16 if min(k, r) > 8 else 8 if min(k, r) > 4 else 4 if min(k, r) > 2 else min(k, r)
     legs = {
-        "rlc_encode_k16_r4": {"kernel": "k_rlc_encode_bs<4,16>", "ms": round(enc_ms, 3),
+        f"rlc_encode_{tag}": {"kernel": f"k_rlc_encode_bs<{rt},{vec}>", "ms": round(enc_ms, 3), "blocks": nb,
                               "payload_GiB_s": round(payload / (enc_ms * 1e-3) / 2**30, 2),
                               "algorithmic_GB_s": round(enc_gbs, 1), "hbm_frac": round(enc_gbs / HBM_PEAK_GBS, 4),
-                              "bytes_per_launch": enc_bytes, "traffic": load_traffic("rlc_encode_k16_r4", nb)},
-        "rlc_decode_k16_e4": {"ms": round(dec_ms, 3), "plan_ms": round(plan_ms, 3), "apply_ms": round(apply_ms, 3),
-                              "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
-                              "apply_kernel": "k_rlc_recover_bs<4,16>", "apply_algorithmic_GB_s": round(app_gbs, 1),
-                              "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
-                              "ref_ub_blocks": n_ub, "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)},
+                              "bytes_per_launch": enc_bytes, "traffic": load_traffic(f"rlc_encode_{tag}", nb)},
     }
-    del work, ws, rec_rows
-    if not args.no_legs and not args.no_pcie and world == 1:
+    if e:
+        legs[f"rlc_decode_k{k}_e{e}"] = {
+            "ms": round(dec_ms, 3), "plan_ms": round(plan_ms, 3), "apply_ms": round(apply_ms, 3),
+            "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
+            "apply_kernel": f"k_rlc_recover_bs<{ert},{vec}>", "apply_algorithmic_GB_s": round(app_gbs, 1),
+            "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
+            "ref_ub_blocks": n_ub, "traffic": load_traffic(f"rlc_decode_apply_k{k}_e{e}", nb)}
+    if e:
+        del work, ws, rec_rows
+    default = args.config == "k16" and (k, r, e, L) == (16, 4, 4, 1200)
+    if default and not args.no_legs and not args.no_pcie and world == 1:
         legs.update(pcie_legs(torch, args, dev))
         legs.update(batching_legs(dev.index or 0, args))
-    if not args.no_legs and world == 1:
+        legs.update(hook_latency_legs(dev.index or 0))
+    if default and not args.no_legs and world == 1:
         # §8f row 2: the repair symbols of the whole batch as FEC frames (header + payload) on the device
         fstride = (14 + L + 15) // 16 * 16
         frames = torch.empty(nb * r * fstride, dtype=torch.uint8, device=dev)
+        fbn_base = fbn_base_of(g0)
         eng.write_repair_frames(rep, frames, nb, r, L, L, fstride, k, r, fbn_base=fbn_base)
         a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
@@ -416,7 +560,7 @@ def main():
         legs["repair_frames_k16_r4"] = {"kernel": "k_write_repair_frames16", "frames": nb * r, "frame_stride": fstride,
                                         "ms": round(ms, 3), "algorithmic_GB_s": round(fb / (ms * 1e-3) / 1e9, 1)}
         del frames
-    if not args.no_legs and world == 1:
+    if default and not args.no_legs and world == 1:
         # north-star leg: k = 32, r = 8 encode, 2^21 blocks (one GPU's share of config 4)
         nb2, k2, r2 = 1 << 21, 32, 8
         del src, rep
@@ -434,7 +578,7 @@ def main():
         torch.cuda.synchronize()
         ms = a.elapsed_time(b_) / 5
         gbs = (k2 + r2) * L * nb2 / (ms * 1e-3) / 1e9
-        legs["rlc_encode_k32_r8"] = {"ms": round(ms, 3), "blocks": nb2,
+        legs["rlc_encode_k32_r8"] = {"kernel": "k_rlc_encode_bs<8,16>", "ms": round(ms, 3), "blocks": nb2,
                                      "payload_GiB_s": round(nb2 * k2 * L / (ms * 1e-3) / 2**30, 2),
                                      "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                                      "traffic": load_traffic("rlc_encode_k32_r8", nb2)}
@@ -446,33 +590,37 @@ def main():
         legs["xor_k4_r1"] = xor_leg(torch, eng, dev, 4, L, 1 << 22)
 
     if rank == 0:
-        if enc_ms >= apply_ms:
-            roof = {"bound": "hbm", "kernel": "k_rlc_encode_bs<4,16> (RLC encode k=16 r=4)",
+        if not e or enc_ms >= apply_ms:
+            roof = {"bound": "hbm", "kernel": f"k_rlc_encode_bs<{rt},{vec}> (RLC encode k={k} r={r})",
                     "achieved": round(enc_gbs, 1), "bytes_per_launch": enc_bytes, "launch_ms": round(enc_ms, 4),
-                    "traffic": load_traffic("rlc_encode_k16_r4", nb)}
+                    "traffic": load_traffic(f"rlc_encode_{tag}", nb)}
         else:
-            roof = {"bound": "hbm", "kernel": "k_rlc_recover_bs<4,16> (RLC decode apply k=16 e=4)",
+            roof = {"bound": "hbm", "kernel": f"k_rlc_recover_bs<{ert},{vec}> (RLC decode apply k={k} e={e})",
                     "achieved": round(app_gbs, 1), "bytes_per_launch": app_bytes, "launch_ms": round(apply_ms, 4),
-                    "traffic": load_traffic("rlc_decode_apply_k16_e4", nb)}
+                    "traffic": load_traffic(f"rlc_decode_apply_k{k}_e{e}", nb)}
         roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),
                      "measured_copy_peak": MEASURED_COPY_GBS,
                      "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4),
-                     "measured_mix41_peak": MEASURED_MIX41_GBS,
-                     "pattern_ceiling": PATTERN_CEILING_GBS,
-                     "frac_of_pattern_ceiling": round(roof["achieved"] / PATTERN_CEILING_GBS, 4)})
-        cpu = None
-        if not args.no_cpu and world == 1:
-            nthreads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-            cpu = cpu_baseline(args, nthreads)
+                     "measured_mix41_peak": MEASURED_MIX41_GBS})
+        if args.config == "k16":
+            roof.update({"pattern_ceiling": PATTERN_CEILING_GBS,
+                         "frac_of_pattern_ceiling": round(roof["achieved"] / PATTERN_CEILING_GBS, 4)})
+        conf = {"workload": cfg["workload"], "k": k, "r": r, "erasures": e, "symbol_bytes": L,
+                "blocks_per_gpu": share, "blocks_total": total_blocks, "resident_blocks_per_gpu": nb,
+                "passes_per_step": passes,
+                "parallelism": f"independent FEC blocks, {world} GPU(s), no collective"}
+        if e:
+            conf["decode_output"] = "recovered symbols into their own buffer (as fec_recover allocates them)"
+        if passes > 1:
+            conf["note"] = (f"a GPU's share ({share} blocks) exceeds HBM: each step codes it in {passes} passes "
+                            f"over {nb} resident blocks, block numbers advancing per pass")
         out = {"metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-               "config": {"workload": "RLC-GF(256) encode k=16 r=4 + decode 4 erasures, 1200B symbols",
-                          "k": k, "r": r, "erasures": e, "symbol_bytes": L, "blocks_per_gpu": nb,
-                          "decode_output": "recovered symbols into their own buffer (as fec_recover allocates them)",
-                          "parallelism": f"independent FEC blocks, {world} GPU(s), no collective"},
-               "roofline": roof, "cpu_baseline": cpu, "legs": legs}
+               "scaling": cfg["scaling"], "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "config": conf, "roofline": roof, "cpu_baseline": cpu, "legs": legs}
+        if per_rank:
+            out["per_rank_ms_per_step"] = per_rank
         print(json.dumps(out))
     if dist:
         dist.barrier()

@@ -529,3 +529,26 @@ int ref_cpu_baseline(int nworkers, const uint8_t *src, uint64_t nblocks, int k, 
     munmap(shm, shm_len);
     return ok ? 0 : -1;
 }
+
+/* In-process, one core (no fork): the same work as one ref_cpu_baseline worker; returns the
+ * number of blocks decoded, or -1.  bench.py's hook-latency leg divides by it for the reference
+ * pluglets' own time per block.  The caller screens out the crash patterns (skip[]). */
+long ref_work_serial(const uint8_t *src, uint64_t nblocks, int k, int r, int L, uint32_t fbn_base,
+                     const uint64_t *sp, const uint8_t *skip, double *enc_s, double *dec_s) {
+    uint8_t *rep = malloc(nblocks * (size_t)r * L + 1);
+    if (!rep || !scheme()) return -1;
+    uint8_t *none = calloc(nblocks + 1, 1);
+    uint8_t *all = malloc(nblocks + 1);
+    memset(all, 1, nblocks + 1);
+    double t0 = now_s();  /* encode only: every block skipped in the decode half */
+    long d = ref_work_range(src, rep, 0, nblocks, k, r, L, fbn_base, sp, all);
+    double t1 = now_s();
+    /* decode only: re-encode untimed is not possible through ref_work_range, so time both and
+     * subtract the encode time measured just before */
+    long d2 = ref_work_range(src, rep, 0, nblocks, k, r, L, fbn_base, sp, skip);
+    double t2 = now_s();
+    *enc_s = t1 - t0;
+    *dec_s = (t2 - t1) - (t1 - t0);
+    free(rep); free(none); free(all);
+    return d < 0 || d2 < 0 ? -1 : d2;
+}

@@ -192,6 +192,22 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
   // straight into it over PCIe, so nothing but status comes back by copy
   uint8_t *zdst = xr ? nullptr : mapped_host(src);
   const uint8_t *zrep = zdst && zc_read() ? mapped_host(rep) : nullptr;
+  // page-locked masks / seeds / outputs as well (the synchronous protoops keep theirs so): the
+  // kernels read and write them in place, and a call is two launches and one synchronisation with
+  // no copies at all -- the latency of one-block calls is launch + PCIe round trips
+  const uint32_t *zseed = nullptr;
+  const uint64_t *zsp = nullptr, *zrp = nullptr;
+  uint8_t *zst = nullptr;
+  uint64_t *zrec = nullptr;
+  if (zrep) {
+    zsp = (const uint64_t *)mapped_host(sp);
+    zrp = zsp ? (const uint64_t *)mapped_host(rp) : nullptr;
+    zst = zrp ? mapped_host(status) : nullptr;
+    zrec = zst ? (uint64_t *)mapped_host(recovered) : nullptr;
+    const uint32_t *sf = seeds ? seeds : fbn;
+    zseed = zrec && sf ? (const uint32_t *)mapped_host(sf) : nullptr;
+    if (!zrec || (sf && !zseed)) zsp = nullptr;  // all or nothing
+  }
   int si = 0, rc = FECGPU_OK;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
@@ -202,12 +218,20 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
     uint64_t *d_sp = (uint64_t *)(aux + ((n * 4 * nseed + 15) & ~(size_t)15));
     uint64_t *d_rp = d_sp + 2 * n, *d_rec = d_rp + 2 * n;
     uint8_t *d_st = (uint8_t *)(d_rec + 2 * n);
-    LCHK(hipMemcpyAsync(d_sp, sp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
-    LCHK(hipMemcpyAsync(d_rp, rp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
-    if (seeds && r) {
-      LCHK(hipMemcpyAsync(d_fbn, seeds + b0 * r, m * 4 * r, hipMemcpyHostToDevice, s.st));
-    } else if (fbn) {
-      LCHK(hipMemcpyAsync(d_fbn, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+    if (zsp) {  // everything page-locked: the kernels use the caller's arrays in place
+      d_sp = const_cast<uint64_t *>(zsp) + 2 * b0;
+      d_rp = const_cast<uint64_t *>(zrp) + 2 * b0;
+      d_rec = zrec + 2 * b0;
+      d_st = zst + b0;
+      if (zseed) d_fbn = const_cast<uint32_t *>(zseed) + (seeds ? b0 * r : b0);
+    } else {
+      LCHK(hipMemcpyAsync(d_sp, sp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync(d_rp, rp + 2 * b0, m * 16, hipMemcpyHostToDevice, s.st));
+      if (seeds && r) {
+        LCHK(hipMemcpyAsync(d_fbn, seeds + b0 * r, m * 4 * r, hipMemcpyHostToDevice, s.st));
+      } else if (fbn) {
+        LCHK(hipMemcpyAsync(d_fbn, fbn + b0, m * 4, hipMemcpyHostToDevice, s.st));
+      }
     }
     const uint8_t *in_src, *in_rep;
     if (zrep) {
@@ -235,8 +259,10 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
     }
     if (rc) break;
     if (!zdst) LCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));
-    LCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
-    LCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
+    if (!zsp) {
+      LCHK(hipMemcpyAsync(status + b0, d_st, m, hipMemcpyDeviceToHost, s.st));
+      LCHK(hipMemcpyAsync(recovered + 2 * b0, d_rec, m * 16, hipMemcpyDeviceToHost, s.st));
+    }
   }
   return finish(c, rc);
 }

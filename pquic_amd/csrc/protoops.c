@@ -39,9 +39,18 @@ static int g_device;
 static fecgpu_host_ctx_t *g_ctx;
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 
-/* per-call staging (host), grown on demand */
+/* Per-call staging, page-locked (fecgpu_host_alloc) and grown on demand: the engine's host path
+ * then runs zero-copy -- the kernels read the staged rows and write repairs / recovered rows and
+ * the small per-block arrays (seeds, masks, status) in place over PCIe -- so a one-block call is
+ * launches plus one synchronisation, with no copy stages. */
 static uint8_t *g_src, *g_rep;
 static size_t g_src_cap, g_rep_cap;
+typedef struct {
+    uint32_t seeds[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
+    uint64_t sp[2], rp[2], rec[2];
+    uint8_t st;
+} aux_t;
+static aux_t *g_aux;
 
 int pquic_fec_bind_host(const pquic_fec_host_api_t *api, int device) {
     pthread_mutex_lock(&g_mu);
@@ -85,19 +94,22 @@ static fecgpu_host_ctx_t *ctx(void) {
     return g_ctx;
 }
 
+static int grow_pinned(uint8_t **p, size_t *cap, size_t need) {
+    if (need <= *cap) return 0;
+    size_t n = *cap ? *cap : 64 * 1024;
+    while (n < need) n *= 2;
+    uint8_t *q = fecgpu_host_alloc(n);
+    if (!q) return -1;
+    fecgpu_host_free(*p);
+    *p = q;
+    *cap = n;
+    return 0;
+}
+
 static int stage(size_t src_bytes, size_t rep_bytes) {
-    if (src_bytes > g_src_cap) {
-        uint8_t *p = realloc(g_src, src_bytes);
-        if (!p) return -1;
-        g_src = p;
-        g_src_cap = src_bytes;
-    }
-    if (rep_bytes > g_rep_cap) {
-        uint8_t *p = realloc(g_rep, rep_bytes);
-        if (!p) return -1;
-        g_rep = p;
-        g_rep_cap = rep_bytes;
-    }
+    if (!g_aux && !(g_aux = fecgpu_host_alloc(sizeof *g_aux))) return -1;
+    if (grow_pinned(&g_src, &g_src_cap, src_bytes) || grow_pinned(&g_rep, &g_rep_cap, rep_bytes ? rep_bytes : 4))
+        return -1;
     return 0;
 }
 
@@ -186,16 +198,16 @@ static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
     pthread_mutex_lock(&g_mu);
     FEC_STAT_ADD(recover_calls, 1);
     const uint32_t L = fec_pad4(maxl ? maxl : 1);
-    uint64_t sp[2], rp[2], rec[2] = {0, 0};
-    uint32_t seeds[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
-    uint8_t st = FECGPU_BLOCK_NOTHING;
     int rc = stage((size_t)k * L, (size_t)r * L);
     fecgpu_host_ctx_t *c = rc ? NULL : ctx();
     if (c) {
-        fec_recover_stage(fb, xor_scheme, maxl, g_src, g_rep, L, sp, rp, seeds);
-        rc = xor_scheme ? fecgpu_xor_decode_host(c, g_src, g_rep, 1, (uint32_t)k, L, sp, rp, &st, rec)
-                        : fecgpu_rlc_decode_host_seeded(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, seeds, sp,
-                                                        rp, &st, rec);
+        aux_t *a = g_aux;
+        a->st = FECGPU_BLOCK_NOTHING;
+        a->rec[0] = a->rec[1] = 0;
+        fec_recover_stage(fb, xor_scheme, maxl, g_src, g_rep, L, a->sp, a->rp, a->seeds);
+        rc = xor_scheme ? fecgpu_xor_decode_host(c, g_src, g_rep, 1, (uint32_t)k, L, a->sp, a->rp, &a->st, a->rec)
+                        : fecgpu_rlc_decode_host_seeded(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, a->seeds,
+                                                        a->sp, a->rp, &a->st, a->rec);
     } else {
         rc = -1;
     }
@@ -204,7 +216,7 @@ static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
         FEC_STAT_ADD(errors, 1);
         ret = PQUIC_FEC_ERR_UNBOUND;
     } else {
-        ret = fec_recover_finish(cnx, fb, xor_scheme, st, rec, g_src, L, maxl);
+        ret = fec_recover_finish(cnx, fb, xor_scheme, g_aux->st, g_aux->rec, g_src, L, maxl);
     }
     pthread_mutex_unlock(&g_mu);
     return ret;

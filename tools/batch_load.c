@@ -15,10 +15,14 @@
 
 #include "pquic_fec_batch.h"
 
-struct st_picoquic_cnx_t { int id; };
+struct st_picoquic_cnx_t { int id; protoop_arg_t in[16], out[16]; };
 
-static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) { (void)c; (void)ak; (void)p; return 0; }
-static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t v) { (void)c; (void)ak; (void)p; (void)v; }
+static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) {
+    return ak == PQUIC_AK_CNX_INPUT ? c->in[p & 15] : c->out[p & 15];
+}
+static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t v) {
+    if (ak == PQUIC_AK_CNX_OUTPUT) c->out[p & 15] = v;
+}
 /* The plugin allocator hands out fixed 2100-byte slots from a free list (picoquic/memory.c:72-95,
  * 181-191); this load generator does the same, so completions cost what they cost in PQUIC
  * rather than glibc malloc's price.  Larger requests fall back to the heap, tagged. */
@@ -161,5 +165,79 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     out[7] = out[4] > 0 ? out[6] / out[4] : 0;
     free(slots); free(pool); free(ss); free(g_lat); free(cnx);
     g_lat = NULL;
+    return 0;
+}
+
+/* Latency of the synchronous drop-in hooks: one block per call, exactly as the block framework
+ * calls fec_generate_repair_symbols (block_framework_sender.h:187) and fec_recover
+ * (fec_protoops.h:246), through pquic_fec_rlc_generate_repair_symbols / pquic_fec_rlc_recover.
+ * Each call stages the block, runs the device and writes the repairs / recovered symbols back
+ * with the bound allocator.  `e` sources are erased for recover (all r repairs present).
+ * out: [0] generate p50 us, [1] p99, [2] mean, [3] recover p50, [4] p99, [5] mean,
+ *      [6] recovered symbols per recover call (check).  Returns 0 or -1. */
+int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double out[7]) {
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
+    if (pquic_fec_bind_host(&api, device) || k > 100 || r > 100 || e > r || e > k) return -1;
+    picoquic_cnx_t cnx;
+    memset(&cnx, 0, sizeof cnx);
+    if (pquic_fec_rlc_create_fec_schemes(&cnx)) return -1;
+    const protoop_arg_t scheme = cnx.out[0];
+    uint8_t *pool = malloc((size_t)k * L);
+    pquic_source_symbol_t *ss = calloc((size_t)k, sizeof *ss);
+    uint64_t *lat = malloc(sizeof *lat * (size_t)ncalls);
+    if (!pool || !ss || !lat) return -1;
+    uint64_t x = 0x5EEDF3C0;
+    for (size_t o = 0; o < (size_t)k * L; o++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; pool[o] = (uint8_t)x; }
+    pquic_fec_block_t fb;
+    long recovered = 0;
+    for (int op = 0; op < 2; op++) {
+        for (long c = -ncalls / 10 - 1; c < ncalls; c++) {  /* the first tenth warms up */
+            const uint32_t fbn = (uint32_t)(c & 0xffffff);
+            memset(&fb, 0, sizeof fb);
+            fb.fec_block_number = fbn;
+            fb.total_source_symbols = (uint8_t)k;
+            fb.total_repair_symbols = (uint8_t)r;
+            for (int j = 0; j < k; j++) {
+                ss[j].fpid.raw = (fbn << 8) | (uint32_t)j;
+                ss[j].data = pool + (size_t)j * L;
+                ss[j].data_length = (uint16_t)L;
+                fb.source_symbols[j] = &ss[j];
+            }
+            fb.current_source_symbols = (uint8_t)k;
+            cnx.in[0] = (protoop_arg_t)(uintptr_t)&fb;
+            cnx.in[1] = scheme;
+            /* repairs for this block (untimed when measuring recover) */
+            uint64_t t0 = now_us();
+            if (pquic_fec_rlc_generate_repair_symbols(&cnx)) return -1;
+            uint64_t t1 = now_us();
+            if (op == 1) {
+                fb.current_repair_symbols = (uint8_t)r;
+                const int first = (int)(c % (k - e + 1) + k - e + 1) % (k - e + 1);
+                for (int j = first; j < first + e; j++) fb.source_symbols[j] = NULL;
+                fb.current_source_symbols = (uint8_t)(k - e);
+                t0 = now_us();
+                if (pquic_fec_rlc_recover(&cnx)) return -1;
+                t1 = now_us();
+                for (int j = first; j < first + e; j++)
+                    if (fb.source_symbols[j]) {
+                        if (c >= 0) recovered++;
+                        bl_free(NULL, fb.source_symbols[j]->data);
+                        bl_free(NULL, fb.source_symbols[j]);
+                    }
+            }
+            for (int i = 0; i < r; i++)
+                if (fb.repair_symbols[i]) { bl_free(NULL, fb.repair_symbols[i]->data); bl_free(NULL, fb.repair_symbols[i]); }
+            if (c >= 0) lat[c] = t1 - t0;
+        }
+        double sum = 0;
+        for (long c = 0; c < ncalls; c++) sum += (double)lat[c];
+        qsort(lat, ncalls, sizeof *lat, cmp_u64);
+        out[3 * op + 0] = (double)lat[ncalls / 2];
+        out[3 * op + 1] = (double)lat[(long)(ncalls * 0.99)];
+        out[3 * op + 2] = sum / ncalls;
+    }
+    out[6] = (double)recovered / ncalls;
+    bl_free(NULL, (void *)(uintptr_t)scheme);
+    free(pool); free(ss); free(lat);
     return 0;
 }
