@@ -33,8 +33,12 @@
 static protoop_arg_t g_in[PROTOOPARGS_MAX];
 static protoop_arg_t g_out[PROTOOPARGS_MAX];
 
+static int g_cc_path;   /* the CC scenario's path object (below) */
+static int g_cc_active;
+
 protoop_arg_t get_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param) {
     (void)cnx;
+    if (ak == AK_CNX_PATH) return (protoop_arg_t)&g_cc_path;
     if (ak == AK_CNX_INPUT) return g_in[param];
     if (ak == AK_CNX_OUTPUT) return g_out[param];
     return 0;
@@ -361,8 +365,10 @@ int ref_skip_frame_synthetic(const uint8_t *bytes, size_t bytes_max, size_t *con
 static bpf_state g_state;
 protoop_arg_t get_cnx_metadata(picoquic_cnx_t *cnx, int idx) { (void)cnx; (void)idx; return (protoop_arg_t)&g_state; }
 void set_cnx_metadata(picoquic_cnx_t *cnx, int idx, protoop_arg_t val) { (void)cnx; (void)idx; (void)val; }
+static protoop_arg_t cc_protoop(const char *pid, protoop_params_t *pp);
 protoop_arg_t plugin_run_protoop(picoquic_cnx_t *cnx, protoop_params_t *pp, char *pid_str, protoop_id_t *pid) {
     (void)cnx; (void)pid;
+    if (g_cc_active) return cc_protoop(pid_str, pp);
     if (strcmp(pid_str, PROTOOPID_NOPARAM_SKIP_FRAME) == 0) {
         size_t consumed = 0;
         int ret = ref_skip_frame_synthetic((const uint8_t *)pp->inputv[0], (size_t)pp->inputv[1], &consumed);
@@ -551,4 +557,128 @@ long ref_work_serial(const uint8_t *src, uint64_t nblocks, int k, int r, int L, 
     *dec_s = (t2 - t1) - (t1 - t0);
     free(rep); free(none); free(all);
     return d < 0 || d2 < 0 ? -1 : d2;
+}
+
+/* ---- recovered packets -> congestion control -----------------------------------
+ * The reference pluglet protoops/maybe_notify_recovered_packets_to_cc.c (prepare_packet_ready pre-hook,
+ * fec_protoops.h:151-184), compiled in place, run against a scripted transport: a retransmit queue of
+ * packets (number, pure-ACK flag, "retransmit needed" verdict), one path (smoothed RTT) and its
+ * application packet context (latest CC notification time).  Every transport call the pluglet makes
+ * is logged as 4 u64: {kind, a, b, c}:
+ *   1 retransmit_needed_by_packet(pn, now, timer_based_in)   2 packet_was_lost(pn)
+ *   3 dequeue_retransmit_packet(pn, should_free)             4 congestion_algorithm_notify(notification,
+ *   5 set latest CC notification time(t)                        lost pn, now) [rtt / bytes are 0] */
+typedef struct { uint64_t pn; int pure_ack, needed; } cc_pkt_t;
+static cc_pkt_t *g_cc_pkts;
+static int g_cc_n;
+static uint64_t g_cc_srtt, g_cc_latest;
+static uint64_t *g_cc_ev;
+static int g_cc_nev, g_cc_maxev;
+static int g_cc_ctx;  /* its address stands in for the packet context (g_cc_path: the path) */
+
+static void cc_log(uint64_t k, uint64_t a, uint64_t b, uint64_t c) {
+    if (g_cc_nev < g_cc_maxev) {
+        uint64_t *e = g_cc_ev + 4 * g_cc_nev;
+        e[0] = k; e[1] = a; e[2] = b; e[3] = c;
+    }
+    g_cc_nev++;
+}
+
+protoop_arg_t get_path(picoquic_path_t *path, access_key_t ak, uint16_t param) {
+    (void)path; (void)param;
+    if (ak == AK_PATH_PKT_CTX) return (protoop_arg_t)&g_cc_ctx;
+    if (ak == AK_PATH_SMOOTHED_RTT) return g_cc_srtt;
+    return 0;
+}
+protoop_arg_t get_pkt_ctx(picoquic_packet_context_t *ctx, access_key_t ak) {
+    (void)ctx;
+    if (ak == AK_PKTCTX_RETRANSMIT_OLDEST) return g_cc_n ? (protoop_arg_t)&g_cc_pkts[0] : 0;
+    if (ak == AK_PKTCTX_LATEST_RETRANSMIT_CC_NOTIFICATION_TIME) return g_cc_latest;
+    return 0;
+}
+void set_pkt_ctx(picoquic_packet_context_t *ctx, access_key_t ak, protoop_arg_t val) {
+    (void)ctx;
+    if (ak == AK_PKTCTX_LATEST_RETRANSMIT_CC_NOTIFICATION_TIME) {
+        g_cc_latest = val;
+        cc_log(5, val, 0, 0);
+    }
+}
+protoop_arg_t get_pkt(picoquic_packet_t *pkt, access_key_t ak) {
+    cc_pkt_t *p = (cc_pkt_t *)pkt;
+    if (ak == AK_PKT_NEXT_PACKET) return p + 1 < g_cc_pkts + g_cc_n ? (protoop_arg_t)(p + 1) : 0;
+    if (ak == AK_PKT_SEQUENCE_NUMBER) return p->pn;
+    if (ak == AK_PKT_IS_PURE_ACK) return (protoop_arg_t)p->pure_ack;
+    return 0;
+}
+
+static protoop_arg_t cc_protoop(const char *pid, protoop_params_t *pp) {
+    if (strcmp(pid, PROTOOPID_NOPARAM_RETRANSMIT_NEEDED_BY_PACKET) == 0) {
+        cc_pkt_t *p = (cc_pkt_t *)pp->inputv[0];
+        cc_log(1, p->pn, pp->inputv[1], pp->inputv[2]);
+        if (pp->outputv) { pp->outputv[0] = 0; pp->outputv[1] = 0; pp->outputv[2] = 0; }
+        return (protoop_arg_t)p->needed;
+    }
+    if (strcmp(pid, PROTOOPID_NOPARAM_PACKET_WAS_LOST) == 0) {
+        cc_log(2, ((cc_pkt_t *)pp->inputv[0])->pn, pp->inputv[1] == (protoop_arg_t)&g_cc_path, 0);
+        return 0;
+    }
+    if (strcmp(pid, PROTOOPID_NOPARAM_DEQUEUE_RETRANSMIT_PACKET) == 0) {
+        cc_log(3, ((cc_pkt_t *)pp->inputv[0])->pn, pp->inputv[1], 0);
+        return 0;
+    }
+    if (strcmp(pid, PROTOOPID_NOPARAM_CONGESTION_ALGORITHM_NOTIFY) == 0) {
+        cc_log(4, pp->inputv[1], pp->inputv[4], pp->inputv[5]);
+        return 0;
+    }
+    return (protoop_arg_t)-1;
+}
+
+protoop_arg_t ref_prepare_packet_ready(picoquic_cnx_t *cnx);
+
+/* One scenario.  pkts: n x {pn, pure_ack, needed}; buf: {start, size, 50 packet numbers} in/out.
+ * Returns the number of events (log holds min(that, maxev)); *latest_out = the final time. */
+int ref_cc_scenario(int n, const uint64_t *pns, const uint8_t *pure, const uint8_t *needed, uint64_t srtt,
+                    uint64_t latest, uint64_t now, uint32_t *buf_start, uint32_t *buf_size, uint64_t *buf_pns,
+                    uint64_t *events, int maxev, uint64_t *latest_out) {
+    cc_pkt_t *pk = calloc((size_t)(n ? n : 1), sizeof *pk);
+    for (int i = 0; i < n; i++) { pk[i].pn = pns[i]; pk[i].pure_ack = pure[i]; pk[i].needed = needed[i]; }
+    g_cc_pkts = pk; g_cc_n = n; g_cc_srtt = srtt; g_cc_latest = latest;
+    g_cc_ev = events; g_cc_nev = 0; g_cc_maxev = maxev;
+    memset(&g_state, 0, sizeof g_state);
+    g_state.recovered_packets.start = *buf_start;
+    g_state.recovered_packets.size = *buf_size;
+    memcpy(g_state.recovered_packets.packet_numbers, buf_pns, sizeof g_state.recovered_packets.packet_numbers);
+    memset(g_in, 0, sizeof g_in);
+    g_in[2] = now;
+    g_cc_active = 1;
+    ref_prepare_packet_ready(NULL);
+    g_cc_active = 0;
+    *buf_start = g_state.recovered_packets.start;
+    *buf_size = g_state.recovered_packets.size;
+    memcpy(buf_pns, g_state.recovered_packets.packet_numbers, sizeof g_state.recovered_packets.packet_numbers);
+    *latest_out = g_cc_latest;
+    free(pk);
+    return g_cc_nev;
+}
+
+protoop_arg_t ref_process_recovered_frame(picoquic_cnx_t *cnx);
+
+/* process_recovered_frame (protoops/process_simple_recovered_frame.c): enqueue a parsed frame's
+ * packet numbers ([n][n x u64], as parse_recovered_frame hands them over) into the ring
+ * {start, size, 50 pns} (in/out). */
+void ref_process_recovered(const uint64_t *pns, int n, uint32_t *buf_start, uint32_t *buf_size, uint64_t *buf_pns) {
+    uint8_t *sp = malloc(1 + 8 * (size_t)(n ? n : 1));
+    sp[0] = (uint8_t)n;
+    memcpy(sp + 1, pns, 8 * (size_t)n);
+    memset(&g_state, 0, sizeof g_state);
+    g_state.recovered_packets.start = *buf_start;
+    g_state.recovered_packets.size = *buf_size;
+    memcpy(g_state.recovered_packets.packet_numbers, buf_pns, sizeof g_state.recovered_packets.packet_numbers);
+    memset(g_in, 0, sizeof g_in);
+    g_in[0] = (protoop_arg_t)sp;
+    ref_process_recovered_frame(NULL);
+    *buf_start = g_state.recovered_packets.start;
+    *buf_size = g_state.recovered_packets.size;
+    memcpy(buf_pns, g_state.recovered_packets.packet_numbers, sizeof g_state.recovered_packets.packet_numbers);
+    free(sp);
 }

@@ -399,3 +399,76 @@ void mh_batch_close(void) {
     g_tickets = NULL;
     g_nt = g_capt = 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Recovered packets -> congestion control (include/pquic_fec_cc.h): the same scripted transport
+ * as oracle/ref/ref_driver.c's ref_cc_scenario, bound through pquic_fec_transport_api_t, with the
+ * same event log, so the product's calls can be compared with the reference pluglet's.
+ * ------------------------------------------------------------------------------------------ */
+#include "pquic_fec_cc.h"
+
+typedef struct { uint64_t pn; int pure_ack, needed; } cc_pkt_t;
+static cc_pkt_t *g_ccp;
+static int g_ccn;
+static uint64_t g_srtt, g_latest, *g_ev;
+static int g_nev, g_maxev;
+static int g_path_obj, g_ctx_obj;
+
+static void ev(uint64_t k, uint64_t a, uint64_t b, uint64_t c) {
+    if (g_nev < g_maxev) { uint64_t *e = g_ev + 4 * g_nev; e[0] = k; e[1] = a; e[2] = b; e[3] = c; }
+    g_nev++;
+}
+static void *t_path(picoquic_cnx_t *cnx) { (void)cnx; return &g_path_obj; }
+static void *t_ctx(void *path) { (void)path; return &g_ctx_obj; }
+static void *t_oldest(void *ctx) { (void)ctx; return g_ccn ? &g_ccp[0] : NULL; }
+static void *t_next(void *p) { cc_pkt_t *q = p; return q + 1 < g_ccp + g_ccn ? q + 1 : NULL; }
+static uint64_t t_pn(void *p) { return ((cc_pkt_t *)p)->pn; }
+static int t_pure(void *p) { return ((cc_pkt_t *)p)->pure_ack; }
+static uint64_t t_latest(void *ctx) { (void)ctx; return g_latest; }
+static void t_set_latest(void *ctx, uint64_t v) { (void)ctx; g_latest = v; ev(5, v, 0, 0); }
+static uint64_t t_srtt(void *path) { (void)path; return g_srtt; }
+static int t_needed(picoquic_cnx_t *cnx, void *p, uint64_t now, int *tb) {
+    (void)cnx;
+    ev(1, ((cc_pkt_t *)p)->pn, now, (uint64_t)*tb);
+    *tb = 0;
+    return ((cc_pkt_t *)p)->needed;
+}
+static void t_lost(picoquic_cnx_t *cnx, void *p, void *path) { (void)cnx; ev(2, ((cc_pkt_t *)p)->pn, path == &g_path_obj, 0); }
+static void t_deq(picoquic_cnx_t *cnx, void *p, int f) { (void)cnx; ev(3, ((cc_pkt_t *)p)->pn, (uint64_t)f, 0); }
+static void t_notify(picoquic_cnx_t *cnx, void *path, int n, uint64_t rtt, uint64_t nb, uint64_t lost, uint64_t now) {
+    (void)cnx; (void)path; (void)rtt; (void)nb;
+    ev(4, (uint64_t)n, lost, now);
+}
+
+int mh_cc_scenario(int n, const uint64_t *pns, const uint8_t *pure, const uint8_t *needed, uint64_t srtt,
+                   uint64_t latest, uint64_t now, uint32_t *buf_start, uint32_t *buf_size, uint64_t *buf_pns,
+                   uint64_t *events, int maxev, uint64_t *latest_out) {
+    static const pquic_fec_transport_api_t t = {t_path, t_ctx, t_oldest, t_next, t_pn, t_pure, t_latest,
+                                                t_set_latest, t_srtt, t_needed, t_lost, t_deq, t_notify};
+    cc_pkt_t *pk = calloc((size_t)(n ? n : 1), sizeof *pk);
+    for (int i = 0; i < n; i++) { pk[i].pn = pns[i]; pk[i].pure_ack = pure[i]; pk[i].needed = needed[i]; }
+    g_ccp = pk; g_ccn = n; g_srtt = srtt; g_latest = latest; g_ev = events; g_nev = 0; g_maxev = maxev;
+    pquic_fec_recovered_packets_buffer_t b;
+    b.start = *buf_start;
+    b.size = *buf_size;
+    memcpy(b.packet_numbers, buf_pns, sizeof b.packet_numbers);
+    picoquic_cnx_t cnx;
+    pquic_fec_maybe_notify_recovered_packets_to_cc(&cnx, &t, &b, now);
+    *buf_start = b.start;
+    *buf_size = b.size;
+    memcpy(buf_pns, b.packet_numbers, sizeof b.packet_numbers);
+    *latest_out = g_latest;
+    free(pk);
+    return g_nev;
+}
+
+void mh_process_recovered(const uint64_t *pns, int n, uint32_t *buf_start, uint32_t *buf_size, uint64_t *buf_pns) {
+    pquic_fec_recovered_packets_buffer_t b;
+    b.start = *buf_start;
+    b.size = *buf_size;
+    memcpy(b.packet_numbers, buf_pns, sizeof b.packet_numbers);
+    pquic_fec_enqueue_recovered_packets(&b, pns, (uint8_t)n);
+    *buf_start = b.start;
+    *buf_size = b.size;
+    memcpy(buf_pns, b.packet_numbers, sizeof b.packet_numbers);
+}

@@ -706,3 +706,51 @@ def test_perm_datapath_vs_oracle(eng, oracle, k, r, L, nb):
     for b in range(nb):
         for j in bits(rec[b], k):
             assert np.array_equal(got[b, j], src_h[b, j])
+
+
+def test_sharded_engine_equals_unsharded(eng):
+    """Multi-GPU partitioning (pquic_amd/shard.py): the engine run on shard ranges with
+    fbn_base_of(b0) produces the bytes of the unsharded run -- encode repairs and decode output --
+    over a global block range that crosses the 24-bit block-number wrap (fec.h:44-50)."""
+    from pquic_amd.shard import fbn_base_of, shard_range
+    k, r, L = 16, 4, 1200
+    g0, total = (1 << 24) - 300, 700          # global blocks [2^24 - 300, 2^24 + 400)
+    src_h = synth_bytes(total * k * L, 314).reshape(total, k, L)
+    src = to_dev(src_h)
+    full = torch.empty((total, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_encode(src, full, k, r, L, fbn_base=fbn_base_of(g0))
+    rng = np.random.default_rng(31)
+    sp = np.zeros((total, 2), np.uint64)
+    rp = np.zeros((total, 2), np.uint64)
+    for b in range(total):
+        miss = rng.choice(k, 4, replace=False)
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        rp[b] = masks_from_lists(1, r, [list(range(r))])[0]
+    work = src.clone()
+    st = torch.empty(total, dtype=torch.uint8, device=DEV)
+    rec = torch.empty((total, 2), dtype=torch.int64, device=DEV)
+    eng.rlc_decode(work, full, to_dev(sp), to_dev(rp), st, rec, k, r, L, fbn_base=fbn_base_of(g0))
+    torch.cuda.synchronize()
+    for world in (2, 3, 8):
+        parts, dec, sts = [], [], []
+        for rank in range(world):
+            a, b = shard_range(total, world, rank)
+            rep = torch.empty((b - a, r, L), dtype=torch.uint8, device=DEV)
+            eng.rlc_encode(src[a:b], rep, k, r, L, fbn_base=fbn_base_of(g0 + a))
+            w = src[a:b].clone()
+            s_ = torch.empty(b - a, dtype=torch.uint8, device=DEV)
+            rc = torch.empty((b - a, 2), dtype=torch.int64, device=DEV)
+            eng.rlc_decode(w, rep, to_dev(sp[a:b]), to_dev(rp[a:b]), s_, rc, k, r, L, fbn_base=fbn_base_of(g0 + a))
+            parts.append(rep)
+            dec.append(w)
+            sts.append(s_)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(parts), full), world
+        assert torch.equal(torch.cat(sts), st), world
+        assert torch.equal(torch.cat(dec), work), world
+    # the wrap: block 2^24 has block number 0, so its repairs equal those of a block numbered 0
+    one = torch.empty((1, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_encode(src[300:301], one, k, r, L, fbn_base=0)
+    torch.cuda.synchronize()
+    assert torch.equal(one, full[300:301])
+    assert (st == DEC_RECOVERED).sum().item() > total * 0.9
