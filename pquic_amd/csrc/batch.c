@@ -15,9 +15,12 @@
  * state the protocol operation would leave it in.  The caller keeps a block unmodified until
  * its completion (pquic_fec_batch.h), which is what lets the copy happen late.
  */
+#define _GNU_SOURCE  /* sched_getaffinity / CPU_COUNT */
 #include "pquic_fec_batch.h"
 
 #include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -25,7 +28,7 @@
 #include "fecgpu.h"
 
 enum { OP_GENERATE = 0, OP_RECOVER = 1 };
-enum { MAX_OPEN = 32, MAX_STAGERS = 16, DEFAULT_STAGERS = 2 };
+enum { MAX_OPEN = 32, MAX_STAGERS = 16, STAGE_CHUNK = 256 /* blocks per staging work item */ };
 
 typedef struct {
     picoquic_cnx_t *cnx;
@@ -48,6 +51,7 @@ typedef struct job {
     entry_t *ent;
     uint64_t t_first;
     int rc;
+    uint32_t next_chunk, chunks_done;  /* staging work items claimed / finished (under the batcher lock) */
 } job_t;
 
 struct pquic_fec_batcher {
@@ -117,6 +121,7 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
     j->cap = cap;
     j->stride = S;
     j->rc = 0;
+    j->next_chunk = j->chunks_done = 0;
     return j;
 }
 
@@ -133,10 +138,10 @@ static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
                                                     j->st, j->rec);
 }
 
-/* Copies a job's blocks into its page-locked rows (the stage halves of fec_core.c). */
-static void stage_job(job_t *j) {
+/* Copies blocks [i0, i1) of a job into its page-locked rows (the stage halves of fec_core.c). */
+static void stage_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     const uint32_t S = j->stride, k = j->k, r = j->r;
-    for (uint32_t i = 0; i < j->n; i++) {
+    for (uint32_t i = i0; i < i1; i++) {
         const entry_t *e = &j->ent[i];
         uint8_t *src = j->src + (size_t)i * k * S;
         if (j->op == OP_GENERATE)
@@ -147,6 +152,9 @@ static void stage_job(job_t *j) {
     }
 }
 
+/* Stager threads split every job into work items of STAGE_CHUNK blocks, so several threads copy
+ * one job at once (a 4096-block k16 job is 79 MB of rows: one thread alone bounded the saturated
+ * rate); the thread finishing a job's last item hands it to the engine thread. */
 static void *stager_main(void *arg) {
     pquic_fec_batcher_t *b = arg;
     pthread_mutex_lock(&b->mu);
@@ -154,20 +162,45 @@ static void *stager_main(void *arg) {
         while (!b->todo_head && !b->stop) pthread_cond_wait(&b->cv_todo, &b->mu);
         if (!b->todo_head) break;  /* stop requested and nothing left */
         job_t *j = b->todo_head;
-        b->todo_head = j->next;
-        if (!b->todo_head) b->todo_tail = NULL;
+        const uint32_t nchunks = (j->n + STAGE_CHUNK - 1) / STAGE_CHUNK;
+        const uint32_t c = j->next_chunk++;
+        if (j->next_chunk >= nchunks) {  /* every item of this job is claimed: the next job is up */
+            b->todo_head = j->next;
+            if (!b->todo_head) b->todo_tail = NULL;
+        }
         pthread_mutex_unlock(&b->mu);
-        stage_job(j);
+        const uint32_t i0 = c * STAGE_CHUNK, i1 = i0 + STAGE_CHUNK < j->n ? i0 + STAGE_CHUNK : j->n;
+        stage_blocks(j, i0, i1);
         pthread_mutex_lock(&b->mu);
-        j->next = NULL;
-        if (b->staged_tail) b->staged_tail->next = j; else b->staged_head = j;
-        b->staged_tail = j;
-        pthread_cond_signal(&b->cv_staged);
+        if (++j->chunks_done == nchunks) {
+            j->next = NULL;
+            if (b->staged_tail) b->staged_tail->next = j; else b->staged_head = j;
+            b->staged_tail = j;
+            pthread_cond_signal(&b->cv_staged);
+        }
     }
     b->stagers_done++;
     pthread_cond_broadcast(&b->cv_staged);
     pthread_mutex_unlock(&b->mu);
     return NULL;
+}
+
+/* CPUs this process may use: the affinity mask bounded by a cgroup v2 CPU quota when one is set
+ * (a shared host can list every CPU in the mask and grant a slice of them). */
+static int host_cpus(void) {
+    cpu_set_t cs;
+    int n = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 2;
+    FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[32] = {0};
+        long per = 0;
+        if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+            const long quota = (atol(q) + per / 2) / per;
+            if (quota >= 1 && quota < n) n = (int)quota;
+        }
+        fclose(f);
+    }
+    return n < 1 ? 1 : n;
 }
 
 static void *worker_main(void *arg) {
@@ -209,8 +242,11 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     pthread_cond_init(&b->cv_todo, NULL);
     pthread_cond_init(&b->cv_staged, NULL);
     pthread_cond_init(&b->cv_done, NULL);
-    const char *ns = getenv("PQUIC_FEC_BATCH_STAGERS");  /* copy threads (default 2) */
-    b->nstagers = ns && atoi(ns) > 0 ? atoi(ns) : DEFAULT_STAGERS;
+    /* copy threads: half the CPUs of the process's share (the caller and the engine thread keep the
+     * rest), at least 2; PQUIC_FEC_BATCH_STAGERS overrides, read once per batcher */
+    const char *ns = getenv("PQUIC_FEC_BATCH_STAGERS");
+    const int half = host_cpus() / 2;
+    b->nstagers = ns && atoi(ns) > 0 ? atoi(ns) : (half > 2 ? half : 2);
     if (b->nstagers > MAX_STAGERS) b->nstagers = MAX_STAGERS;
     int started = 0;
     for (; started < b->nstagers; started++)

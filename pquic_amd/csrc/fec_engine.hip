@@ -43,9 +43,10 @@ static std::atomic<uint64_t> g_stats[4];
 // measured best.  They are read from the environment ONCE, on first use, so the engine's behaviour
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
-enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ, K_N };
+enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ,
+              K_RING, K_N };
 static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
-                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read"};
+                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -68,6 +69,7 @@ static void knobs_from_env() {
   g_knob[K_XOR_GENERIC] = num(getenv("FECGPU_XOR_GENERIC"), 0) != 0;
   g_knob[K_XOR_IDX64] = num(getenv("FECGPU_XOR_IDX64"), 0) != 0;
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
+  g_knob[K_RING] = num(getenv("FECGPU_RING"), 0);  // 1: the LDS-ring data path (bs2 bodies) where it applies
 }
 
 static inline int knob(KnobId id) {
@@ -1470,6 +1472,321 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
                      L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst);
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-ring data path (bs2_* bodies, gen_bitslice.py body2): the sources of a group stream into a
+// per-wave LDS ring by LDS-DMA, D-1 rows ahead (up to 1 KiB per wave-instruction, linear in memory
+// and in LDS); each step reads its 32 B per lane from the ring into the plane registers.  The rows
+// cost no VGPRs, so occupancy is set by the accumulators (RT <= 8: 4 waves per SIMD) and the ring
+// depth only by LDS.  16-B pieces only (symbol_size >= 16); blocks of at least D sources.
+// ---------------------------------------------------------------------------------------------
+#define FEC_BS2_D(MODE, RT) FEC_BS2_D_##MODE##_RT##RT
+
+template <int RT> struct Bs2Depth;
+#define FEC_BS2_DEPTH(RT) \
+  template <> struct Bs2Depth<RT> { static constexpr int enc = FEC_BS2_D(ENC, RT), dec = FEC_BS2_D(DEC, RT); };
+FEC_BS2_DEPTH(1) FEC_BS2_DEPTH(2) FEC_BS2_DEPTH(4) FEC_BS2_DEPTH(8) FEC_BS2_DEPTH(16)
+#undef FEC_BS2_DEPTH
+
+// Lane geometry of one chunk of cb bytes (cb >= 16) as 16-B pieces, the last pulled back to end at cb.
+// DMA: instruction 1 moves pieces 0..63 (lane = piece), instruction 2 pieces 64.. (lane = piece - 64);
+// piece t lands at ring slot + 16 t.  Compute: lane l (< A = ceil(pieces / 2)) owns pieces l and l + A.
+// c0 is added to the global offsets (decode: the table holds row starts; encode passes 0 and offsets
+// its base pointers instead).
+struct Bs2Lanes {
+  uint32_t g1, g2, rd1, rd2, off0, off1;
+  uint64_t vmlo, vmhi, vm0, vm1;
+  int npieces;
+  __device__ __forceinline__ Bs2Lanes(int lane, int cb, uint32_t c0) {
+    npieces = (cb + 15) / 16;
+    const int A = (npieces + 1) / 2;
+    auto gofs = [&](int t) { return (uint32_t)(t * 16 < cb - 16 ? t * 16 : cb - 16); };
+    const bool d1 = lane < npieces, d2 = lane + 64 < npieces;
+    g1 = c0 + (d1 ? gofs(lane) : 0u);
+    g2 = c0 + (d2 ? gofs(lane + 64) : 0u);
+    vmlo = __ballot(d1);
+    vmhi = __ballot(d2);
+    const int p1 = lane + A;
+    const bool ok0 = lane < A, ok1 = lane < A && p1 < npieces;
+    rd1 = ok0 ? 16u * (uint32_t)lane : 0u;
+    rd2 = ok1 ? 16u * (uint32_t)p1 : 0u;
+    off0 = ok0 ? c0 + gofs(lane) : 0u;
+    off1 = ok1 ? c0 + gofs(p1) : 0u;
+    vm0 = __ballot(ok0);
+    vm1 = __ballot(ok1);
+  }
+};
+
+static inline uint32_t bs2_slot_bytes(int chunk_bytes) { return (uint32_t)((chunk_bytes + 127) / 128 * 128); }
+
+#define BS2_LANE_ARGS ln.g1, ln.g2, ln.vmlo, ln.vmhi, ln.rd1, ln.rd2, ln.off0, ln.off1, ln.vm0, ln.vm1
+#define BS2_CALL_ENC(RT, ND) \
+  bs2_enc_r##RT##_d##ND(sp, rpp, (uint32_t)L, rslo, rshi, sdl, ll, (uint32_t)rt, nsrc, (uint32_t)k, ca, ring, ringend, \
+                        slotb, BS2_LANE_ARGS)
+#define BS2_CALL_DEC(RT, ND) \
+  bs2_dec_r##RT##_d##ND(ia, oa, nsrc, (uint32_t)k, ca, ring, ringend, slotb, BS2_LANE_ARGS)
+
+template <int RT>
+__device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp, int L, uint32_t rslo, uint32_t rshi,
+                                             uint64_t sdl, uint64_t ll, int rt, uint32_t nsrc, int k, uint32_t ca,
+                                             uint32_t ring, uint32_t ringend, uint32_t slotb, const Bs2Lanes &ln) {
+  if (two) {
+    if constexpr (RT == 1) BS2_CALL_ENC(1, 2); else if constexpr (RT == 2) BS2_CALL_ENC(2, 2);
+    else if constexpr (RT == 4) BS2_CALL_ENC(4, 2); else if constexpr (RT == 8) BS2_CALL_ENC(8, 2);
+    else BS2_CALL_ENC(16, 2);
+  } else {
+    if constexpr (RT == 1) BS2_CALL_ENC(1, 1); else if constexpr (RT == 2) BS2_CALL_ENC(2, 1);
+    else if constexpr (RT == 4) BS2_CALL_ENC(4, 1); else if constexpr (RT == 8) BS2_CALL_ENC(8, 1);
+    else BS2_CALL_ENC(16, 1);
+  }
+}
+
+template <int RT>
+__device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa, uint32_t nsrc, int k, uint32_t ca,
+                                             uint32_t ring, uint32_t ringend, uint32_t slotb, const Bs2Lanes &ln) {
+  if (two) {
+    if constexpr (RT == 1) BS2_CALL_DEC(1, 2); else if constexpr (RT == 2) BS2_CALL_DEC(2, 2);
+    else if constexpr (RT == 4) BS2_CALL_DEC(4, 2); else if constexpr (RT == 8) BS2_CALL_DEC(8, 2);
+    else BS2_CALL_DEC(16, 2);
+  } else {
+    if constexpr (RT == 1) BS2_CALL_DEC(1, 1); else if constexpr (RT == 2) BS2_CALL_DEC(2, 1);
+    else if constexpr (RT == 4) BS2_CALL_DEC(4, 1); else if constexpr (RT == 8) BS2_CALL_DEC(8, 1);
+    else BS2_CALL_DEC(16, 1);
+  }
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                       int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
+                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
+                                                       uint32_t slotb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
+  constexpr int D = Bs2Depth<RT>::enc;
+  const uint32_t ring = lds_addr(lds) + pad16((uint32_t)(G * k * CSB)), ringend = ring + D * slotb;
+  const int rt = r - r0 < RT ? r - r0 : RT;
+  const uint64_t NG = (nblocks + G - 1) / G;
+  const uint64_t bstep = ilv ? NG : 1;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    const uint64_t b0 = ilv ? q : q * G;
+    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const int ng = left < (uint64_t)G ? (int)left : G;
+    __syncthreads();
+    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0 + lane % RT)
+      const int g = lane / RT, i = lane % RT;
+      const uint64_t b = b0 + g * bstep;
+      uint16_t *row = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB) + i;
+      if (g < ng && i < rt) {
+        Tmt t;
+        const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
+        tmt_init(t, rlc_seed(f, (uint32_t)(r0 + i)));
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = (uint16_t)((tmt_coef(t) + 1u) * FEC_BS_CASE_BYTES);
+      } else {
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;
+      }
+      if constexpr (RT < 4) {
+        if (i == 0)
+          for (int j = 0; j < k; j++)
+            for (int x = RT; x < 4; x++) row[j * (CSB / 2) + x] = 0;
+      }
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ch++) {
+      const int c0 = ch * chunk_bytes;
+      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+      const Bs2Lanes ln(lane, cb, 0u);
+      const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);
+      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L + c0);
+      const uint64_t rstep = bstep * (uint64_t)r * L;
+      const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;
+      const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
+      const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
+      bs2_enc_call<RT>(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
+                       ringend, slotb, ln);
+    }
+  }
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
+                                                        uint8_t *status, uint64_t *recovered, int ilv,
+                                                        uint8_t *dst, uint32_t slotb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  RecoverLds<RT> S(lds, G, k);
+  constexpr int D = Bs2Depth<RT>::dec;
+  const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k)),
+                 ringend = ring + D * slotb;
+  const uint64_t NG = (nblocks + G - 1) / G;
+  const uint64_t bstep = ilv ? NG : 1;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    const uint64_t b0 = ilv ? q : q * G;
+    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const int ng = left < (uint64_t)G ? (int)left : G;
+    bool act = false;
+    int st = FECGPU_BLOCK_NOTHING, e = 0;
+    if (lane < ng) {
+      const uint8_t *h = ws + (b0 + lane * bstep) * (uint64_t)WL.stride;
+      st = h[0];
+      e = h[1];
+      act = st == FECGPU_BLOCK_RECOVERED && e > r0;
+    }
+    const uint64_t am = __ballot(act);
+    const int nact = __popcll(am);
+    __syncthreads();
+    if (act) {
+      const int t = __popcll(am & ((1ull << lane) - 1));
+      S.gid[t] = (uint8_t)lane;
+      S.ecnt[t] = (uint8_t)(e - r0 < RT ? e - r0 : RT);
+    }
+    __syncthreads();
+    for (int x = lane; x < nact * k; x += 64) {
+      const int t = x / k, j = x - t * k;
+      const uint64_t b = b0 + S.gid[t] * bstep;
+      const int rt = S.ecnt[t];
+      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      constexpr int NF = RecoverLds<RT>::CSB / 2;
+      uint16_t *row = reinterpret_cast<uint16_t *>(S.coef + (size_t)x * RecoverLds<RT>::CSB);
+#pragma unroll
+      for (int u = 0; u < NF; u++)
+        row[u] = (u < rt) ? (uint16_t)((h[WL.off_D + (r0 + u) * k + j] + 1u) * FEC_BS_CASE_BYTES) : (uint16_t)0;
+      const uint32_t sl = h[WL.off_slot + j];
+      const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
+                                     : src + (b * (uint64_t)k + sl) * (uint64_t)L;
+      S.intab[x] = (uint64_t)(uintptr_t)p;
+    }
+    for (int x = lane; x < nact * 16; x += 64) {
+      const int t = x >> 4, u = x & 15;
+      const uint64_t b = b0 + S.gid[t] * bstep;
+      const int rt = S.ecnt[t];
+      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      uint8_t *rc = S.rec + (size_t)t * kDecRec;
+      rc[kDecRecNz + u] = 0;
+      if (u < rt) {
+        const int j = h[WL.off_unk + r0 + u];
+        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
+        if (status) {
+          uint32_t m = 0;
+          for (int v = u + 1; v < rt; v++) m |= (uint32_t)(h[WL.off_dep + u * WL.em + v] != 0) << v;
+          S.unk[x] = (uint8_t)j;
+          S.depm[x] = m;
+        }
+      }
+      if (u == 0) {
+        reinterpret_cast<uint64_t *>(rc)[kDecRecNzPtr] = (uint64_t)(uintptr_t)(h + WL.off_nz + r0);
+        reinterpret_cast<uint32_t *>(rc)[kDecRecRt] = (uint32_t)rt;
+      }
+    }
+    __syncthreads();
+    if (nact) {
+      for (int ch = 0; ch < nchunks; ch++) {
+        const int c0 = ch * chunk_bytes;
+        const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+        const Bs2Lanes ln(lane, cb, (uint32_t)c0);
+        bs2_dec_call<RT>(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
+                         lds_addr(S.coef), ring, ringend, slotb, ln);
+      }
+    }
+    __syncthreads();
+    if (status) {
+      if (lane < ng) {
+        const uint64_t b = b0 + lane * bstep;
+        uint64_t m0 = 0, m1 = 0;
+        if (act) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
+          const int t = __popcll(am & ((1ull << lane) - 1));
+          const uint8_t *nzf = S.rec + (size_t)t * kDecRec + kDecRecNz;
+          uint32_t det = 0;
+          for (int u = e - 1; u >= 0; u--) {
+            if (nzf[u] && (S.depm[t * 16 + u] & ~det) == 0) {
+              det |= 1u << u;
+              const int j = S.unk[t * 16 + u];
+              if (j < 64) m0 |= 1ull << j; else m1 |= 1ull << (j - 64);
+            }
+          }
+        }
+        status[b] = (uint8_t)st;
+        recovered[2 * b] = m0;
+        recovered[2 * b + 1] = m1;
+      }
+    } else {
+      for (int x = lane; x < nact * 16; x += 64) {
+        const uint8_t *rc = S.rec + (size_t)(x >> 4) * kDecRec;
+        if (rc[kDecRecNz + (x & 15)])
+          reinterpret_cast<uint8_t *>(reinterpret_cast<const uint64_t *>(rc)[kDecRecNzPtr])[x & 15] = 1;
+      }
+    }
+  }
+}
+
+// Groups for the ring path: as bs_group, then halved until the workgroup's LDS (coefficient rows or
+// decode staging + the ring) leaves room for `waves` waves per CU (160 KiB of LDS per CU).
+static inline int bs2_group(int RT, int k, int per_j, int per_block, bool enc, int nchunks, size_t ring_bytes,
+                            int waves) {
+  int g = bs_group(RT, k, per_j, per_block, enc, nchunks);
+  const size_t budget = (size_t)160 * 1024 / (size_t)waves;
+  while (g > 1 && (size_t)g * (k * per_j + per_block) + 256 + ring_bytes > budget) g >>= 1;
+  return g;
+}
+
+// Target waves per CU for the ring kernels (VGPR-limited occupancy of the bodies: RT <= 4: 5,
+// RT = 8: 4, RT = 16: 2 waves per SIMD).
+static inline int bs2_waves_per_cu(int RT) { return RT <= 4 ? 20 : RT == 8 ? 16 : 8; }
+
+template <int RT>
+static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
+                              uint32_t fbn_base, const uint32_t *fbn, int r0, uint64_t sbs, uint32_t fbn_step,
+                              hipStream_t s) {
+  const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
+  const size_t ring_bytes = (size_t)Bs2Depth<RT>::enc * slotb;
+  const int G = sbs == (uint64_t)k * L
+                    ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT))
+                    : 1;
+  const size_t lds = pad16((uint32_t)(G * k * FEC_BS_COEF_ROW_BYTES(RT))) + ring_bytes;
+  const uint64_t groups = (nb + G - 1) / G;
+  hipLaunchKernelGGL((k_rlc_encode_bs2<RT>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r, L,
+                     c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups(), slotb);
+}
+
+template <int RT>
+static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
+                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
+                               uint8_t *dst) {
+  const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
+  const size_t ring_bytes = (size_t)Bs2Depth<RT>::dec * slotb;
+  const int G = bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, ring_bytes,
+                          bs2_waves_per_cu(RT));
+  const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + ring_bytes;
+  const uint64_t groups = (nb + G - 1) / G;
+  hipLaunchKernelGGL((k_rlc_recover_bs2<RT>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r, L,
+                     c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, slotb);
+}
+
+// The ring path applies to 16-B pieces (symbol_size >= 16) and blocks of at least D sources (one
+// epilogue in any wait window, see gen_bitslice.py body2).
+static int bs2_depth(int RT, bool enc) {
+  switch (RT) {
+    case 1: return enc ? Bs2Depth<1>::enc : Bs2Depth<1>::dec;
+    case 2: return enc ? Bs2Depth<2>::enc : Bs2Depth<2>::dec;
+    case 4: return enc ? Bs2Depth<4>::enc : Bs2Depth<4>::dec;
+    case 8: return enc ? Bs2Depth<8>::enc : Bs2Depth<8>::dec;
+    default: return enc ? Bs2Depth<16>::enc : Bs2Depth<16>::dec;
+  }
+}
+static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
+  return knob(K_RING) != 0 && cfg.vec == 16 && (int)k >= bs2_depth(rt, enc);
+}
+
+#define FEC_BS2_DISPATCH(FN, ...)                                                               \
+  switch (rt) {                                                                                \
+    case 1: FN<1>(__VA_ARGS__); break;  case 2: FN<2>(__VA_ARGS__); break;                    \
+    case 4: FN<4>(__VA_ARGS__); break;  case 8: FN<8>(__VA_ARGS__); break;                    \
+    default: FN<16>(__VA_ARGS__); break;                                                       \
+  }
+
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
   switch (rt * 100 + cfg.vec) {                                                    \
     case 116: FN<1, 16>(__VA_ARGS__); break;  case 108: FN<1, 8>(__VA_ARGS__); break;   \
@@ -1493,16 +1810,16 @@ static int bs_table_check() {
   if (dev < 0 || dev >= 64) return set_err(FECGPU_ERR_NO_DEVICE, "%s", "device index out of range");
   int st = g_tab_state[dev].load();
   if (st == 0) {
-    uint64_t *d = nullptr, h = 0;
+    uint64_t *d = nullptr, h[2] = {0, 0};
     hipStream_t ps;
     HIPCHK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
-    HIPCHK(hipMalloc(&d, sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&d, sizeof h));
     hipLaunchKernelGGL(fec_bs_case_table_addr, dim3(1), dim3(64), 0, ps, d);
-    HIPCHK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, ps));
+    HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, ps));
     HIPCHK(hipStreamSynchronize(ps));
     HIPCHK(hipFree(d));
     HIPCHK(hipStreamDestroy(ps));
-    st = (h != 0 && (h & 0xFFFF) == 0) ? 1 : -1;
+    st = (h[0] != 0 && (h[0] & 0xFFFF) == 0 && h[1] != 0 && (h[1] & 0xFFFF) == 0) ? 1 : -1;
     g_tab_state[dev].store(st);
   }
   if (st < 0) return set_err(FECGPU_ERR_HIP, "%s", "GF(256) case table is not 64 KiB-aligned in device memory");
@@ -1908,9 +2225,16 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
     const BsCfg cfg = pick_bs_cfg((int)symbol_size);
     const EncTile et = pick_enc_tile(r);
     const int rt = et.rt;
-    for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
-      FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                      (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
+    if (use_ring(rt, k, cfg, true) && et.waves == 1) {
+      for (int r0 = 0; r0 < (int)r; r0 += rt) {
+        FEC_BS2_DISPATCH(launch_encode_bs2, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
+                         (int)symbol_size, cfg, fbn_base, fbn, r0, (uint64_t)k * symbol_size, 1u, s)
+      }
+    } else {
+      for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
+        FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
+                        (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
+      }
     }
   }
   HIPCHK(hipGetLastError());
@@ -2097,10 +2421,17 @@ static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64
   if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const bool fused = (int)L.em <= rt;  // one pass covers every unknown of every block
+  const bool ring = use_ring(rt, k, cfg, false);
   for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-    FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
-                    (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
-                    (uint8_t *)dst)
+    if (ring) {
+      FEC_BS2_DISPATCH(launch_recover_bs2, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+                       (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
+                       (uint8_t *)dst)
+    } else {
+      FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+                      (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
+                      (uint8_t *)dst)
+    }
   }
   HIPCHK(hipGetLastError());
   return fused ? FECGPU_OK : launch_finalize(nblocks, k, r, status, recovered, ws, s);

@@ -149,27 +149,29 @@ def v(n):
     return f"v{n}"
 
 
-def emit_table():
-    lines = ['  .text', '  .p2align 16', '  .globl fec_bs_case_table', '  .hidden fec_bs_case_table', 'fec_bs_case_table:']
+def emit_table(sym="fec_bs_case_table", tl=None, th=None):
+    tl = tl or TL
+    th = th or TH
+    lines = ['  .text', '  .p2align 16', f'  .globl {sym}', f'  .hidden {sym}', f'{sym}:']
     # entry 0: the chain's end (a zero field) returns to the caller
     lines.append(f"  s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
-    lines.append(f"  .org fec_bs_case_table + {CASE_BYTES}")
+    lines.append(f"  .org {sym} + {CASE_BYTES}")
     for c in range(256):
         body = []
         for o, (nl, nh) in enumerate(case_rows(c)):
             if nl and nh:
-                body.append(f"v_bitop3_b32 v{o}, v{o}, {v(TL[nl])}, {v(TH[nh])} bitop3:0x96")
+                body.append(f"v_bitop3_b32 v{o}, v{o}, {v(tl[nl])}, {v(th[nh])} bitop3:0x96")
             elif nl:
-                body.append(f"v_xor_b32 v{o}, v{o}, {v(TL[nl])}")
+                body.append(f"v_xor_b32 v{o}, v{o}, {v(tl[nl])}")
             elif nh:
-                body.append(f"v_xor_b32 v{o}, v{o}, {v(TH[nh])}")
+                body.append(f"v_xor_b32 v{o}, v{o}, {v(th[nh])}")
         # chain tail: next repair's accumulators, next 16-bit case offset, jump (entry 0 returns)
         body += [f"s_add_u32 m0, m0, 8",
                  f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
                  f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}",
                  f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
         lines += ["  " + b for b in body]
-        lines.append(f"  .org fec_bs_case_table + {CASE_BYTES * (c + 2)}")
+        lines.append(f"  .org {sym} + {CASE_BYTES * (c + 2)}")
     return lines
 
 
@@ -196,11 +198,14 @@ def transpose_fwd(src_words):
     return out
 
 
-def transpose_inplace(regs):
+def transpose_inplace(regs, tmp=None):
+    """The three exchange rounds on 8 registers in place (an involution: words <-> bit planes).
+    tmp: 4 temporaries (two pairs, so consecutive exchanges overlap) or 2 (one pair)."""
+    tmp = tmp or TMP
     out = []
     for sh, mi, pairs in STAGES:
         for pi, (a, b) in enumerate(pairs):
-            t0, t1 = (TMP[0], TMP[1]) if pi % 2 == 0 else (TMP[2], TMP[3])
+            t0, t1 = (tmp[0], tmp[1]) if pi % 2 == 0 or len(tmp) < 4 else (tmp[2], tmp[3])
             out += [f"v_lshlrev_b32 v{t0}, {sh}, v{regs[b]}",
                     f"v_lshrrev_b32 v{t1}, {sh}, v{regs[a]}",
                     f"v_bitop3_b32 v{regs[a]}, s{S_MASK[mi]}, v{regs[a]}, v{t0} bitop3:0xca",
@@ -208,9 +213,9 @@ def transpose_inplace(regs):
     return out
 
 
-def combos():
+def combos(tl=None, th=None):
     out = []
-    for T, name in ((TL, "L"), (TH, "H")):
+    for T in (tl or TL, th or TH):
         out += [f"v_xor_b32 v{T[3]}, v{T[1]}, v{T[2]}",
                 f"v_xor_b32 v{T[5]}, v{T[1]}, v{T[4]}",
                 f"v_xor_b32 v{T[6]}, v{T[2]}, v{T[4]}",
@@ -462,6 +467,283 @@ def emit_function(mode, RT, VEC, P):
     return "\n".join(out), top
 
 
+# ============================================================================ v2: LDS-DMA ring
+# The source rows stream into a per-wave LDS ring by LDS-DMA (global_load_lds_dwordx4: one wave-
+# instruction moves up to 1 KiB, 16 B per lane, linear in memory and in LDS) issued D-1 sources
+# ahead, instead of into D-1 sets of VGPRs.  A step reads its 32 B per lane from the ring straight
+# into the plane registers and transposes them in place, so the data costs no VGPRs beyond the
+# 8 plane registers: the accumulators and the Four-Russians tables set the occupancy (RT <= 8:
+# 4 waves per SIMD instead of 3), and the ring depth only costs LDS.
+T2_BASE = int(os.environ.get("FEC_GEN2_BASE", "16"))  # v0 .. v(T2_BASE-1) stay with the compiler
+S_WSLOT, S_RSLOT, S_PEND, S_PRT, S_COPTR, S_WTAB = 93, 94, 95, 96, 97, 98  # S_WTAB: 98-99
+SGPR_CLOBBER2 = list(range(60, 100))
+CASE_TABLE2 = "fec_bs2_case_table"
+
+
+def regmap2(mode: str, ntmp: int = 4):
+    B = T2_BASE
+    assert B % 2 == 0
+    tl = {1: B, 2: B + 1, 4: B + 2, 8: B + 3}
+    th = {1: B + 4, 2: B + 5, 4: B + 6, 8: B + 7}
+    others = [3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15]
+    for i, n in enumerate(others):
+        tl[n] = B + 8 + i
+        th[n] = B + 19 + i
+    tmp = list(range(B + 30, B + 30 + ntmp))
+    nxt = B + 30 + ntmp + (ntmp & 1)
+    m = {"pl": list(range(B, B + 8)), "tl": tl, "th": th, "tmp": tmp}
+    if mode == "dec":
+        m.update(inptr=nxt, outptr=nxt + 1, naddr=nxt + 2, acc=nxt + 4)
+    else:
+        m["acc"] = nxt
+    return m
+
+
+def body2(mode: str, RT: int, D: int, NDMA: int):
+    """One group of blocks x one column chunk, sources through the LDS ring (see above).
+    Wait accounting: vmcnt counts DMAs and stores together in issue order.  Source s's DMAs were
+    issued D-1 steps ahead; the younger operations at its wait are the NDMA * (D-1) DMAs issued
+    since, plus -- during the D-1 steps after a block's epilogue -- that epilogue's 2 * rt stores.
+    Those steps take an out-of-line wait from a table indexed by rt; blocks are at least D sources
+    long (the wrapper sizes D <= k), so at most one epilogue is ever in the window."""
+    R = regmap2(mode)
+    PL, TLm, THm, TMPm = R["pl"], R["tl"], R["th"], R["tmp"]
+    acc_base = R["acc"]
+    assert acc_base + 8 * RT <= 256 and acc_base % 2 == 0
+    assert NDMA * (D - 1) + 2 * RT <= 63, "vmcnt is 6 bits"
+    L = []
+    a = L.append
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a(f"s_mov_b32 s{S_SAVEM0}, m0")
+    a(f"s_mov_b64 s[{S_SAVEEX}:{S_SAVEEX + 1}], exec")
+    for i, mk in enumerate(MASKS):
+        a(f"s_mov_b32 s{S_MASK[i]}, 0x{mk:08x}")
+    a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
+    a(f"s_add_u32 s{S_TAB}, s{S_TAB}, {CASE_TABLE2}@rel32@lo+4")
+    a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, {CASE_TABLE2}@rel32@hi+12")
+    a(f"s_lshr_b32 s{S_TABHI}, s{S_TAB}, 16")
+    a(f"s_mov_b32 s{S_TGT + 1}, s{S_TAB + 1}")
+    a(f"s_getpc_b64 s[{S_EPI}:{S_EPI + 1}]")
+    a(".Lepipc_%=:")
+    a(f"s_add_u32 s{S_EPI}, s{S_EPI}, .Lepi_%= - .Lepipc_%=")
+    a(f"s_addc_u32 s{S_EPI + 1}, s{S_EPI + 1}, 0")
+    a(f"s_getpc_b64 s[{S_WTAB}:{S_WTAB + 1}]")
+    a(".Lwtabpc_%=:")
+    a(f"s_add_u32 s{S_WTAB}, s{S_WTAB}, .Lwtab_%= - .Lwtabpc_%=")
+    a(f"s_addc_u32 s{S_WTAB + 1}, s{S_WTAB + 1}, 0")
+    for r in range(acc_base, acc_base + 8 * RT):
+        a(f"v_mov_b32 v{r}, 0")
+    a(f"s_mov_b32 s{S_COPTR}, %[coef]")
+    if mode == "enc":
+        a(f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], %[src]")
+        a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
+        a(f"s_mov_b32 s{S_JL}, 0")
+    else:
+        a(f"v_mov_b32 v{R['inptr']}, %[intab]")
+        a(f"ds_read_b64 v[{R['naddr']}:{R['naddr'] + 1}], v{R['inptr']}")  # source 0's address
+        a(f"v_add_u32 v{R['inptr']}, 8, v{R['inptr']}")
+        a(f"v_mov_b32 v{R['outptr']}, %[outtab]")
+    a(f"s_sub_u32 s{S_S}, %[nsrc], 1")
+    a(f"s_sub_u32 s{S_J}, %[k], 1")
+    a(f"s_sub_u32 s{S_T2}, %[nsrc], {D - 1}")
+    a(f"s_cselect_b32 s{S_T2}, 0, s{S_T2}")
+    a(f"s_mov_b32 s{S_WSLOT}, %[ring]")
+    a(f"s_mov_b32 s{S_RSLOT}, %[ring]")
+    a(f"s_mov_b32 s{S_PEND}, 0")
+
+    def dma_issue():
+        out = []
+        if mode == "dec":  # this source's address (read one DMA ago), then fetch the next one
+            out += ["s_waitcnt lgkmcnt(0)",
+                    f"v_readfirstlane_b32 s{S_CUR}, v{R['naddr']}",
+                    f"v_readfirstlane_b32 s{S_CUR + 1}, v{R['naddr'] + 1}",
+                    f"ds_read_b64 v[{R['naddr']}:{R['naddr'] + 1}], v{R['inptr']}",
+                    f"v_add_u32 v{R['inptr']}, 8, v{R['inptr']}",
+                    "s_nop 1"]  # VALU-written SGPR -> VMEM base: 5 wait states with the moves below
+        out += [f"s_mov_b32 m0, s{S_WSLOT}",
+                "s_mov_b64 exec, %[vmlo]",  # also the M0 -> LDS-DMA wait state
+                f"global_load_lds_dwordx4 %[g1], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
+        if NDMA == 2:
+            out += ["s_add_u32 m0, m0, 1024",
+                    "s_mov_b64 exec, %[vmhi]",
+                    f"global_load_lds_dwordx4 %[g2], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
+        out += [f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]",
+                f"s_add_u32 s{S_WSLOT}, s{S_WSLOT}, %[slotb]",
+                f"s_cmp_lt_u32 s{S_WSLOT}, %[ringend]",
+                f"s_cselect_b32 s{S_WSLOT}, s{S_WSLOT}, %[ring]"]
+        if mode == "enc":  # next row of this block, or the first row of the group's next block
+            out += [f"s_add_u32 s{S_JL}, s{S_JL}, 1",
+                    f"s_cmp_eq_u32 s{S_JL}, %[k]",
+                    f"s_cselect_b64 s[{S_CQ}:{S_CQ + 1}], %[sdl], %[ll]",
+                    f"s_cselect_b32 s{S_JL}, 0, s{S_JL}",
+                    f"s_add_u32 s{S_CUR}, s{S_CUR}, s{S_CQ}",
+                    f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_CQ + 1}"]
+        return out
+
+    for q in range(D - 1):  # prologue: DMAs for sources 0 .. D-2
+        a(f"s_cmp_lt_u32 {q}, %[nsrc]")
+        a(f"s_cbranch_scc0 .Lpro_done_%=")
+        L.extend(dma_issue())
+    a(".Lpro_done_%=:")
+    csb = coef_row_bytes(RT)
+    dsr = "ds_read_b64" if csb == 8 else "ds_read_b128"
+    ndw = min(4, csb // 4)
+    nch = max(1, RT // 4)
+    CO = TMPm[:ndw]
+    base_wait = NDMA * (D - 1)
+    ool = []
+    a(".Lstep_%=:")
+    a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
+    a(f"s_cbranch_scc1 .Lnodma_%=")
+    L.extend(dma_issue())
+    a(f"s_cmp_lg_u32 s{S_PEND}, 0")
+    a(f"s_cbranch_scc1 .Lbigwait_%=")
+    a(f"s_waitcnt vmcnt({base_wait})")
+    a(".Lgot_%=:")
+    ool += [".Lnodma_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", "s_branch .Lgot_%="]
+    ool += [".Lbigwait_%=:",
+            f"s_sub_u32 s{S_PEND}, s{S_PEND}, 1",
+            f"s_lshl_b32 s{S_CQ}, s{S_PRT}, 3",
+            f"s_add_u32 s{S_CQ}, s{S_CQ}, s{S_WTAB}",
+            f"s_addc_u32 s{S_CQ + 1}, s{S_WTAB + 1}, 0",
+            f"s_setpc_b64 s[{S_CQ}:{S_CQ + 1}]"]
+    # this source: 32 B per lane from the ring into the plane registers
+    a(f"v_add_u32 v{TMPm[0]}, s{S_RSLOT}, %[rd1]")
+    a(f"v_add_u32 v{TMPm[1]}, s{S_RSLOT}, %[rd2]")
+    a(f"ds_read_b128 v[{PL[0]}:{PL[3]}], v{TMPm[0]}")
+    a(f"ds_read_b128 v[{PL[4]}:{PL[7]}], v{TMPm[1]}")
+    a(f"s_add_u32 s{S_RSLOT}, s{S_RSLOT}, %[slotb]")
+    a(f"s_cmp_lt_u32 s{S_RSLOT}, %[ringend]")
+    a(f"s_cselect_b32 s{S_RSLOT}, s{S_RSLOT}, %[ring]")
+    a("s_waitcnt lgkmcnt(0)")
+    L.extend(transpose_inplace(PL, TMPm))
+    # coefficient fields (case offsets) into the temporaries under the combos
+    a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
+    a(f"{dsr} {regrange(CO[0], ndw)}, v{TMPm[3]}")
+    L.extend(combos(TLm, THm))
+    a("s_waitcnt lgkmcnt(0)")
+    for w in range(ndw):
+        a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+    if csb == 32:
+        a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
+        a(f"ds_read_b128 {regrange(CO[0], 4)}, v{TMPm[3]} offset:16")
+    a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
+    for ch in range(nch):
+        if ch == 2:
+            a("s_set_gpr_idx_off")
+            a("s_waitcnt lgkmcnt(0)")
+            for w in range(4):
+                a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+        a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
+        a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
+        if ch % 2 == 0:
+            a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+        a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+    a("s_set_gpr_idx_off")
+    a(f"s_sub_u32 s{S_J}, s{S_J}, 1")
+    a(f"s_cbranch_scc1 .Lepicall_%=")
+    a(".Lnoepi_%=:")
+    a(f"s_sub_u32 s{S_S}, s{S_S}, 1")
+    a(f"s_cbranch_scc1 .Lexit_%=")
+    a(f"s_branch .Lstep_%=")
+    ool += [".Lepicall_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
+            f"s_sub_u32 s{S_J}, %[k], 1", "s_branch .Lnoepi_%="]
+    L.extend(ool)
+    # the big-wait table: entry i (8 bytes) waits for source s with i repairs' stores in the window
+    a(".Lwtab_%=:")
+    for i in range(RT + 1):
+        a(f"s_waitcnt vmcnt({base_wait + 2 * i})")
+        a("s_branch .Lgot_%=")
+
+    # ---- per-block epilogue subroutine: inverse transpose, stores, clear; opens the big-wait window
+    a(".Lepi_%=:")
+    tmpA, tmpB = TMPm[2], TMPm[3]
+    if mode == "enc":
+        a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
+        a(f"s_mov_b32 s{S_RT}, %[rt]")
+    else:
+        a(f"ds_read_b32 v{tmpA}, v{R['outptr']} offset:{DEC_REC_RT}")
+        a("s_waitcnt lgkmcnt(0)")
+        a(f"v_readfirstlane_b32 s{S_RT}, v{tmpA}")
+    for i in range(RT):
+        accs = [acc_base + 8 * i + w for w in range(8)]
+        a(f"s_cmp_le_u32 s{S_RT}, {i}")
+        a(f"s_cbranch_scc1 .Lepi_done_%=")
+        L.extend(transpose_inplace(accs, TMPm))
+        if mode == "dec":
+            a(f"ds_read_b64 v[{tmpA}:{tmpB}], v{R['outptr']} offset:{8 * i}")
+            a(f"v_or3_b32 v{TMPm[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
+            a(f"v_or3_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[3]}, v{accs[4]}")
+            a(f"v_or3_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[5]}, v{accs[6]}")
+            a(f"v_or_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[7]}")
+            a(f"v_cmp_ne_u32 vcc, 0, v{TMPm[0]}")
+            a(f"v_mov_b32 v{TMPm[1]}, 1")
+            a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
+            a(f"ds_write_b8 v{R['outptr']}, v{TMPm[1]} offset:{DEC_REC_NZ + i}")
+            a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+            a("s_waitcnt lgkmcnt(0)")
+            a(f"v_readfirstlane_b32 s{S_O2}, v{tmpA}")
+            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{tmpB}")
+            a("s_nop 4")  # VALU-written SGPR -> VMEM base
+        for q in range(2):
+            a(f"s_mov_b64 exec, %[vm{q}]")
+            a(f"global_store_dwordx4 %[off{q}], {regrange(accs[4 * q], 4)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
+        a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+        if mode == "enc":
+            a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
+            a(f"s_addc_u32 s{S_O2 + 1}, s{S_O2 + 1}, 0")
+    a(".Lepi_done_%=:")
+    a(f"s_mov_b32 s{S_PRT}, s{S_RT}")
+    a(f"s_mov_b32 s{S_PEND}, {D - 1}")
+    for r in range(acc_base, acc_base + 8 * RT):
+        a(f"v_mov_b32 v{r}, 0")
+    if mode == "enc":
+        a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rslo]")
+        a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, %[rshi]")
+    else:
+        a(f"v_add_u32 v{R['outptr']}, {DEC_REC_BYTES}, v{R['outptr']}")
+    a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+    a(".Lexit_%=:")
+    a("s_waitcnt lgkmcnt(0)")
+    a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+    a(f"s_mov_b32 m0, s{S_SAVEM0}")
+    return L, acc_base + 8 * RT
+
+
+def emit_function2(mode, RT, D, NDMA):
+    lines, top = body2(mode, RT, D, NDMA)
+    name = f"bs2_{mode}_r{RT}_d{NDMA}"
+    common = ("uint32_t nsrc, uint32_t k, uint32_t coef, uint32_t ring, uint32_t ringend, uint32_t slotb, "
+              "uint32_t g1, uint32_t g2, uint64_t vmlo, uint64_t vmhi, uint32_t rd1, uint32_t rd2, "
+              "uint32_t off0, uint32_t off1, uint64_t vm0, uint64_t vm1")
+    if mode == "enc":
+        sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rslo, "
+               f"uint32_t rshi, uint64_t sdl, uint64_t ll, uint32_t rt, {common})")
+        ins = ['[src] "s"(src)', '[rep] "s"(rep)', '[L] "s"(L)', '[rslo] "s"(rslo)', '[rshi] "s"(rshi)',
+               '[sdl] "s"(sdl)', '[ll] "s"(ll)', '[rt] "s"(rt)']
+    else:
+        sig = f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, {common})"
+        ins = ['[intab] "v"(intab)', '[outtab] "v"(outtab)']
+    ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "s"(coef)', '[ring] "s"(ring)', '[ringend] "s"(ringend)',
+            '[slotb] "s"(slotb)', '[g1] "v"(g1)', '[g2] "v"(g2)', '[vmlo] "s"(vmlo)', '[vmhi] "s"(vmhi)',
+            '[rd1] "v"(rd1)', '[rd2] "v"(rd2)', '[off0] "v"(off0)', '[off1] "v"(off1)', '[vm0] "s"(vm0)',
+            '[vm1] "s"(vm1)']
+    clob = [f'"v{r}"' for r in range(T2_BASE, top)] + [f'"s{r}"' for r in SGPR_CLOBBER2] + ['"vcc"', '"scc"',
+                                                                                          '"memory"']
+    out = [sig + " {", "  asm volatile(", cstring(lines), "      :",
+           "      : " + ", ".join(ins), "      : " + ", ".join(clob) + ");", "}"]
+    return "\n".join(out), top
+
+
+RING_DEPTH = {("enc", 1): 4, ("enc", 2): 4, ("enc", 4): 4, ("enc", 8): 4, ("enc", 16): 8,
+              ("dec", 1): 4, ("dec", 2): 4, ("dec", 4): 4, ("dec", 8): 4, ("dec", 16): 8}
+
+
+def ring_depth(mode: str, RT: int) -> int:
+    return int(os.environ.get(f"FEC_GEN2_D_{mode.upper()}_RT{RT}") or os.environ.get("FEC_GEN2_D")
+               or RING_DEPTH[(mode, RT)])
+
+
 DEC_REC_BYTES = 160  # per-block decode record in LDS: 16 x 8 B output addresses | rt @136 | nz flags @144
 DEC_REC_RT = 136
 DEC_REC_NZ = 144
@@ -526,18 +808,34 @@ def main():
              '    "s_endpgm\\n"']
     parts += [f'    "{ln}\\n"' for ln in emit_table()]
     parts += ['    "  s_endpgm\\n");', "}", ""]
-    parts += ["// The table's runtime address (the case tails build targets as TAB.hi:TAB.lo[31:16]:offset,",
-              "// which needs 64 KiB alignment): the engine checks it once per device before any launch.",
+    # the LDS-ring bodies' table: the same cases over their plane-register numbering (regmap2)
+    R2 = regmap2("enc")
+    parts += ["// The same 256 cases over the LDS-ring bodies' plane registers (regmap2).",
+              "__global__ void fec_bs2_case_table_holder() {",
+              "  asm volatile(",
+              '    "s_endpgm\\n"']
+    parts += [f'    "{ln}\\n"' for ln in emit_table(CASE_TABLE2, R2["tl"], R2["th"])]
+    parts += ['    "  s_endpgm\\n");', "}", ""]
+    parts += ["// The tables' runtime addresses (the case tails build targets as TAB.hi:TAB.lo[31:16]:offset,",
+              "// which needs 64 KiB alignment): the engine checks them once per device before any launch.",
               "__global__ void fec_bs_case_table_addr(uint64_t *out) {",
-              "  uint32_t lo, hi;",
+              "  uint32_t lo, hi, lo2, hi2;",
               "  asm volatile(",
               '    "s_getpc_b64 s[60:61]\\n"',
               '    "s_add_u32 s60, s60, fec_bs_case_table@rel32@lo+4\\n"',
               '    "s_addc_u32 s61, s61, fec_bs_case_table@rel32@hi+12\\n"',
               '    "s_mov_b32 %0, s60\\n"',
               '    "s_mov_b32 %1, s61\\n"',
-              '    : "=s"(lo), "=s"(hi) : : "s60", "s61");',
-              "  if (threadIdx.x == 0) out[0] = ((uint64_t)hi << 32) | lo;",
+              '    "s_getpc_b64 s[60:61]\\n"',
+              f'    "s_add_u32 s60, s60, {CASE_TABLE2}@rel32@lo+4\\n"',
+              f'    "s_addc_u32 s61, s61, {CASE_TABLE2}@rel32@hi+12\\n"',
+              '    "s_mov_b32 %2, s60\\n"',
+              '    "s_mov_b32 %3, s61\\n"',
+              '    : "=s"(lo), "=s"(hi), "=s"(lo2), "=s"(hi2) : : "s60", "s61");',
+              "  if (threadIdx.x == 0) {",
+              "    out[0] = ((uint64_t)hi << 32) | lo;",
+              "    out[1] = ((uint64_t)hi2 << 32) | lo2;",
+              "  }",
               "}", ""]
     tops = {}
     for mode in ("enc", "dec"):
@@ -547,9 +845,19 @@ def main():
             tops[(mode, RT, VEC, P)] = top
             parts.append(fn)
             parts.append("")
+    parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
+    for mode in ("enc", "dec"):
+        for RT in (1, 2, 4, 8, 16):
+            D = ring_depth(mode, RT)
+            parts.append(f"#define FEC_BS2_D_{mode.upper()}_RT{RT} {D}")
+            for NDMA in (1, 2):
+                fn, top = emit_function2(mode, RT, D, NDMA)
+                tops[(mode + "2", RT, NDMA, D)] = top
+                parts.append(fn)
+                parts.append("")
     with open(OUT, "w") as f:
         f.write("\n".join(parts))
-    print(f"wrote {OUT}: {len(CONFIGS) * 2} bodies, max VGPR {max(tops.values())}")
+    print(f"wrote {OUT}: {len(CONFIGS) * 2} + 20 bodies, max VGPR {max(tops.values())}")
 
 
 if __name__ == "__main__":
