@@ -69,7 +69,8 @@ static void knobs_from_env() {
   g_knob[K_XOR_GENERIC] = num(getenv("FECGPU_XOR_GENERIC"), 0) != 0;
   g_knob[K_XOR_IDX64] = num(getenv("FECGPU_XOR_IDX64"), 0) != 0;
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
-  g_knob[K_RING] = num(getenv("FECGPU_RING"), 0);  // 1: the LDS-ring data path (bs2 bodies) where it applies
+  // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair encode tiles
+  g_knob[K_RING] = num(getenv("FECGPU_RING"), 2);
 }
 
 static inline int knob(KnobId id) {
@@ -1496,7 +1497,7 @@ struct Bs2Lanes {
   uint32_t g1, g2, rd1, rd2, off0, off1;
   uint64_t vmlo, vmhi, vm0, vm1;
   int npieces;
-  __device__ __forceinline__ Bs2Lanes(int lane, int cb, uint32_t c0) {
+  __device__ __forceinline__ Bs2Lanes(int lane, int cb, uint32_t c0, uint32_t ring) {
     npieces = (cb + 15) / 16;
     const int A = (npieces + 1) / 2;
     auto gofs = [&](int t) { return (uint32_t)(t * 16 < cb - 16 ? t * 16 : cb - 16); };
@@ -1507,8 +1508,8 @@ struct Bs2Lanes {
     vmhi = __ballot(d2);
     const int p1 = lane + A;
     const bool ok0 = lane < A, ok1 = lane < A && p1 < npieces;
-    rd1 = ok0 ? 16u * (uint32_t)lane : 0u;
-    rd2 = ok1 ? 16u * (uint32_t)p1 : 0u;
+    rd1 = ring + (ok0 ? 16u * (uint32_t)lane : 0u);  // LDS addresses in slot 0 (steps add the slot)
+    rd2 = ring + (ok1 ? 16u * (uint32_t)p1 : 0u);
     off0 = ok0 ? c0 + gofs(lane) : 0u;
     off1 = ok1 ? c0 + gofs(p1) : 0u;
     vm0 = __ballot(ok0);
@@ -1516,19 +1517,19 @@ struct Bs2Lanes {
   }
 };
 
-static inline uint32_t bs2_slot_bytes(int chunk_bytes) { return (uint32_t)((chunk_bytes + 127) / 128 * 128); }
+static inline uint32_t bs2_slot_bytes(int) { return FEC_BS2_SLOT; }  // the bodies address slots by immediates
 
 #define BS2_LANE_ARGS ln.g1, ln.g2, ln.vmlo, ln.vmhi, ln.rd1, ln.rd2, ln.off0, ln.off1, ln.vm0, ln.vm1
 #define BS2_CALL_ENC(RT, ND) \
-  bs2_enc_r##RT##_d##ND(sp, rpp, (uint32_t)L, rslo, rshi, sdl, ll, (uint32_t)rt, nsrc, (uint32_t)k, ca, ring, ringend, \
-                        slotb, BS2_LANE_ARGS)
+  bs2_enc_r##RT##_d##ND(sp, rpp, (uint32_t)L, rslo, rshi, sdl, ll, (uint32_t)rt, nsrc, (uint32_t)k, ca, ring, \
+                        BS2_LANE_ARGS)
 #define BS2_CALL_DEC(RT, ND) \
-  bs2_dec_r##RT##_d##ND(ia, oa, nsrc, (uint32_t)k, ca, ring, ringend, slotb, BS2_LANE_ARGS)
+  bs2_dec_r##RT##_d##ND(ia, oa, nsrc, (uint32_t)k, ca, ring, BS2_LANE_ARGS)
 
 template <int RT>
 __device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp, int L, uint32_t rslo, uint32_t rshi,
                                              uint64_t sdl, uint64_t ll, int rt, uint32_t nsrc, int k, uint32_t ca,
-                                             uint32_t ring, uint32_t ringend, uint32_t slotb, const Bs2Lanes &ln) {
+                                             uint32_t ring, const Bs2Lanes &ln) {
   if (two) {
     if constexpr (RT == 1) BS2_CALL_ENC(1, 2); else if constexpr (RT == 2) BS2_CALL_ENC(2, 2);
     else if constexpr (RT == 4) BS2_CALL_ENC(4, 2); else if constexpr (RT == 8) BS2_CALL_ENC(8, 2);
@@ -1542,7 +1543,7 @@ __device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp
 
 template <int RT>
 __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa, uint32_t nsrc, int k, uint32_t ca,
-                                             uint32_t ring, uint32_t ringend, uint32_t slotb, const Bs2Lanes &ln) {
+                                             uint32_t ring, const Bs2Lanes &ln) {
   if (two) {
     if constexpr (RT == 1) BS2_CALL_DEC(1, 2); else if constexpr (RT == 2) BS2_CALL_DEC(2, 2);
     else if constexpr (RT == 4) BS2_CALL_DEC(4, 2); else if constexpr (RT == 8) BS2_CALL_DEC(8, 2);
@@ -1554,18 +1555,26 @@ __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa,
   }
 }
 
+// W waves per workgroup split a group's repairs (wave w: repairs r0 + w RT ..), each with its own
+// coefficient rows and ring; they read the same source rows close together in time (L2 serves the
+// repeats).  W = 1 unless a tile knob asks for more.
 template <int RT>
-__global__ __launch_bounds__(64) void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
-                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
-                                                       int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
-                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
-                                                       uint32_t slotb) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? 3 : 1)))
+void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
+                                                        int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
+                                                        uint32_t slotb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
   constexpr int D = Bs2Depth<RT>::enc;
-  const uint32_t ring = lds_addr(lds) + pad16((uint32_t)(G * k * CSB)), ringend = ring + D * slotb;
-  const int rt = r - r0 < RT ? r - r0 : RT;
+  const uint32_t per_wave = pad16((uint32_t)(G * k * CSB)) + D * slotb;
+  uint8_t *lds = lds_all + (size_t)wave * per_wave;
+  const uint32_t ring = lds_addr(lds) + pad16((uint32_t)(G * k * CSB));
+  r0 += wave * RT;
+  const int rt = r - r0 < RT ? r - r0 : RT;  // <= 0: this wave has no repairs (waits at barriers)
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
@@ -1592,10 +1601,11 @@ __global__ __launch_bounds__(64) void k_rlc_encode_bs2(const uint8_t *__restrict
       }
     }
     __syncthreads();
+    if (rt <= 0) continue;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-      const Bs2Lanes ln(lane, cb, 0u);
+      const Bs2Lanes ln(lane, cb, 0u, ring);
       const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);
       const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L + c0);
       const uint64_t rstep = bstep * (uint64_t)r * L;
@@ -1603,7 +1613,7 @@ __global__ __launch_bounds__(64) void k_rlc_encode_bs2(const uint8_t *__restrict
       const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
       const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
       bs2_enc_call<RT>(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
-                       ringend, slotb, ln);
+                       ln);
     }
   }
 }
@@ -1618,9 +1628,7 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs2(uint8_t *__restrict__ sr
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   RecoverLds<RT> S(lds, G, k);
-  constexpr int D = Bs2Depth<RT>::dec;
-  const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k)),
-                 ringend = ring + D * slotb;
+  const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k));
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
@@ -1686,9 +1694,9 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs2(uint8_t *__restrict__ sr
       for (int ch = 0; ch < nchunks; ch++) {
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-        const Bs2Lanes ln(lane, cb, (uint32_t)c0);
+        const Bs2Lanes ln(lane, cb, (uint32_t)c0, ring);
         bs2_dec_call<RT>(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
-                         lds_addr(S.coef), ring, ringend, slotb, ln);
+                         lds_addr(S.coef), ring, ln);
       }
     }
     __syncthreads();
@@ -1734,20 +1742,22 @@ static inline int bs2_group(int RT, int k, int per_j, int per_block, bool enc, i
 
 // Target waves per CU for the ring kernels (VGPR-limited occupancy of the bodies: RT <= 4: 5,
 // RT = 8: 4, RT = 16: 2 waves per SIMD).
-static inline int bs2_waves_per_cu(int RT) { return RT <= 4 ? 20 : RT == 8 ? 16 : 8; }
+// resident waves per CU the LDS budget is sized for (RT = 16 reaches 3 per SIMD only with the
+// two-temporary register map of a FEC_GEN2_BASE=8 build)
+static inline int bs2_waves_per_cu(int RT) { return RT <= 4 ? 20 : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 12 : 8; }
 
 template <int RT>
 static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
-                              uint32_t fbn_base, const uint32_t *fbn, int r0, uint64_t sbs, uint32_t fbn_step,
+                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                               hipStream_t s) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth<RT>::enc * slotb;
   const int G = sbs == (uint64_t)k * L
                     ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT))
                     : 1;
-  const size_t lds = pad16((uint32_t)(G * k * FEC_BS_COEF_ROW_BYTES(RT))) + ring_bytes;
+  const size_t lds = (size_t)W * (pad16((uint32_t)(G * k * FEC_BS_COEF_ROW_BYTES(RT))) + ring_bytes);
   const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_encode_bs2<RT>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r, L,
+  hipLaunchKernelGGL((k_rlc_encode_bs2<RT>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k, r, L,
                      c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups(), slotb);
 }
 
@@ -1777,7 +1787,9 @@ static int bs2_depth(int RT, bool enc) {
   }
 }
 static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
-  return knob(K_RING) != 0 && cfg.vec == 16 && (int)k >= bs2_depth(rt, enc);
+  const int m = knob(K_RING);
+  if (m == 0 || cfg.vec != 16 || (int)k < bs2_depth(rt, enc)) return false;
+  return m == 1 || (rt == 16 && enc);
 }
 
 #define FEC_BS2_DISPATCH(FN, ...)                                                               \
@@ -2225,10 +2237,10 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
     const BsCfg cfg = pick_bs_cfg((int)symbol_size);
     const EncTile et = pick_enc_tile(r);
     const int rt = et.rt;
-    if (use_ring(rt, k, cfg, true) && et.waves == 1) {
-      for (int r0 = 0; r0 < (int)r; r0 += rt) {
+    if (use_ring(rt, k, cfg, true)) {
+      for (int r0 = 0; r0 < (int)r; r0 += rt * et.waves) {
         FEC_BS2_DISPATCH(launch_encode_bs2, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                         (int)symbol_size, cfg, fbn_base, fbn, r0, (uint64_t)k * symbol_size, 1u, s)
+                         (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
       }
     } else {
       for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {

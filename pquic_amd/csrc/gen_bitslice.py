@@ -345,27 +345,43 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
         a(f"s_cbranch_scc1 .Lnopf{b}_%=")
         L.extend(load_source(nb))
-        a(f"s_waitcnt vmcnt({NP * (P - 1)})")
+        # FEC_GEN_NOVMWAIT=1 (timing probe only, results are garbage): no wait for the source rows
+        a(f"s_waitcnt vmcnt({63 if os.environ.get('FEC_GEN_NOVMWAIT') else NP * (P - 1)})")
         a(f".Lpf{b}_%=:")
         ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
         L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
+        # FEC_GEN_CONSTCOEF=1 (timing probe only, results are garbage): every live field is the
+        # case of one fixed coefficient and no coefficient row is read
+        constco = bool(os.environ.get("FEC_GEN_CONSTCOEF"))
+        fld = (0x53 + 1) * CASE_BYTES
+
+        def const_fields():
+            for w in range(ndw if csb < 32 else 4):
+                lo = fld if 2 * w < RT else 0
+                hi = fld if 2 * w + 1 < RT else 0
+                a(f"s_mov_b32 s{S_C[w]}, 0x{(hi << 16) | lo:08x}")
         # the coefficient fields land in the (now free) transpose temporaries under the combos
-        a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
-        if csb <= 16:
-            a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
+        if not constco:
+            a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
+            if csb <= 16:
+                a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
         L.extend(combos())
-        a("s_waitcnt lgkmcnt(0)")
-        for w in range(ndw):
-            a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-        if csb == 32:  # second half of the offsets lands while the first two chains run
+        if constco:
+            const_fields()
+        else:
+            a("s_waitcnt lgkmcnt(0)")
+            for w in range(ndw):
+                a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+        if csb == 32 and not constco:  # second half of the offsets lands while the first two chains run
             a(f"ds_read_b128 {regrange(CO[0], 4)}, v{COPTR} offset:16")
             a(f"v_add_u32 v{COPTR}, 32, v{COPTR}")
         for ch in range(nch):
             if ch == 2:  # RT = 16: offsets 8..15 (no VALU may run in GPR-index mode)
                 a("s_set_gpr_idx_off")
-                a("s_waitcnt lgkmcnt(0)")
-                for w in range(4):
-                    a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+                if not constco:
+                    a("s_waitcnt lgkmcnt(0)")
+                    for w in range(4):
+                        a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
             a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
             a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
             if ch % 2 == 0:  # chain 1 continues M0 where chain 0 left it (4 cases later)
@@ -474,8 +490,8 @@ def emit_function(mode, RT, VEC, P):
 # into the plane registers and transposes them in place, so the data costs no VGPRs beyond the
 # 8 plane registers: the accumulators and the Four-Russians tables set the occupancy (RT <= 8:
 # 4 waves per SIMD instead of 3), and the ring depth only costs LDS.
-T2_BASE = int(os.environ.get("FEC_GEN2_BASE", "16"))  # v0 .. v(T2_BASE-1) stay with the compiler
-S_WSLOT, S_RSLOT, S_PEND, S_PRT, S_COPTR, S_WTAB = 93, 94, 95, 96, 97, 98  # S_WTAB: 98-99
+T2_BASE = int(os.environ.get("FEC_GEN2_BASE", "8"))  # v0 .. v(T2_BASE-1) stay with the compiler
+S_PEND, S_PRT, S_COPTR, S_WTAB = 95, 96, 97, 98  # S_WTAB: 98-99
 SGPR_CLOBBER2 = list(range(60, 100))
 CASE_TABLE2 = "fec_bs2_case_table"
 
@@ -499,23 +515,33 @@ def regmap2(mode: str, ntmp: int = 4):
     return m
 
 
+S2_SLOT = 2048  # bytes per ring slot: a whole column chunk; the unrolled steps address slots by immediates
+
+
 def body2(mode: str, RT: int, D: int, NDMA: int):
     """One group of blocks x one column chunk, sources through the LDS ring (see above).
-    Wait accounting: vmcnt counts DMAs and stores together in issue order.  Source s's DMAs were
-    issued D-1 steps ahead; the younger operations at its wait are the NDMA * (D-1) DMAs issued
-    since, plus -- during the D-1 steps after a block's epilogue -- that epilogue's 2 * rt stores.
-    Those steps take an out-of-line wait from a table indexed by rt; blocks are at least D sources
-    long (the wrapper sizes D <= k), so at most one epilogue is ever in the window."""
-    R = regmap2(mode)
+    The step is unrolled D times, so step b reads ring slot b and refills slot (b + D - 1) % D with
+    immediate offsets (no slot arithmetic).  A step waits for its source's DMAs, issues the reads of
+    its 32 B per lane, and only then issues the next DMA (the LDS latency hides under it).
+    Wait accounting: vmcnt counts DMAs and stores together in issue order.  At source s's wait the
+    younger operations are the NDMA * (D-2) DMAs of sources s+1 .. s+D-2, plus -- during the D-1
+    steps after a block's epilogue -- that epilogue's 2 * rt stores; those steps take their wait from
+    a table indexed by rt.  Blocks are at least D sources long (the wrapper sizes D <= k), so at most
+    one epilogue is ever in the window.  Steps that issue no DMA (the last D-1) wait for everything."""
+    NT = int(os.environ.get("FEC_GEN2_NTMP", "2")) if mode == "enc" else 4
+    R = regmap2(mode, NT)
     PL, TLm, THm, TMPm = R["pl"], R["tl"], R["th"], R["tmp"]
+    XT = [TLm[3], TLm[5], TLm[6], TLm[7]]  # dead until the combos: the forward transpose's temporaries
     acc_base = R["acc"]
     assert acc_base + 8 * RT <= 256 and acc_base % 2 == 0
-    assert NDMA * (D - 1) + 2 * RT <= 63, "vmcnt is 6 bits"
+    assert D >= 3 and NDMA * (D - 2) + 2 * RT <= 63, "vmcnt is 6 bits"
+    assert (D - 1) * S2_SLOT < 65536, "ds_read offsets are 16 bits"
     L = []
     a = L.append
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a(f"s_mov_b32 s{S_SAVEM0}, m0")
     a(f"s_mov_b64 s[{S_SAVEEX}:{S_SAVEEX + 1}], exec")
+    a("s_mov_b64 exec, %[vm0]")  # compute on the lanes that own pieces (the DMAs set their own)
     for i, mk in enumerate(MASKS):
         a(f"s_mov_b32 s{S_MASK[i]}, 0x{mk:08x}")
     a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
@@ -547,30 +573,27 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     a(f"s_sub_u32 s{S_J}, %[k], 1")
     a(f"s_sub_u32 s{S_T2}, %[nsrc], {D - 1}")
     a(f"s_cselect_b32 s{S_T2}, 0, s{S_T2}")
-    a(f"s_mov_b32 s{S_WSLOT}, %[ring]")
-    a(f"s_mov_b32 s{S_RSLOT}, %[ring]")
     a(f"s_mov_b32 s{S_PEND}, 0")
 
-    def dma_issue():
+    def dma_issue(slot, lgkm_older=0):
+        """DMA of row S_CUR into ring slot `slot`; decode first takes the row's address (read one
+        DMA ago; `lgkm_older` LDS reads were issued after it)."""
         out = []
-        if mode == "dec":  # this source's address (read one DMA ago), then fetch the next one
-            out += ["s_waitcnt lgkmcnt(0)",
+        if mode == "dec":
+            out += [f"s_waitcnt lgkmcnt({lgkm_older})",
                     f"v_readfirstlane_b32 s{S_CUR}, v{R['naddr']}",
                     f"v_readfirstlane_b32 s{S_CUR + 1}, v{R['naddr'] + 1}",
                     f"ds_read_b64 v[{R['naddr']}:{R['naddr'] + 1}], v{R['inptr']}",
                     f"v_add_u32 v{R['inptr']}, 8, v{R['inptr']}",
                     "s_nop 1"]  # VALU-written SGPR -> VMEM base: 5 wait states with the moves below
-        out += [f"s_mov_b32 m0, s{S_WSLOT}",
+        out += [f"s_add_u32 m0, %[ring], {slot * S2_SLOT}",
                 "s_mov_b64 exec, %[vmlo]",  # also the M0 -> LDS-DMA wait state
                 f"global_load_lds_dwordx4 %[g1], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
         if NDMA == 2:
             out += ["s_add_u32 m0, m0, 1024",
                     "s_mov_b64 exec, %[vmhi]",
                     f"global_load_lds_dwordx4 %[g2], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
-        out += [f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]",
-                f"s_add_u32 s{S_WSLOT}, s{S_WSLOT}, %[slotb]",
-                f"s_cmp_lt_u32 s{S_WSLOT}, %[ringend]",
-                f"s_cselect_b32 s{S_WSLOT}, s{S_WSLOT}, %[ring]"]
+        out += ["s_mov_b64 exec, %[vm0]"]
         if mode == "enc":  # next row of this block, or the first row of the group's next block
             out += [f"s_add_u32 s{S_JL}, s{S_JL}, 1",
                     f"s_cmp_eq_u32 s{S_JL}, %[k]",
@@ -580,84 +603,108 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                     f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_CQ + 1}"]
         return out
 
-    for q in range(D - 1):  # prologue: DMAs for sources 0 .. D-2
+    for q in range(D - 1):  # prologue: DMAs for sources 0 .. D-2 into slots 0 .. D-2
         a(f"s_cmp_lt_u32 {q}, %[nsrc]")
         a(f"s_cbranch_scc0 .Lpro_done_%=")
-        L.extend(dma_issue())
+        L.extend(dma_issue(q))
     a(".Lpro_done_%=:")
     csb = coef_row_bytes(RT)
     dsr = "ds_read_b64" if csb == 8 else "ds_read_b128"
     ndw = min(4, csb // 4)
     nch = max(1, RT // 4)
-    CO = TMPm[:ndw]
-    base_wait = NDMA * (D - 1)
+    base_wait = NDMA * (D - 2)
     ool = []
-    a(".Lstep_%=:")
-    a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
-    a(f"s_cbranch_scc1 .Lnodma_%=")
-    L.extend(dma_issue())
-    a(f"s_cmp_lg_u32 s{S_PEND}, 0")
-    a(f"s_cbranch_scc1 .Lbigwait_%=")
-    a(f"s_waitcnt vmcnt({base_wait})")
-    a(".Lgot_%=:")
-    ool += [".Lnodma_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", "s_branch .Lgot_%="]
-    ool += [".Lbigwait_%=:",
-            f"s_sub_u32 s{S_PEND}, s{S_PEND}, 1",
-            f"s_lshl_b32 s{S_CQ}, s{S_PRT}, 3",
-            f"s_add_u32 s{S_CQ}, s{S_CQ}, s{S_WTAB}",
-            f"s_addc_u32 s{S_CQ + 1}, s{S_WTAB + 1}, 0",
-            f"s_setpc_b64 s[{S_CQ}:{S_CQ + 1}]"]
-    # this source: 32 B per lane from the ring into the plane registers
-    a(f"v_add_u32 v{TMPm[0]}, s{S_RSLOT}, %[rd1]")
-    a(f"v_add_u32 v{TMPm[1]}, s{S_RSLOT}, %[rd2]")
-    a(f"ds_read_b128 v[{PL[0]}:{PL[3]}], v{TMPm[0]}")
-    a(f"ds_read_b128 v[{PL[4]}:{PL[7]}], v{TMPm[1]}")
-    a(f"s_add_u32 s{S_RSLOT}, s{S_RSLOT}, %[slotb]")
-    a(f"s_cmp_lt_u32 s{S_RSLOT}, %[ringend]")
-    a(f"s_cselect_b32 s{S_RSLOT}, s{S_RSLOT}, %[ring]")
-    a("s_waitcnt lgkmcnt(0)")
-    L.extend(transpose_inplace(PL, TMPm))
-    # coefficient fields (case offsets) into the temporaries under the combos
-    a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
-    a(f"{dsr} {regrange(CO[0], ndw)}, v{TMPm[3]}")
-    L.extend(combos(TLm, THm))
-    a("s_waitcnt lgkmcnt(0)")
-    for w in range(ndw):
-        a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-    if csb == 32:
-        a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
-        a(f"ds_read_b128 {regrange(CO[0], 4)}, v{TMPm[3]} offset:16")
-    a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
-    for ch in range(nch):
-        if ch == 2:
-            a("s_set_gpr_idx_off")
+
+    def data_reads(b):
+        return [f"ds_read_b128 v[{PL[0]}:{PL[3]}], %[rd1] offset:{b * S2_SLOT}",
+                f"ds_read_b128 v[{PL[4]}:{PL[7]}], %[rd2] offset:{b * S2_SLOT}"]
+
+    for b in range(D):
+        a(f".Lstep{b}_%=:")
+        a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
+        a(f"s_cbranch_scc1 .Lnodma{b}_%=")
+        a(f"s_cmp_lg_u32 s{S_PEND}, 0")
+        a(f"s_cbranch_scc1 .Lbigwait{b}_%=")
+        a(f"s_waitcnt vmcnt({base_wait})")
+        a(f".Lgot{b}_%=:")
+        L.extend(data_reads(b))
+        L.extend(dma_issue((b + D - 1) % D, lgkm_older=2))
+        a(f".Lrd{b}_%=:")
+        ool += [f".Lnodma{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)"] + data_reads(b) + \
+               [f"s_branch .Lrd{b}_%="]
+        ool += [f".Lbigwait{b}_%=:",
+                f"s_sub_u32 s{S_PEND}, s{S_PEND}, 1",
+                f"s_lshl_b32 s{S_CQ}, s{S_PRT}, 3",
+                f"s_add_u32 s{S_CQ}, s{S_CQ}, s{S_WTAB}",
+                f"s_addc_u32 s{S_CQ + 1}, s{S_WTAB + 1}, 0",
+                f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_CQ}:{S_CQ + 1}]",
+                f"s_branch .Lgot{b}_%="]
+        # the first coefficient fields go out behind the data reads (one wait covers both)
+        if NT >= 4:
+            a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
+            a(f"{dsr} {regrange(TMPm[0], ndw)}, v{TMPm[3]}")
+        else:
+            a(f"v_mov_b32 v{TMPm[1]}, s{S_COPTR}")
+            a(f"ds_read_b64 v[{TMPm[0]}:{TMPm[1]}], v{TMPm[1]}")
+        a("s_waitcnt lgkmcnt(1)")
+        L.extend(transpose_inplace(PL, XT))
+        L.extend(combos(TLm, THm))
+        if NT >= 4:
+            CO = TMPm[:ndw]
             a("s_waitcnt lgkmcnt(0)")
-            for w in range(4):
+            for w in range(ndw):
                 a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-        a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
-        a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
-        if ch % 2 == 0:
-            a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
-        a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
-    a("s_set_gpr_idx_off")
-    a(f"s_sub_u32 s{S_J}, s{S_J}, 1")
-    a(f"s_cbranch_scc1 .Lepicall_%=")
-    a(".Lnoepi_%=:")
-    a(f"s_sub_u32 s{S_S}, s{S_S}, 1")
-    a(f"s_cbranch_scc1 .Lexit_%=")
-    a(f"s_branch .Lstep_%=")
-    ool += [".Lepicall_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
-            f"s_sub_u32 s{S_J}, %[k], 1", "s_branch .Lnoepi_%="]
+            if csb == 32:
+                a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
+                a(f"ds_read_b128 {regrange(CO[0], 4)}, v{TMPm[3]} offset:16")
+            a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
+            for ch in range(nch):
+                if ch == 2:
+                    a("s_set_gpr_idx_off")
+                    a("s_waitcnt lgkmcnt(0)")
+                    for w in range(4):
+                        a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+                a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
+                a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
+                if ch % 2 == 0:
+                    a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+        else:
+            # two temporaries: each chain's 4 fields (8 B) are read while the previous chain runs
+            T0, T1 = TMPm[0], TMPm[1]
+            for ch in range(nch):
+                if ch:
+                    a("s_set_gpr_idx_off")
+                a("s_waitcnt lgkmcnt(0)")
+                a(f"v_readfirstlane_b32 s{S_C[0]}, v{T0}")
+                a(f"v_readfirstlane_b32 s{S_C[1]}, v{T1}")
+                if ch + 1 < nch:
+                    a(f"v_mov_b32 v{T1}, s{S_COPTR}")
+                    a(f"ds_read_b64 v[{T0}:{T1}], v{T1} offset:{8 * (ch + 1)}")
+                a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[0]}:{S_C[1]}]")
+                a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
+                a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+            a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
+        a("s_set_gpr_idx_off")
+        a(f"s_sub_u32 s{S_J}, s{S_J}, 1")
+        a(f"s_cbranch_scc1 .Lepicall{b}_%=")
+        a(f".Lnoepi{b}_%=:")
+        a(f"s_sub_u32 s{S_S}, s{S_S}, 1")
+        a(f"s_cbranch_scc1 .Lexit_%=")
+        ool += [f".Lepicall{b}_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
+                f"s_sub_u32 s{S_J}, %[k], 1", f"s_branch .Lnoepi{b}_%="]
+    a(f"s_branch .Lstep0_%=")
     L.extend(ool)
     # the big-wait table: entry i (8 bytes) waits for source s with i repairs' stores in the window
     a(".Lwtab_%=:")
     for i in range(RT + 1):
         a(f"s_waitcnt vmcnt({base_wait + 2 * i})")
-        a("s_branch .Lgot_%=")
+        a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
 
     # ---- per-block epilogue subroutine: inverse transpose, stores, clear; opens the big-wait window
     a(".Lepi_%=:")
-    tmpA, tmpB = TMPm[2], TMPm[3]
+    tmpA, tmpB = TMPm[-2], TMPm[-1]
     if mode == "enc":
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
@@ -680,7 +727,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
             a(f"v_mov_b32 v{TMPm[1]}, 1")
             a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
             a(f"ds_write_b8 v{R['outptr']}, v{TMPm[1]} offset:{DEC_REC_NZ + i}")
-            a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+            a("s_mov_b64 exec, %[vm0]")
             a("s_waitcnt lgkmcnt(0)")
             a(f"v_readfirstlane_b32 s{S_O2}, v{tmpA}")
             a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{tmpB}")
@@ -688,7 +735,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         for q in range(2):
             a(f"s_mov_b64 exec, %[vm{q}]")
             a(f"global_store_dwordx4 %[off{q}], {regrange(accs[4 * q], 4)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
-        a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+        a("s_mov_b64 exec, %[vm0]")
         if mode == "enc":
             a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
             a(f"s_addc_u32 s{S_O2 + 1}, s{S_O2 + 1}, 0")
@@ -713,7 +760,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
 def emit_function2(mode, RT, D, NDMA):
     lines, top = body2(mode, RT, D, NDMA)
     name = f"bs2_{mode}_r{RT}_d{NDMA}"
-    common = ("uint32_t nsrc, uint32_t k, uint32_t coef, uint32_t ring, uint32_t ringend, uint32_t slotb, "
+    common = ("uint32_t nsrc, uint32_t k, uint32_t coef, uint32_t ring, "
               "uint32_t g1, uint32_t g2, uint64_t vmlo, uint64_t vmhi, uint32_t rd1, uint32_t rd2, "
               "uint32_t off0, uint32_t off1, uint64_t vm0, uint64_t vm1")
     if mode == "enc":
@@ -724,8 +771,7 @@ def emit_function2(mode, RT, D, NDMA):
     else:
         sig = f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, {common})"
         ins = ['[intab] "v"(intab)', '[outtab] "v"(outtab)']
-    ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "s"(coef)', '[ring] "s"(ring)', '[ringend] "s"(ringend)',
-            '[slotb] "s"(slotb)', '[g1] "v"(g1)', '[g2] "v"(g2)', '[vmlo] "s"(vmlo)', '[vmhi] "s"(vmhi)',
+    ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "s"(coef)', '[ring] "s"(ring)', '[g1] "v"(g1)', '[g2] "v"(g2)', '[vmlo] "s"(vmlo)', '[vmhi] "s"(vmhi)',
             '[rd1] "v"(rd1)', '[rd2] "v"(rd2)', '[off0] "v"(off0)', '[off1] "v"(off1)', '[vm0] "s"(vm0)',
             '[vm1] "s"(vm1)']
     clob = [f'"v{r}"' for r in range(T2_BASE, top)] + [f'"s{r}"' for r in SGPR_CLOBBER2] + ['"vcc"', '"scc"',
@@ -735,7 +781,7 @@ def emit_function2(mode, RT, D, NDMA):
     return "\n".join(out), top
 
 
-RING_DEPTH = {("enc", 1): 4, ("enc", 2): 4, ("enc", 4): 4, ("enc", 8): 4, ("enc", 16): 8,
+RING_DEPTH = {("enc", 1): 4, ("enc", 2): 4, ("enc", 4): 4, ("enc", 8): 4, ("enc", 16): 4,
               ("dec", 1): 4, ("dec", 2): 4, ("dec", 4): 4, ("dec", 8): 4, ("dec", 16): 8}
 
 
@@ -846,6 +892,7 @@ def main():
             parts.append(fn)
             parts.append("")
     parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
+    parts.append(f"#define FEC_BS2_SLOT {S2_SLOT}  // ring slot bytes (the bodies address slots by immediates)")
     for mode in ("enc", "dec"):
         for RT in (1, 2, 4, 8, 16):
             D = ring_depth(mode, RT)

@@ -679,13 +679,21 @@ def test_roundtrip_k32_e8(eng, oracle):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 300), (32, 8, 1200, 100), (7, 5, 2052, 60), (64, 16, 9000, 6)])
-def test_perm_datapath_vs_oracle(eng, oracle, k, r, L, nb):
-    """The v_perm data path (knob datapath_perm, kept for A/B against the bitsliced one) gives
-    the same encode and decode bytes as the oracle."""
+ALT_PATH_CASES = [(16, 4, 1200, 300), (32, 8, 1200, 100), (7, 5, 2052, 60), (64, 16, 9000, 6)]
+RING_CASES = ALT_PATH_CASES + [(8, 1, 1200, 90), (10, 2, 16, 70), (9, 16, 1040, 50), (40, 16, 4100, 7),
+                               (33, 9, 2048, 40), (4, 3, 20, 65)]
+
+
+@pytest.mark.parametrize("knob,k,r,L,nb", [("datapath_perm",) + c for c in ALT_PATH_CASES] +
+                         [("ring",) + c for c in RING_CASES])
+def test_alt_datapath_vs_oracle(eng, oracle, knob, k, r, L, nb):
+    """The v_perm data path (knob datapath_perm) and the LDS-DMA ring data path (knob ring), kept
+    for A/B against the default bitsliced one, give the same encode and decode bytes as the
+    oracle (the ring path over tiles of 1..16 repairs, one and two DMAs per row, several chunks,
+    short blocks that fall back to the default path)."""
     rng = np.random.default_rng(k + 7 * r)
     src_h = synth_bytes(nb * k * L, 3 + k).reshape(nb, k, L)
-    with eng.knob("datapath_perm", 1):
+    with eng.knob(knob, 1):
         src = to_dev(src_h)
         rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
         eng.rlc_encode(src, rep, k, r, L, fbn_base=41)

@@ -4,7 +4,8 @@ prints median kernel times.  Removes the process-to-process variance (buffer pla
 dominates whole-bench A/B runs.
 A variant may also name another build of the library: "name:LIB=pquic_amd/lib/variants/X/libpquic_fec.so"
 (loaded side by side under its own handle).
-usage: python tools/ab_inproc.py "name:VAR=VAL,VAR=VAL" ... [--cycles N] [--reps R]"""
+usage: python tools/ab_inproc.py "name:VAR=VAL,VAR=VAL" ... [--cycles N] [--reps R] [--case=mode:k:r:nblocks:L ...]
+[--only: drop the three default cases]"""
 import os
 import statistics
 import sys
@@ -89,6 +90,11 @@ if "--apply-to" in sys.argv:  # decode with the recovered rows written to a sepa
     CASES += [(16, 4, 1 << 20, "decto", 1200)]
 if "--frames" in sys.argv:  # repair symbols -> FEC frames in 1216-B slots (the bench's frames leg)
     CASES += [(16, 4, 1 << 20, "frames", 1200)]
+for spec in (a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")):  # mode:k:r:nblocks:L
+    m, kk, rr, nn, ll = spec.split(":")
+    CASES.append((int(kk), int(rr), int(nn), m, int(ll)))
+if "--only" in sys.argv:
+    CASES = CASES[3:]
 for (k, r, nb, mode, L) in CASES:
     bufs = setup(k, r, nb, min(k, r), L)
     cases.append((f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L, bufs))
@@ -113,6 +119,7 @@ def run(case, eng):
 
 defaults = {(name, kn): engines[name].get_knob(kn) for name, _ in variants for kn in knobs}
 times = {(v[0], c[0]): [] for v in variants for c in cases}
+digests = {}
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 for cyc in range(cycles):
     for name, env in variants:
@@ -122,6 +129,13 @@ for cyc in range(cycles):
             e.set_knob(kn, want.get(kn, defaults[(name, kn)]))
         for c in cases:
             run(c, e)  # warm
+            if c[4] == "enc":  # every variant must produce the same repair bytes
+                rep = c[6][1]
+                sub = rep[::61].contiguous().view(torch.int32).view(-1).to(torch.int64)
+                h = (sub * (torch.arange(sub.numel(), device=dev) % 65521 + 1)).sum().item()
+                ref = digests.setdefault(c[0], h)
+                if h != ref:
+                    print(f"MISMATCH {name} {c[0]}", flush=True)
             ev[0].record()
             for _ in range(reps):
                 run(c, e)
