@@ -1619,7 +1619,8 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
 }
 
 template <int RT>
-__global__ __launch_bounds__(64) void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT == 16 ? 3 : RT == 8 ? 4 : 1)))
+void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint8_t *ws, int r0, int G,
                                                         uint8_t *status, uint64_t *recovered, int ilv,

@@ -492,6 +492,7 @@ def emit_function(mode, RT, VEC, P):
 # 4 waves per SIMD instead of 3), and the ring depth only costs LDS.
 T2_BASE = int(os.environ.get("FEC_GEN2_BASE", "8"))  # v0 .. v(T2_BASE-1) stay with the compiler
 S_PEND, S_PRT, S_COPTR, S_WTAB = 95, 96, 97, 98  # S_WTAB: 98-99
+S_INPTR, S_OUTPTR, S_NADDR = 93, 94, 82  # decode only (S_NADDR: 82-83, encode's S_OUT)
 SGPR_CLOBBER2 = list(range(60, 100))
 CASE_TABLE2 = "fec_bs2_case_table"
 
@@ -507,12 +508,8 @@ def regmap2(mode: str, ntmp: int = 4):
         th[n] = B + 19 + i
     tmp = list(range(B + 30, B + 30 + ntmp))
     nxt = B + 30 + ntmp + (ntmp & 1)
-    m = {"pl": list(range(B, B + 8)), "tl": tl, "th": th, "tmp": tmp}
-    if mode == "dec":
-        m.update(inptr=nxt, outptr=nxt + 1, naddr=nxt + 2, acc=nxt + 4)
-    else:
-        m["acc"] = nxt
-    return m
+    # decode's table pointers and the next row address live in SGPRs (S_INPTR, S_OUTPTR, S_NADDR)
+    return {"pl": list(range(B, B + 8)), "tl": tl, "th": th, "tmp": tmp, "acc": nxt}
 
 
 S2_SLOT = 2048  # bytes per ring slot: a whole column chunk; the unrolled steps address slots by immediates
@@ -528,7 +525,8 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     steps after a block's epilogue -- that epilogue's 2 * rt stores; those steps take their wait from
     a table indexed by rt.  Blocks are at least D sources long (the wrapper sizes D <= k), so at most
     one epilogue is ever in the window.  Steps that issue no DMA (the last D-1) wait for everything."""
-    NT = int(os.environ.get("FEC_GEN2_NTMP", "2")) if mode == "enc" else 4
+    NT = int(os.environ.get("FEC_GEN2_NTMP", "2"))
+    assert mode == "enc" or NT == 2
     R = regmap2(mode, NT)
     PL, TLm, THm, TMPm = R["pl"], R["tl"], R["th"], R["tmp"]
     XT = [TLm[3], TLm[5], TLm[6], TLm[7]]  # dead until the combos: the forward transpose's temporaries
@@ -565,27 +563,32 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
         a(f"s_mov_b32 s{S_JL}, 0")
     else:
-        a(f"v_mov_b32 v{R['inptr']}, %[intab]")
-        a(f"ds_read_b64 v[{R['naddr']}:{R['naddr'] + 1}], v{R['inptr']}")  # source 0's address
-        a(f"v_add_u32 v{R['inptr']}, 8, v{R['inptr']}")
-        a(f"v_mov_b32 v{R['outptr']}, %[outtab]")
+        a(f"s_mov_b32 s{S_INPTR}, %[intab]")
+        a(f"s_mov_b32 s{S_OUTPTR}, %[outtab]")
     a(f"s_sub_u32 s{S_S}, %[nsrc], 1")
     a(f"s_sub_u32 s{S_J}, %[k], 1")
     a(f"s_sub_u32 s{S_T2}, %[nsrc], {D - 1}")
     a(f"s_cselect_b32 s{S_T2}, 0, s{S_T2}")
     a(f"s_mov_b32 s{S_PEND}, 0")
 
-    def dma_issue(slot, lgkm_older=0):
-        """DMA of row S_CUR into ring slot `slot`; decode first takes the row's address (read one
-        DMA ago; `lgkm_older` LDS reads were issued after it)."""
+    T0, T1 = TMPm[0], TMPm[1]
+
+    def naddr_read():
+        """decode: issue the read of the next row address (table entry S_INPTR) into T0:T1"""
+        return [f"v_mov_b32 v{T1}, s{S_INPTR}",
+                f"ds_read_b64 v[{T0}:{T1}], v{T1}",
+                f"s_add_u32 s{S_INPTR}, s{S_INPTR}, 8"]
+
+    def naddr_take():
+        """decode: the address read by naddr_read (waited for) into S_NADDR"""
+        return [f"v_readfirstlane_b32 s{S_NADDR}, v{T0}",
+                f"v_readfirstlane_b32 s{S_NADDR + 1}, v{T1}"]
+
+    def dma_issue(slot):
+        """DMA of row S_CUR (decode: S_NADDR) into ring slot `slot`"""
         out = []
         if mode == "dec":
-            out += [f"s_waitcnt lgkmcnt({lgkm_older})",
-                    f"v_readfirstlane_b32 s{S_CUR}, v{R['naddr']}",
-                    f"v_readfirstlane_b32 s{S_CUR + 1}, v{R['naddr'] + 1}",
-                    f"ds_read_b64 v[{R['naddr']}:{R['naddr'] + 1}], v{R['inptr']}",
-                    f"v_add_u32 v{R['inptr']}, 8, v{R['inptr']}",
-                    "s_nop 1"]  # VALU-written SGPR -> VMEM base: 5 wait states with the moves below
+            out += [f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], s[{S_NADDR}:{S_NADDR + 1}]"]
         out += [f"s_add_u32 m0, %[ring], {slot * S2_SLOT}",
                 "s_mov_b64 exec, %[vmlo]",  # also the M0 -> LDS-DMA wait state
                 f"global_load_lds_dwordx4 %[g1], s[{S_CUR}:{S_CUR + 1}]@LDPOL@"]
@@ -606,8 +609,12 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     for q in range(D - 1):  # prologue: DMAs for sources 0 .. D-2 into slots 0 .. D-2
         a(f"s_cmp_lt_u32 {q}, %[nsrc]")
         a(f"s_cbranch_scc0 .Lpro_done_%=")
+        if mode == "dec":
+            L.extend(naddr_read() + ["s_waitcnt lgkmcnt(0)"] + naddr_take() + ["s_nop 4"])
         L.extend(dma_issue(q))
     a(".Lpro_done_%=:")
+    if mode == "dec":  # the address of source D-1, taken at step 0
+        L.extend(naddr_read())
     csb = coef_row_bytes(RT)
     dsr = "ds_read_b64" if csb == 8 else "ds_read_b128"
     ndw = min(4, csb // 4)
@@ -628,7 +635,11 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"s_waitcnt vmcnt({base_wait})")
         a(f".Lgot{b}_%=:")
         L.extend(data_reads(b))
-        L.extend(dma_issue((b + D - 1) % D, lgkm_older=2))
+        if mode == "dec":  # the address read one step ago (issued before this step's data reads)
+            a("s_waitcnt lgkmcnt(2)")
+            L.extend(naddr_take())
+            a("s_nop 4")  # VALU-written SGPR -> VMEM base
+        L.extend(dma_issue((b + D - 1) % D))
         a(f".Lrd{b}_%=:")
         ool += [f".Lnodma{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)"] + data_reads(b) + \
                [f"s_branch .Lrd{b}_%="]
@@ -639,14 +650,21 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                 f"s_addc_u32 s{S_CQ + 1}, s{S_WTAB + 1}, 0",
                 f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_CQ}:{S_CQ + 1}]",
                 f"s_branch .Lgot{b}_%="]
-        # the first coefficient fields go out behind the data reads (one wait covers both)
-        if NT >= 4:
+        # the first coefficient fields go out behind the data reads (one wait covers both); decode
+        # first waits for the data and issues the next address read (T0:T1 are free again only
+        # after the chains), so its fields go out after that read is taken
+        if mode == "dec":
+            a("s_waitcnt lgkmcnt(0)")
+            a(f"v_mov_b32 v{T1}, s{S_COPTR}")
+            a(f"ds_read_b64 v[{T0}:{T1}], v{T1}")
+        elif NT >= 4:
             a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
             a(f"{dsr} {regrange(TMPm[0], ndw)}, v{TMPm[3]}")
+            a("s_waitcnt lgkmcnt(1)")
         else:
             a(f"v_mov_b32 v{TMPm[1]}, s{S_COPTR}")
             a(f"ds_read_b64 v[{TMPm[0]}:{TMPm[1]}], v{TMPm[1]}")
-        a("s_waitcnt lgkmcnt(1)")
+            a("s_waitcnt lgkmcnt(1)")
         L.extend(transpose_inplace(PL, XT))
         L.extend(combos(TLm, THm))
         if NT >= 4:
@@ -690,6 +708,8 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"s_sub_u32 s{S_J}, s{S_J}, 1")
         a(f"s_cbranch_scc1 .Lepicall{b}_%=")
         a(f".Lnoepi{b}_%=:")
+        if mode == "dec":  # the address of source s + D, taken at the next step
+            L.extend(naddr_read())
         a(f"s_sub_u32 s{S_S}, s{S_S}, 1")
         a(f"s_cbranch_scc1 .Lexit_%=")
         ool += [f".Lepicall{b}_%=:", f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_EPI}:{S_EPI + 1}]",
@@ -704,33 +724,37 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
 
     # ---- per-block epilogue subroutine: inverse transpose, stores, clear; opens the big-wait window
     a(".Lepi_%=:")
-    tmpA, tmpB = TMPm[-2], TMPm[-1]
+    # decode's scratch: the Four-Russians table registers, dead between a block's last source and
+    # the next source's combos (E0:E1 the output address, E2 the record pointer, E3/E4 the flag)
+    E = [TLm[3], TLm[5], TLm[6], TLm[7], TLm[9]]
+    assert E[0] % 2 == 0 and E[1] == E[0] + 1
     if mode == "enc":
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
     else:
-        a(f"ds_read_b32 v{tmpA}, v{R['outptr']} offset:{DEC_REC_RT}")
+        a(f"v_mov_b32 v{E[2]}, s{S_OUTPTR}")
+        a(f"ds_read_b32 v{E[0]}, v{E[2]} offset:{DEC_REC_RT}")
         a("s_waitcnt lgkmcnt(0)")
-        a(f"v_readfirstlane_b32 s{S_RT}, v{tmpA}")
+        a(f"v_readfirstlane_b32 s{S_RT}, v{E[0]}")
     for i in range(RT):
         accs = [acc_base + 8 * i + w for w in range(8)]
         a(f"s_cmp_le_u32 s{S_RT}, {i}")
         a(f"s_cbranch_scc1 .Lepi_done_%=")
         L.extend(transpose_inplace(accs, TMPm))
         if mode == "dec":
-            a(f"ds_read_b64 v[{tmpA}:{tmpB}], v{R['outptr']} offset:{8 * i}")
-            a(f"v_or3_b32 v{TMPm[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
-            a(f"v_or3_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[3]}, v{accs[4]}")
-            a(f"v_or3_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[5]}, v{accs[6]}")
-            a(f"v_or_b32 v{TMPm[0]}, v{TMPm[0]}, v{accs[7]}")
-            a(f"v_cmp_ne_u32 vcc, 0, v{TMPm[0]}")
-            a(f"v_mov_b32 v{TMPm[1]}, 1")
+            a(f"ds_read_b64 v[{E[0]}:{E[1]}], v{E[2]} offset:{8 * i}")
+            a(f"v_or3_b32 v{E[3]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
+            a(f"v_or3_b32 v{E[3]}, v{E[3]}, v{accs[3]}, v{accs[4]}")
+            a(f"v_or3_b32 v{E[3]}, v{E[3]}, v{accs[5]}, v{accs[6]}")
+            a(f"v_or_b32 v{E[3]}, v{E[3]}, v{accs[7]}")
+            a(f"v_cmp_ne_u32 vcc, 0, v{E[3]}")
+            a(f"v_mov_b32 v{E[4]}, 1")
             a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
-            a(f"ds_write_b8 v{R['outptr']}, v{TMPm[1]} offset:{DEC_REC_NZ + i}")
+            a(f"ds_write_b8 v{E[2]}, v{E[4]} offset:{DEC_REC_NZ + i}")
             a("s_mov_b64 exec, %[vm0]")
             a("s_waitcnt lgkmcnt(0)")
-            a(f"v_readfirstlane_b32 s{S_O2}, v{tmpA}")
-            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{tmpB}")
+            a(f"v_readfirstlane_b32 s{S_O2}, v{E[0]}")
+            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{E[1]}")
             a("s_nop 4")  # VALU-written SGPR -> VMEM base
         for q in range(2):
             a(f"s_mov_b64 exec, %[vm{q}]")
@@ -748,7 +772,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rslo]")
         a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, %[rshi]")
     else:
-        a(f"v_add_u32 v{R['outptr']}, {DEC_REC_BYTES}, v{R['outptr']}")
+        a(f"s_add_u32 s{S_OUTPTR}, s{S_OUTPTR}, {DEC_REC_BYTES}")
     a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
     a(".Lexit_%=:")
     a("s_waitcnt lgkmcnt(0)")
@@ -770,7 +794,7 @@ def emit_function2(mode, RT, D, NDMA):
                '[sdl] "s"(sdl)', '[ll] "s"(ll)', '[rt] "s"(rt)']
     else:
         sig = f"__device__ __forceinline__ void {name}(uint32_t intab, uint32_t outtab, {common})"
-        ins = ['[intab] "v"(intab)', '[outtab] "v"(outtab)']
+        ins = ['[intab] "s"(intab)', '[outtab] "s"(outtab)']
     ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "s"(coef)', '[ring] "s"(ring)', '[g1] "v"(g1)', '[g2] "v"(g2)', '[vmlo] "s"(vmlo)', '[vmhi] "s"(vmhi)',
             '[rd1] "v"(rd1)', '[rd2] "v"(rd2)', '[off0] "v"(off0)', '[off1] "v"(off1)', '[vm0] "s"(vm0)',
             '[vm1] "s"(vm1)']
