@@ -1229,8 +1229,12 @@ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, 
 // W waves per workgroup can split the repairs of one group of blocks: wave w owns repairs
 // r0 + w*RT .. +RT, streaming the same source rows close together in time (L2 serves the
 // repeats).  Default W = 1 (see pick_enc_tile); W > 1 is kept for FECGPU_ENC_TILE experiments.
+#ifndef FEC_V1_ENC8_WAVES
+#define FEC_V1_ENC8_WAVES 1  // set by bitslice_gen.h when 8-repair encode tiles use the compact register map
+#endif
 template <int RT, int VEC>
-__global__ __launch_bounds__(256) void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 8 ? FEC_V1_ENC8_WAVES : 1)))
+void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
                                                        int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv) {

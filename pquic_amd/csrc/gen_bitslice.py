@@ -50,6 +50,7 @@ OUTPTR = 68  # decode only
 NADDR = 70   # decode only: the next source's address, read from the table one source ahead
 DATA_BASE = 68  # encode; decode data buffers start at 70 (tuples must start on an even VGPR)
 CASE_BYTES = 80  # <= 8 VOP3 (64 B) + the 16-byte chain tail; table entry 0 is the return stub
+V1_TABLE = "fec_bs_case_table"
 # stage-0 destinations (scratch, overwritten by the combos), stage-2 destinations (planes)
 XS = [TL[3], TL[5], TL[6], TL[7], TH[3], TH[5], TH[6], TH[7]]
 PL = [TL[1], TL[2], TL[4], TL[8], TH[1], TH[2], TH[4], TH[8]]
@@ -266,8 +267,8 @@ def body(mode: str, RT: int, VEC: int, P: int):
     for i, m in enumerate(MASKS):
         a(f"s_mov_b32 s{S_MASK[i]}, 0x{m:08x}")
     a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
-    a(f"s_add_u32 s{S_TAB}, s{S_TAB}, fec_bs_case_table@rel32@lo+4")
-    a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, fec_bs_case_table@rel32@hi+12")
+    a(f"s_add_u32 s{S_TAB}, s{S_TAB}, {V1_TABLE}@rel32@lo+4")
+    a(f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, {V1_TABLE}@rel32@hi+12")
     # the table is 64 KiB-aligned and 20 KiB long: a target is TAB's upper 48 bits with the case
     # offset as its low 16 (s_pack_ll of the queue field and TAB.lo >> 16); the engine checks the
     # alignment on the device before the first launch (fec_bs_case_table_addr)
@@ -852,6 +853,45 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
 CONFIGS = [(RT, VEC) for VEC in (16, 8, 4) for RT in (1, 2, 4, 8, 16)]
 
 
+_V1_LAYOUT_NAMES = ("T_BASE", "TL", "TH", "TMP", "CO", "COPTR", "INPTR", "OUTPTR", "NADDR", "DATA_BASE", "XS",
+                    "PL", "V1_TABLE")
+
+
+def v1_compact_layout():
+    """The register-prefetch bodies on the ring bodies' compact register map (table registers from
+    v8, the ring case table): 8-repair encode tiles then fit 4 waves/SIMD (128 VGPRs) at a prefetch
+    depth of 2 -- k32 r8 encode -1.8 % against 3 waves at depth 4 (profiles/r02_ab_v1_compact.log)."""
+    R = regmap2("enc", 4)
+    coptr = T2_BASE + 34
+    tl, th = R["tl"], R["th"]
+    return {"T_BASE": T2_BASE, "TL": tl, "TH": th, "TMP": R["tmp"], "CO": R["tmp"], "COPTR": coptr,
+            "INPTR": coptr + 1, "OUTPTR": coptr + 2, "NADDR": coptr + 4,
+            "DATA_BASE": coptr + 1 + ((coptr + 1) & 1),
+            "XS": [tl[3], tl[5], tl[6], tl[7], th[3], th[5], th[6], th[7]],
+            "PL": [tl[1], tl[2], tl[4], tl[8], th[1], th[2], th[4], th[8]], "V1_TABLE": CASE_TABLE2}
+
+
+class _Layout:
+    """Temporarily switch the module's v1 register map (the v1 emitters read the globals)."""
+
+    def __init__(self, m):
+        self.m = m
+
+    def __enter__(self):
+        g = globals()
+        self.saved = {n: g[n] for n in _V1_LAYOUT_NAMES}
+        if self.m:
+            g.update(self.m)
+
+    def __exit__(self, *exc):
+        globals().update(self.saved)
+
+
+# encode tile sizes whose register-prefetch bodies use the compact map at 4 waves/SIMD
+COMPACT_ENC = {int(x) for x in os.environ.get("FEC_GEN_COMPACT_ENC", "8").split(",") if x}
+COMPACT_VGPRS = 128
+
+
 def main():
     selfcheck()
     parts = ["// GENERATED by pquic_amd/csrc/gen_bitslice.py -- do not edit.",
@@ -908,10 +948,19 @@ def main():
               "  }",
               "}", ""]
     tops = {}
+    for RT in sorted(COMPACT_ENC):
+        parts.append(f"#define FEC_V1_ENC{RT}_WAVES {512 // COMPACT_VGPRS}  // compact-map encode tiles (v1_compact_layout)")
     for mode in ("enc", "dec"):
         for RT, VEC in CONFIGS:
-            P = prefetch_depth(mode, RT, VEC)
-            fn, top = emit_function(mode, RT, VEC, P)
+            compact = mode == "enc" and RT in COMPACT_ENC
+            with _Layout(v1_compact_layout() if compact else None):
+                if compact:
+                    NP = 32 // VEC
+                    P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= COMPACT_VGPRS
+                            and NP * (P - 1) <= 63)
+                else:
+                    P = prefetch_depth(mode, RT, VEC)
+                fn, top = emit_function(mode, RT, VEC, P)
             tops[(mode, RT, VEC, P)] = top
             parts.append(fn)
             parts.append("")
