@@ -329,10 +329,15 @@ __device__ __forceinline__ void clip128(uint64_t &m0, uint64_t &m1, int n) {
   else if (n < 128) m1 &= (1ull << (n - 64)) - 1;
 }
 
-__global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r, uint32_t fbn_base,
-                                                 const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
-                                                 const uint64_t *rp, uint8_t *ws) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+// One block's plan by one wave (row-parallel elimination).  `lds` holds the log/exp tables at 0
+// (plan_load_tables) and room for plan_lds_bytes(k, r).  Every lane of the wave must call it.
+__device__ __forceinline__ void plan_load_tables(uint8_t *lds) {
+  for (int i = threadIdx.x; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+}
+
+__device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
+                                const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *ws,
+                                uint8_t *lds) {
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   const int em = (int)L.em;
@@ -341,11 +346,9 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
   const PlanLds P = plan_carve(lds, em, kpad, empad);
   uint8_t *A = P.A, *V = P.V, *X = P.X, *EXP = P.exp, *LOG = P.log, *terms = P.terms;
   int *unk = P.unk, *sel = P.sel, *perm = P.perm;
-  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
   // x * y with y != 0 given as log y
   auto mul_l = [&](uint32_t x, uint32_t ly) -> uint32_t { return x ? EXP[LOG[x] + ly] : 0u; };
-
-  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+  {
     uint8_t *h = ws + b * (uint64_t)L.stride;
     uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
     clip128(s0, s1, k);
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
     // rlc_fec_scheme_gf256.c:140-144
     if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {
       if (lane == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
-      continue;
+      return;
     }
     const int n = k - cur_ss;  // unknowns == equations (n_eq = min(n_unk, cur_rs) = n_unk)
     uint64_t m0 = ~s0, m1 = ~s1;
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
     for (int i = 64 + lane; i < n; i += 64) ub |= A[perm[i] * empad + i] == 0;
     if (__any(ub)) {
       if (lane == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
-      continue;
+      return;
     }
     // back substitution (:71-114), column-oriented: x_i = V[pi] / A[pi][i], then V[pm] -= A[pm][i] x_i
     for (int i = n - 1; i >= 0; i--) {
@@ -472,6 +475,14 @@ __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r,
       h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | sel[rank128(m0, m1, j)]) : (uint8_t)j;
     if (lane == 0) { h[0] = FECGPU_BLOCK_RECOVERED; h[1] = (uint8_t)n; }
   }
+}
+
+__global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                 const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
+                                                 const uint64_t *rp, uint8_t *ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  plan_load_tables(lds);
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1319,19 +1330,18 @@ struct RecoverLds {
   }
 };
 
+// One group of the recover data pass (group q of NG, blocks b0, b0 + bstep, ...); every lane of the
+// wave calls it.  k_rlc_recover_bs runs it over a grid-stride loop; k_rlc_decode_small after the
+// wave plan of the group's block.
 template <int RT, int VEC>
-__global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
-                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
-                                                       int chunk_bytes, uint8_t *ws, int r0, int G,
-                                                       uint8_t *status, uint64_t *recovered, int ilv,
-                                                       uint8_t *dst) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+__device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_t *__restrict__ src,
+                                 const uint8_t *__restrict__ rep, uint64_t nblocks, int k, int r, int L, int nchunks,
+                                 int chunk_bytes, uint8_t *ws, int r0, int G, uint8_t *status, uint64_t *recovered,
+                                 int ilv, uint8_t *dst, uint8_t *lds) {
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   RecoverLds<RT> S(lds, G, k);
-  const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
-  const uint64_t bstep = ilv ? NG : 1;
-  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+  {
     const uint64_t b0 = ilv ? q : q * G;
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
@@ -1432,6 +1442,42 @@ __global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src
           reinterpret_cast<uint8_t *>(reinterpret_cast<const uint64_t *>(rc)[kDecRecNzPtr])[x & 15] = 1;
       }
     }
+  }
+}
+
+template <int RT, int VEC>
+__global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+                                                       uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                       int chunk_bytes, uint8_t *ws, int r0, int G,
+                                                       uint8_t *status, uint64_t *recovered, int ilv,
+                                                       uint8_t *dst) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
+  const uint64_t bstep = ilv ? NG : 1;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x)
+    recover_bs_group<RT, VEC>(q, NG, bstep, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, r0, G, status,
+                              recovered, ilv, dst, lds);
+}
+
+// Decode of a few blocks in ONE launch (the synchronous hooks decode one block per call): each
+// workgroup plans its block with the wave plan, then runs the single-pass data pass on it.  The
+// plan's workspace record goes through global memory (the fence makes it visible to the loads).
+template <int RT, int VEC>
+__global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
+                                                         int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
+                                                         const uint32_t *seeds, const uint64_t *sp,
+                                                         const uint64_t *rp, uint8_t *ws, uint8_t *status,
+                                                         uint64_t *recovered, uint8_t *dst) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    __syncthreads();
+    plan_load_tables(lds);
+    plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    __threadfence();
+    __syncthreads();
+    recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, 0, 1, status,
+                              recovered, 0, dst, lds);
   }
 }
 
@@ -2311,6 +2357,8 @@ static int decode_args(const void *src, const void *rep, uint64_t nblocks, uint3
   return FECGPU_OK;
 }
 
+constexpr uint64_t kPlanWaveMaxBlocks = 64;  // below this many blocks a wave per block plans fastest
+
 static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
                             const uint32_t *seeds, const uint64_t *src_present, const uint64_t *rep_present,
                             void *workspace, size_t workspace_bytes, void *stream) {
@@ -2323,8 +2371,12 @@ static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t f
   const size_t lane_lds = plan_lane_lds(k, r);
   // knob "plan" (FECGPU_PLAN=reg|tile|lane|wave) overrides the size rule (A/B experiments; the tests
   // compare the plan kernels on the same inputs through fecgpu_set_knob)
-  const int force = knob(K_PLAN);
+  int force = knob(K_PLAN);
   const uint32_t em = ws_layout(k, r).em;
+  // a few blocks (the synchronous hooks run one): every block gets its own wave and the wave plan's
+  // row-parallel elimination, instead of a lane's serial replay -- one-block recover hook
+  // 47 -> 40 us (profiles/r02_hook_plan.log)
+  if (force == 0 && nblocks <= kPlanWaveMaxBlocks && plan_lds_bytes(k, r) <= 65536) force = PLAN_WAVE;
   if ((force == 0 || force == 3) && k <= 32 && em <= 8) {
     const size_t reg_lds = 768 + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);
     const uint64_t groups = (nblocks + 63) / 64;
@@ -2468,34 +2520,79 @@ int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint
                            workspace_bytes, (hipStream_t)stream);
 }
 
+extern "C++" {
+template <int RT, int VEC>
+static void launch_decode_small(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
+                                uint32_t fbn_base, const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
+                                const uint64_t *rp, uint8_t *ws, uint8_t *status, uint64_t *recovered, uint8_t *dst,
+                                hipStream_t s) {
+  const size_t pl = plan_lds_bytes((uint32_t)k, (uint32_t)r), rl = RecoverLds<RT>::bytes(1, k);
+  hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC>), dim3((uint32_t)nb), dim3(64), pl > rl ? pl : rl, s, src, rep,
+                     nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, ws, status, recovered, dst);
+}
+}  // extern "C++"
+
+// Below this many blocks a decode is one launch (k_rlc_decode_small): plan and data pass per
+// workgroup.  One-block recover hook p50 46 us (lane plan + data pass, two launches) -> 40 (wave
+// plan, two launches) -> 37 (one launch) (profiles/r02_hook_plan.log, r02_hook_small.log; the
+// first line of the latter is this path, the second the forced lane-register plan).
+constexpr uint64_t kDecodeSmallMaxBlocks = 64;
+
+// Plan + apply; recovered rows to dst (dst == src: in place).  seeds != nullptr: per-repair seeds.
+static int decode_impl(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k, uint32_t r,
+                       uint32_t L, uint32_t fbn_base, const uint32_t *fbn, const uint32_t *seeds,
+                       const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered, void *ws,
+                       size_t wsb, hipStream_t s) {
+  int rc = decode_args(src, rep, nblocks, k, r, L, sp, rp, status, recovered, ws, wsb);
+  if (rc || nblocks == 0) return rc;
+  if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL output buffer");
+  if ((uintptr_t)dst % 4) return set_err(FECGPU_ERR_INVALID, "%s", "output buffer must be 4-byte aligned");
+  const WsLayout WL = ws_layout(k, r);
+  // the one-launch path: a few blocks, one data pass (e <= 16), the default kernels (no knob forces a
+  // plan kernel or another data path)
+  if (nblocks <= kDecodeSmallMaxBlocks && r > 0 && WL.em <= 16 && knob(K_PLAN) == 0 && !use_perm_path() &&
+      plan_lds_bytes(k, r) <= 65536) {
+    const BsCfg cfg = pick_bs_cfg((int)L);
+    const int rt = WL.em <= 1 ? 1 : WL.em <= 2 ? 2 : WL.em <= 4 ? 4 : WL.em <= 8 ? 8 : 16;
+    if (!use_ring(rt, k, cfg, false)) {
+      if (int rc2 = bs_table_check()) return rc2;
+      g_stats[2]++;
+      g_stats[3] += nblocks;
+      FEC_BS_DISPATCH(launch_decode_small, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r, (int)L,
+                      cfg, fbn_base, fbn, seeds, sp, rp, (uint8_t *)ws, status, recovered, (uint8_t *)dst, s)
+      HIPCHK(hipGetLastError());
+      return FECGPU_OK;
+    }
+  }
+  rc = decode_plan_impl(nblocks, k, r, fbn_base, fbn, seeds, sp, rp, ws, wsb, s);
+  if (rc) return rc;
+  return decode_apply_impl(src, rep, dst, nblocks, k, r, L, status, recovered, ws, wsb, s);
+}
+
 int fecgpu_rlc_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
                       uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn,
                       const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
                       uint64_t *recovered, void *workspace, size_t workspace_bytes, void *stream) {
-  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, src_present, rep_present, status, recovered,
-                       workspace, workspace_bytes);
-  if (rc || nblocks == 0) return rc;
-  if ((rc = fecgpu_rlc_decode_plan(nblocks, k, r, fbn_base, fbn, src_present, rep_present, workspace,
-                                   workspace_bytes, stream)))
-    return rc;
-  if ((rc = fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, status, recovered, workspace,
-                                    workspace_bytes, stream)))
-    return rc;
-  return FECGPU_OK;
+  return decode_impl(src, rep, src, nblocks, k, r, symbol_size, fbn_base, fbn, nullptr, src_present, rep_present,
+                     status, recovered, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int fecgpu_rlc_decode_seeded(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t r,
                              uint32_t symbol_size, const uint32_t *rep_seed, const uint64_t *src_present,
                              const uint64_t *rep_present, uint8_t *status, uint64_t *recovered, void *workspace,
                              size_t workspace_bytes, void *stream) {
-  int rc = decode_args(src, rep, nblocks, k, r, symbol_size, src_present, rep_present, status, recovered,
-                       workspace, workspace_bytes);
-  if (rc || nblocks == 0) return rc;
-  if ((rc = fecgpu_rlc_decode_plan_seeded(nblocks, k, r, rep_seed, src_present, rep_present, workspace,
-                                          workspace_bytes, stream)))
-    return rc;
-  return fecgpu_rlc_decode_apply(src, rep, nblocks, k, r, symbol_size, status, recovered, workspace,
-                                 workspace_bytes, stream);
+  if (nblocks && r && !rep_seed) return set_err(FECGPU_ERR_INVALID, "%s", "NULL rep_seed");
+  return decode_impl(src, rep, src, nblocks, k, r, symbol_size, 0, nullptr, rep_seed, src_present, rep_present,
+                     status, recovered, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+// host_path.hip: decode with the recovered rows to dst (library-internal)
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_rlc_decode_to_internal(
+    const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k, uint32_t r, uint32_t L,
+    uint32_t fbn_base, const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp,
+    uint8_t *status, uint64_t *recovered, void *ws, size_t wsb, void *stream) {
+  return decode_impl(src, rep, dst, nblocks, k, r, L, fbn_base, fbn, seeds, sp, rp, status, recovered, ws, wsb,
+                     (hipStream_t)stream);
 }
 
 int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,

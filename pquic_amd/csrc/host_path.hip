@@ -92,6 +92,10 @@ static uint8_t *mapped_host(const void *p) {
 // being staged by copies: measured 49.2 -> 51.0 GiB/s encode, 39.2 -> 50.3 GiB/s decode
 // (k16 r4, 2^18 blocks).  Knob zc_read = 0 (FECGPU_ZC_READ=0) restores the staged copies (A/B).
 int fecgpu_knob_zc_read(void);  // fec_engine.hip (library-internal, C linkage)
+int fecgpu_rlc_decode_to_internal(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                                  uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn,
+                                  const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *status,
+                                  uint64_t *recovered, void *ws, size_t wsb, void *stream);  // fec_engine.hip
 static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 
 static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t per_block) {
@@ -250,12 +254,11 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
     } else {
       const size_t wsb = fecgpu_rlc_decode_workspace(n, k, r);
       LCHK(grow(&s.d_ws, &s.cap_ws, wsb));
-      rc = seeds ? fecgpu_rlc_decode_plan_seeded(m, k, r, d_fbn, d_sp, d_rp, s.d_ws, s.cap_ws, s.st)
-                 : fecgpu_rlc_decode_plan(m, k, r, (uint32_t)((fbn_base + b0) & 0xffffffu), fbn ? d_fbn : nullptr,
-                                          d_sp, d_rp, s.d_ws, s.cap_ws, s.st);
-      if (!rc)
-        rc = fecgpu_rlc_decode_apply_to(in_src, in_rep, zdst ? zdst + b0 * sb : s.d_src, m, k, r, L, d_st, d_rec,
-                                        s.d_ws, s.cap_ws, s.st);
+      // plan + data pass (one launch for a few blocks, e.g. the synchronous hook's one)
+      rc = fecgpu_rlc_decode_to_internal(in_src, in_rep, zdst ? zdst + b0 * sb : s.d_src, m, k, r, L,
+                                         seeds ? 0u : (uint32_t)((fbn_base + b0) & 0xffffffu),
+                                         (!seeds && fbn) ? d_fbn : nullptr, seeds ? d_fbn : nullptr, d_sp, d_rp,
+                                         d_st, d_rec, s.d_ws, s.cap_ws, s.st);
     }
     if (rc) break;
     if (!zdst) LCHK(hipMemcpyAsync((uint8_t *)src + b0 * sb, s.d_src, m * sb, hipMemcpyDeviceToHost, s.st));

@@ -211,6 +211,35 @@ def test_decode_vs_oracle(eng, oracle, k, r, L, nb, emax):
     assert {DEC_RECOVERED, DEC_NOTHING} <= set(st.tolist())
 
 
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 1), (16, 4, 1200, 64), (32, 8, 1200, 7), (5, 5, 20, 33),
+                                      (64, 16, 9000, 3), (20, 16, 2052, 9), (3, 1, 4, 2)])
+def test_small_batch_decode_one_launch(eng, oracle, k, r, L, nb):
+    """Up to 64 blocks decode in one launch (wave plan + data pass per workgroup, as the
+    synchronous hooks run); same bytes, statuses and masks as the oracle and as the two-launch
+    path a forced plan kernel takes."""
+    rng = np.random.default_rng(nb * 7 + k)
+    src_h = synth_bytes(nb * k * L, 5 + r).reshape(nb, k, L)
+    fbn_base = int(rng.integers(0, 1 << 24))
+    rep_h = oracle.rlc_encode_batch(src_h, r, fbn_base)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        e = int(rng.integers(0, min(k, r) + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        rp[b] = masks_from_lists(1, r, [rng.choice(r, int(rng.integers(max(0, e - 1), r + 1)), replace=False).tolist()])[0]
+    work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+    with eng.knob("plan", 1):  # the wave plan as its own launch, then the data pass
+        _, got2, st2, rec2 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+    ref = work.copy()
+    st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
+    assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)
+    assert np.array_equal(st2, st_ref) and np.array_equal(rec2, rec_ref)
+    for b in range(nb):
+        for j in bits(rec[b], k):
+            assert np.array_equal(got[b, j], src_h[b, j]) and np.array_equal(got2[b, j], src_h[b, j])
+
+
 def test_decode_zero_symbol_propagation(eng, oracle):
     """All-zero sources are undetermined in the reference, and so is every unknown whose
     back-substitution row references them (rlc_fec_scheme_gf256.c:88-101)."""
