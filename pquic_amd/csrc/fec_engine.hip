@@ -1216,8 +1216,9 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
 }
 
 // Blocks per group: at most 64 / RT (one coefficient lane per (block, repair)), bounded by the LDS
-// budget.  Defaults measured in-process (profiles/r01_ab_group.log, three boxes):
-// - encode tiles of 4 repairs: groups of 4 blocks (k16 r4 -2.6..-3.1 % against 16);
+// budget.  Defaults measured in-process (profiles/r01_ab_group.log, three boxes; r02_ab_group*.log):
+// - encode tiles of 4 repairs: groups of 2 blocks (round 2, four boxes: k16 r4 -3.0..-4.1 % against
+//   4; round 1 had 4 against 16: -2.6..-3.1 %);
 // - decode tiles of 4: groups of 8 (k16 e4 -0.8..-1 %);
 // - symbols wider than one column chunk (L > 2 KiB): one block per group (k64 r16 L9000 encode
 //   -2.3 %, decode -8.3 %: the chunk passes then revisit one block's rows);
@@ -1230,7 +1231,7 @@ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, 
   } else if (nchunks > 1) {
     g = 1;
   } else if (RT == 4) {
-    g = enc ? 4 : 8;
+    g = enc ? 2 : 8;
   }
   while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
   return g;
@@ -1243,8 +1244,12 @@ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, 
 #ifndef FEC_V1_ENC8_WAVES
 #define FEC_V1_ENC8_WAVES 1  // set by bitslice_gen.h when 8-repair encode tiles use the compact register map
 #endif
+#ifndef FEC_V1_ENC4_WAVES
+#define FEC_V1_ENC4_WAVES 1  // likewise for 4-repair tiles
+#endif
 template <int RT, int VEC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 8 ? FEC_V1_ENC8_WAVES : 1)))
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(RT == 8 ? FEC_V1_ENC8_WAVES : RT == 4 ? FEC_V1_ENC4_WAVES : 1)))
 void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,

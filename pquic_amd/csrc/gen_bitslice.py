@@ -892,6 +892,11 @@ COMPACT_ENC = {int(x) for x in os.environ.get("FEC_GEN_COMPACT_ENC", "8").split(
 COMPACT_VGPRS = 128
 
 
+def compact_vgprs(RT: int) -> int:
+    """VGPR budget of a compact-map encode tile (512 / budget = waves per SIMD)."""
+    return int(os.environ.get(f"FEC_GEN_COMPACT_VGPRS_RT{RT}") or COMPACT_VGPRS)
+
+
 def main():
     selfcheck()
     parts = ["// GENERATED by pquic_amd/csrc/gen_bitslice.py -- do not edit.",
@@ -949,14 +954,14 @@ def main():
               "}", ""]
     tops = {}
     for RT in sorted(COMPACT_ENC):
-        parts.append(f"#define FEC_V1_ENC{RT}_WAVES {512 // COMPACT_VGPRS}  // compact-map encode tiles (v1_compact_layout)")
+        parts.append(f"#define FEC_V1_ENC{RT}_WAVES {512 // compact_vgprs(RT)}  // compact-map encode tiles (v1_compact_layout)")
     for mode in ("enc", "dec"):
         for RT, VEC in CONFIGS:
             compact = mode == "enc" and RT in COMPACT_ENC
             with _Layout(v1_compact_layout() if compact else None):
                 if compact:
                     NP = 32 // VEC
-                    P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= COMPACT_VGPRS
+                    P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= compact_vgprs(RT)
                             and NP * (P - 1) <= 63)
                 else:
                     P = prefetch_depth(mode, RT, VEC)
