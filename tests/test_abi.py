@@ -124,3 +124,18 @@ def test_oversized_block_rejected_without_device_call():
     mh.mh_protoop_stats(st1.ctypes.data_as(C.POINTER(C.c_uint64)))
     assert st1[0] == st0[0] and st1[1] == st0[1]
     assert st1[4] == st0[4] + 6
+
+
+def test_generated_bodies_match_generator(tmp_path):
+    """pquic_amd/csrc/bitslice_gen.h is exactly what gen_bitslice.py writes with its defaults (the
+    generator also self-checks the plane algebra and the transpose against a byte-level GF model)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gen = os.path.join(root, "pquic_amd", "csrc", "gen_bitslice.py")
+    out = tmp_path / "bitslice_gen.h"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("FEC_GEN")}
+    env["FEC_GEN_OUT"] = str(out)
+    subprocess.run([sys.executable, gen], check=True, env=env, capture_output=True)
+    with open(os.path.join(root, "pquic_amd", "csrc", "bitslice_gen.h")) as f:
+        assert out.read_text() == f.read()
