@@ -110,6 +110,16 @@ def encode_kernel_name(k, r, L):
     return f"k_rlc_encode_bs<{rt},{vec}>"
 
 
+def apply_kernel_name(k, r, L):
+    """The decode data-pass kernel of the default dispatch (fec_engine.hip decode_apply_impl)."""
+    em = min(k, r)
+    ert = 16 if em > 8 else 8 if em > 4 else 4 if em > 2 else em
+    vec = 16 if L >= 16 else 8 if L % 8 == 0 else 4
+    if ert == 16 and vec == 16 and k >= 5:
+        return "k_rlc_recover_bs2<16>"
+    return f"k_rlc_recover_bs<{ert},{vec}>"
+
+
 def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     """One BASELINE config as a side leg: RLC encode, then decode with e random erasures,
     device-resident, per-kernel event timing; decode correctness gated on the output."""
@@ -147,6 +157,7 @@ def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     torch.cuda.empty_cache()
     pay = nb * k * L / 2**30
     return {"blocks": nb, "k": k, "r": r, "L": L, "erasures": e, "encode_kernel": encode_kernel_name(k, r, L),
+            "apply_kernel": apply_kernel_name(k, r, L),
             "encode_ms": round(t[0], 3),
             "plan_ms": round(t[1], 3), "apply_ms": round(t[2], 3),
             "payload_GiB_s": round(pay / ((t[0] + t[1] + t[2]) * 1e-3), 2),
@@ -532,9 +543,6 @@ def main():
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     app_gbs = app_bytes / (apply_ms * 1e-3) / 1e9 if e else 0.0
     tag = f"k{k}_r{r}" + ("" if L == 1200 else f"_L{L}")
-    rt = 16 if r >= 16 else 8 if r >= 8 else 4 if r >= 4 else 2 if r >= 2 else 1
-    vec = 16 if L >= 16 else 8 if L % 8 == 0 else 4
-    ert = 16 if min(k, r) > 8 else 8 if min(k, r) > 4 else 4 if min(k, r) > 2 else min(k, r)
     enc_kernel = encode_kernel_name(k, r, L)
     legs = {
         f"rlc_encode_{tag}": {"kernel": enc_kernel, "ms": round(enc_ms, 3), "blocks": nb,
@@ -546,7 +554,7 @@ def main():
         legs[f"rlc_decode_k{k}_e{e}"] = {
             "ms": round(dec_ms, 3), "plan_ms": round(plan_ms, 3), "apply_ms": round(apply_ms, 3),
             "payload_GiB_s": round(payload / (dec_ms * 1e-3) / 2**30, 2),
-            "apply_kernel": f"k_rlc_recover_bs<{ert},{vec}>", "apply_algorithmic_GB_s": round(app_gbs, 1),
+            "apply_kernel": apply_kernel_name(k, r, L), "apply_algorithmic_GB_s": round(app_gbs, 1),
             "apply_hbm_frac": round(app_gbs / HBM_PEAK_GBS, 4), "recovered_blocks": n_rec,
             "ref_ub_blocks": n_ub, "traffic": load_traffic(f"rlc_decode_apply_k{k}_e{e}", nb)}
     if e:
@@ -608,7 +616,7 @@ def main():
                     "achieved": round(enc_gbs, 1), "bytes_per_launch": enc_bytes, "launch_ms": round(enc_ms, 4),
                     "traffic": load_traffic(f"rlc_encode_{tag}", nb)}
         else:
-            roof = {"bound": "hbm", "kernel": f"k_rlc_recover_bs<{ert},{vec}> (RLC decode apply k={k} e={e})",
+            roof = {"bound": "hbm", "kernel": f"{apply_kernel_name(k, r, L)} (RLC decode apply k={k} e={e})",
                     "achieved": round(app_gbs, 1), "bytes_per_launch": app_bytes, "launch_ms": round(apply_ms, 4),
                     "traffic": load_traffic(f"rlc_decode_apply_k{k}_e{e}", nb)}
         roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),

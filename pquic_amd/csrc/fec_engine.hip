@@ -69,7 +69,7 @@ static void knobs_from_env() {
   g_knob[K_XOR_GENERIC] = num(getenv("FECGPU_XOR_GENERIC"), 0) != 0;
   g_knob[K_XOR_IDX64] = num(getenv("FECGPU_XOR_IDX64"), 0) != 0;
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
-  // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair encode tiles
+  // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair tiles
   g_knob[K_RING] = num(getenv("FECGPU_RING"), 2);
 }
 
@@ -1450,8 +1450,12 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
   }
 }
 
+#ifndef FEC_V1_DEC4_WAVES
+#define FEC_V1_DEC4_WAVES 1  // set by bitslice_gen.h when 4-unknown decode tiles use the compact register map
+#endif
 template <int RT, int VEC>
-__global__ __launch_bounds__(64) void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT == 4 ? FEC_V1_DEC4_WAVES : 1)))
+void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
                                                        uint8_t *status, uint64_t *recovered, int ilv,
@@ -1845,7 +1849,7 @@ static int bs2_depth(int RT, bool enc) {
 static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
   const int m = knob(K_RING);
   if (m == 0 || cfg.vec != 16 || (int)k < bs2_depth(rt, enc)) return false;
-  return m == 1 || (rt == 16 && enc);
+  return m == 1 || rt == 16;
 }
 
 #define FEC_BS2_DISPATCH(FN, ...)                                                               \

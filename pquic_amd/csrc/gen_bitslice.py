@@ -807,7 +807,7 @@ def emit_function2(mode, RT, D, NDMA):
 
 
 RING_DEPTH = {("enc", 1): 4, ("enc", 2): 4, ("enc", 4): 4, ("enc", 8): 4, ("enc", 16): 4,
-              ("dec", 1): 4, ("dec", 2): 4, ("dec", 4): 4, ("dec", 8): 4, ("dec", 16): 8}
+              ("dec", 1): 4, ("dec", 2): 4, ("dec", 4): 4, ("dec", 8): 4, ("dec", 16): 5}
 
 
 def ring_depth(mode: str, RT: int) -> int:
@@ -889,6 +889,7 @@ class _Layout:
 
 # encode tile sizes whose register-prefetch bodies use the compact map at 4 waves/SIMD
 COMPACT_ENC = {int(x) for x in os.environ.get("FEC_GEN_COMPACT_ENC", "8").split(",") if x}
+COMPACT_DEC = {int(x) for x in os.environ.get("FEC_GEN_COMPACT_DEC", "").split(",") if x}
 COMPACT_VGPRS = 128
 
 
@@ -955,13 +956,16 @@ def main():
     tops = {}
     for RT in sorted(COMPACT_ENC):
         parts.append(f"#define FEC_V1_ENC{RT}_WAVES {512 // compact_vgprs(RT)}  // compact-map encode tiles (v1_compact_layout)")
+    for RT in sorted(COMPACT_DEC):
+        parts.append(f"#define FEC_V1_DEC{RT}_WAVES {512 // compact_vgprs(RT)}  // compact-map decode tiles")
     for mode in ("enc", "dec"):
         for RT, VEC in CONFIGS:
-            compact = mode == "enc" and RT in COMPACT_ENC
+            compact = RT in (COMPACT_ENC if mode == "enc" else COMPACT_DEC)
             with _Layout(v1_compact_layout() if compact else None):
                 if compact:
                     NP = 32 // VEC
-                    P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= compact_vgprs(RT)
+                    margin = int(os.environ.get("FEC_GEN_DEC_MARGIN", "14")) if mode == "dec" else 0
+                    P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= compact_vgprs(RT) - margin
                             and NP * (P - 1) <= 63)
                 else:
                     P = prefetch_depth(mode, RT, VEC)
