@@ -258,6 +258,10 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
         pthread_cond_broadcast(&b->cv_todo);
         pthread_mutex_unlock(&b->mu);
         for (int i = 0; i < started; i++) pthread_join(b->stager[i], NULL);
+        pthread_cond_destroy(&b->cv_todo);
+        pthread_cond_destroy(&b->cv_staged);
+        pthread_cond_destroy(&b->cv_done);
+        pthread_mutex_destroy(&b->mu);
         fecgpu_host_ctx_destroy(b->ctx);
         free(b);
         return NULL;
