@@ -27,7 +27,11 @@
 #ifdef FEC_BS_GEN_HEADER  // A/B experiments: an alternative generated body set
 #include FEC_BS_GEN_HEADER
 #else
+#ifdef FEC_GEN_HDR  // A/B builds of a generator variant (tools/gen_variant.py)
+#include FEC_GEN_HDR
+#else
 #include "bitslice_gen.h"
+#endif
 #endif
 #include "../../include/fecgpu.h"
 

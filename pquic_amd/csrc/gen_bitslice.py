@@ -39,9 +39,34 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.environ.get("FEC_GEN_OUT") or os.path.join(HERE, "bitslice_gen.h")
 
 # ----------------------------------------------------------------------------- register map
+# T64: the exchange rounds shift two words per instruction (v_lshlrev_b64 / v_lshrrev_b64 on an
+# aligned register pair) -- 36 VALU per transpose instead of 48.  The pairs a 64-bit shift takes
+# must be adjacent, so a lane's 8 words and a repair's 8 accumulator planes sit in the slot order
+# SIG (self-inverse: slot s holds logical word / plane SIG[s]), round 0 writes an 8-register
+# scratch block in natural order, round 1 runs in place there, round 2 writes the destination.
+T64 = os.environ.get("FEC_GEN_T64", "0") != "0"
+SIG64 = [0, 2, 1, 3, 4, 6, 5, 7]
+SIG = SIG64 if T64 else list(range(8))
+TAIL_HH = os.environ.get("FEC_GEN_TAIL_HH", "0") != "0"
+
+
+def table_map(B):
+    """Four-Russians table registers from B: the planes (singletons 1, 2, 4, 8 of TL and TH) at
+    B..B+7, the 22 combinations at B+8..B+29."""
+    tl = {1: B, 2: B + 1, 4: B + 2, 8: B + 3}
+    th = {1: B + 4, 2: B + 5, 4: B + 6, 8: B + 7}
+    for i, n in enumerate([3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15]):
+        tl[n] = B + 8 + i
+        th[n] = B + 19 + i
+    return tl, th
+
+
 T_BASE = 32
-TL = {n: T_BASE + n - 1 for n in range(1, 16)}          # v32..v46
-TH = {n: T_BASE + 15 + n - 1 for n in range(1, 16)}     # v47..v61
+if T64:
+    TL, TH = table_map(T_BASE)                           # v32..v61
+else:
+    TL = {n: T_BASE + n - 1 for n in range(1, 16)}      # v32..v46
+    TH = {n: T_BASE + 15 + n - 1 for n in range(1, 16)}  # v47..v61
 TMP = [62, 63, 64, 65]
 CO = TMP  # coefficient fields: read into the transpose temporaries once the transpose is done
 COPTR = 66
@@ -160,17 +185,25 @@ def emit_table(sym="fec_bs_case_table", tl=None, th=None):
     for c in range(256):
         body = []
         for o, (nl, nh) in enumerate(case_rows(c)):
+            s = SIG[o]  # plane o's accumulator slot
             if nl and nh:
-                body.append(f"v_bitop3_b32 v{o}, v{o}, {v(tl[nl])}, {v(th[nh])} bitop3:0x96")
+                body.append(f"v_bitop3_b32 v{s}, v{s}, {v(tl[nl])}, {v(th[nh])} bitop3:0x96")
             elif nl:
-                body.append(f"v_xor_b32 v{o}, v{o}, {v(tl[nl])}")
+                body.append(f"v_xor_b32 v{s}, v{s}, {v(tl[nl])}")
             elif nh:
-                body.append(f"v_xor_b32 v{o}, v{o}, {v(th[nh])}")
+                body.append(f"v_xor_b32 v{s}, v{s}, {v(th[nh])}")
         # chain tail: next repair's accumulators, next 16-bit case offset, jump (entry 0 returns)
-        body += [f"s_add_u32 m0, m0, 8",
-                 f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
-                 f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}",
-                 f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
+        if TAIL_HH:  # the next offset is the queue's second field: packed before the shift, so the
+            # jump waits on one SALU result instead of two (TAB.lo[31:16] comes from S_TAB itself)
+            body += [f"s_pack_hh_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TAB}",
+                     f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
+                     f"s_add_u32 m0, m0, 8",
+                     f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
+        else:
+            body += [f"s_add_u32 m0, m0, 8",
+                     f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
+                     f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}",
+                     f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]"]
         lines += ["  " + b for b in body]
         lines.append(f"  .org {sym} + {CASE_BYTES * (c + 2)}")
     return lines
@@ -212,6 +245,93 @@ def transpose_inplace(regs, tmp=None):
                     f"v_bitop3_b32 v{regs[a]}, s{S_MASK[mi]}, v{regs[a]}, v{t0} bitop3:0xca",
                     f"v_bitop3_b32 v{regs[b]}, s{S_MASK[mi]}, v{t1}, v{regs[b]} bitop3:0xca"]
     return out
+
+
+def t64_scratch(B):
+    """T64 scratch of a table map based at B: 8 consecutive registers for rounds 0-1 and two
+    register pairs of shift temporaries, all among the combination registers (dead between a
+    block's last case and the next source's combos; clear of the ring decode epilogue's B+8..B+12)."""
+    return list(range(B + 14, B + 22)), list(range(B + 22, B + 26))
+
+
+def transpose64(inp, out, X, T):
+    """The three exchange rounds with 64-bit shifts (36 VALU).  inp[w]: register of logical word
+    (or plane) w, with (inp[0], inp[2]), (inp[1], inp[3]), (inp[4], inp[6]), (inp[5], inp[7]) aligned
+    register pairs; out[p]: destination of plane (or word) p (may alias inp); X: 8 consecutive
+    scratch registers (aligned); T: 4 temporaries (two aligned pairs).
+    A 64-bit shift moves the low word's top bits into the high word's low bits (left) or the high
+    word's low bits into the low word's top bits (right); every mask keeps the other operand
+    there (its low s bits are set, its top s bits clear), so those bits never reach a result."""
+    assert X[0] % 2 == 0 and X == list(range(X[0], X[0] + 8))
+    assert T[0] % 2 == 0 and T[1] == T[0] + 1 and T[2] % 2 == 0 and T[3] == T[2] + 1
+    for h in (0, 4):
+        for a, b in ((h, h + 2), (h + 1, h + 3)):
+            assert inp[a] % 2 == 0 and inp[b] == inp[a] + 1, (inp, a, b)
+    assert not set(X) & set(inp) and not set(T) & (set(inp) | set(X))
+    m = [f"s{S_MASK[i]}" for i in range(3)]
+    mux = lambda d, sel, x, y: f"v_bitop3_b32 v{d}, {sel}, v{x}, v{y} bitop3:0xca"  # noqa: E731
+    tb, ta = T[0], T[2]
+    L = []
+    for h in (0, 4):  # round 0 (shift 1): pairs (h, h+1), (h+2, h+3); inp -> X
+        L += [f"v_lshlrev_b64 v[{tb}:{tb + 1}], 1, v[{inp[h + 1]}:{inp[h + 1] + 1}]",
+              f"v_lshrrev_b64 v[{ta}:{ta + 1}], 1, v[{inp[h]}:{inp[h] + 1}]",
+              mux(X[h], m[0], inp[h], tb), mux(X[h + 1], m[0], ta, inp[h + 1]),
+              mux(X[h + 2], m[0], inp[h + 2], tb + 1), mux(X[h + 3], m[0], ta + 1, inp[h + 3])]
+    for h in (0, 4):  # round 1 (shift 2): pairs (h, h+2), (h+1, h+3); in place in X
+        L += [f"v_lshlrev_b64 v[{tb}:{tb + 1}], 2, v[{X[h + 2]}:{X[h + 3]}]",
+              f"v_lshrrev_b64 v[{ta}:{ta + 1}], 2, v[{X[h]}:{X[h + 1]}]",
+              mux(X[h], m[1], X[h], tb), mux(X[h + 1], m[1], X[h + 1], tb + 1),
+              mux(X[h + 2], m[1], ta, X[h + 2]), mux(X[h + 3], m[1], ta + 1, X[h + 3])]
+    for g in (0, 2):  # round 2 (shift 4): pairs (g, g+4), (g+1, g+5); X -> out
+        L += [f"v_lshlrev_b64 v[{tb}:{tb + 1}], 4, v[{X[g + 4]}:{X[g + 5]}]",
+              f"v_lshrrev_b64 v[{ta}:{ta + 1}], 4, v[{X[g]}:{X[g + 1]}]",
+              mux(out[g], m[2], X[g], tb), mux(out[g + 1], m[2], X[g + 1], tb + 1),
+              mux(out[g + 4], m[2], ta, X[g + 4]), mux(out[g + 5], m[2], ta + 1, X[g + 5])]
+    return L
+
+
+def simulate(lines, regs):
+    """Run the exchange-round instructions of `lines` on a {vgpr: u32} register file (self-check)."""
+    import re
+    M = 0xFFFFFFFF
+    smask = {f"s{S_MASK[i]}": MASKS[i] for i in range(3)}
+    for ln in lines:
+        p = re.match(r"v_(lshl|lshr)rev_b64 v\[(\d+):(\d+)\], (\d+), v\[(\d+):(\d+)\]", ln)
+        if p:
+            d, s, x = int(p.group(2)), int(p.group(4)), int(p.group(5))
+            val = regs[x] | (regs[x + 1] << 32)
+            val = (val << s) if p.group(1) == "lshl" else (val >> s)
+            regs[d], regs[d + 1] = val & M, (val >> 32) & M
+            continue
+        p = re.match(r"v_(lshl|lshr)rev_b32 v(\d+), (\d+), v(\d+)", ln)
+        if p:
+            s, x = int(p.group(3)), regs[int(p.group(4))]
+            regs[int(p.group(2))] = ((x << s) if p.group(1) == "lshl" else (x >> s)) & M
+            continue
+        p = re.match(r"v_bitop3_b32 v(\d+), (s\d+), v(\d+), v(\d+) bitop3:0xca", ln)
+        assert p, ln
+        mk, a, b = smask[p.group(2)], regs[int(p.group(3))], regs[int(p.group(4))]
+        regs[int(p.group(1))] = ((mk & a) | (~mk & b)) & M
+    return regs
+
+
+def selfcheck_t64():
+    """transpose64 as the bodies call it: words loaded in slot order SIG -> planes; planes in
+    accumulator slots SIG -> words back in their load slots; and the transpose_inplace twin."""
+    rnd = random.Random(2)
+    base, X, T = 100, list(range(120, 128)), list(range(130, 134))
+    fwd = transpose64([base + SIG64[w] for w in range(8)], list(range(140, 148)), X, T)
+    inv = transpose64([base + SIG64[o] for o in range(8)], [base + SIG64[w] for w in range(8)], X, T)
+    for _ in range(200):
+        phys = [rnd.getrandbits(32) for _ in range(8)]  # slot s holds logical word SIG64[s]
+        words = [phys[SIG64[w]] for w in range(8)]
+        regs = {r: rnd.getrandbits(32) for r in range(100, 150)}
+        regs.update({base + s: phys[s] for s in range(8)})
+        simulate(fwd, regs)
+        assert [regs[140 + p] for p in range(8)] == transpose_model(words)
+        regs.update({base + SIG64[o]: transpose_model(words)[o] for o in range(8)})
+        simulate(inv, regs)
+        assert [regs[base + s] for s in range(8)] == phys
 
 
 def combos(tl=None, th=None):
@@ -350,7 +470,10 @@ def body(mode: str, RT: int, VEC: int, P: int):
         a(f"s_waitcnt vmcnt({63 if os.environ.get('FEC_GEN_NOVMWAIT') else NP * (P - 1)})")
         a(f".Lpf{b}_%=:")
         ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
-        L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
+        if T64:
+            L.extend(transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE)))
+        else:
+            L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
         # FEC_GEN_CONSTCOEF=1 (timing probe only, results are garbage): every live field is the
         # case of one fixed coefficient and no coefficient row is read
         constco = bool(os.environ.get("FEC_GEN_CONSTCOEF"))
@@ -412,7 +535,11 @@ def body(mode: str, RT: int, VEC: int, P: int):
         accs = [acc_base + 8 * i + w for w in range(8)]
         a(f"s_cmp_le_u32 s{S_RT}, {i}")
         a(f"s_cbranch_scc1 .Lepi_done_%=")
-        L.extend(transpose_inplace(accs))
+        if T64:
+            slots = [accs[SIG[o]] for o in range(8)]  # plane o / word o
+            L.extend(transpose64(slots, slots, *t64_scratch(T_BASE)))
+        else:
+            L.extend(transpose_inplace(accs))
         if mode == "dec":
             a(f"ds_read_b64 v[{TMP[2]}:{TMP[3]}], v{OUTPTR} offset:{8 * i}")
             a(f"v_or3_b32 v{TMP[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
@@ -666,7 +793,10 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
             a(f"v_mov_b32 v{TMPm[1]}, s{S_COPTR}")
             a(f"ds_read_b64 v[{TMPm[0]}:{TMPm[1]}], v{TMPm[1]}")
             a("s_waitcnt lgkmcnt(1)")
-        L.extend(transpose_inplace(PL, XT))
+        if T64:
+            L.extend(transpose64([PL[SIG[w]] for w in range(8)], PL, *t64_scratch(T2_BASE)))
+        else:
+            L.extend(transpose_inplace(PL, XT))
         L.extend(combos(TLm, THm))
         if NT >= 4:
             CO = TMPm[:ndw]
@@ -741,7 +871,11 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         accs = [acc_base + 8 * i + w for w in range(8)]
         a(f"s_cmp_le_u32 s{S_RT}, {i}")
         a(f"s_cbranch_scc1 .Lepi_done_%=")
-        L.extend(transpose_inplace(accs, TMPm))
+        if T64:
+            slots = [accs[SIG[o]] for o in range(8)]
+            L.extend(transpose64(slots, slots, *t64_scratch(T2_BASE)))
+        else:
+            L.extend(transpose_inplace(accs, TMPm))
         if mode == "dec":
             a(f"ds_read_b64 v[{E[0]}:{E[1]}], v{E[2]} offset:{8 * i}")
             a(f"v_or3_b32 v{E[3]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
@@ -900,6 +1034,7 @@ def compact_vgprs(RT: int) -> int:
 
 def main():
     selfcheck()
+    selfcheck_t64()
     parts = ["// GENERATED by pquic_amd/csrc/gen_bitslice.py -- do not edit.",
              "// Bitsliced GF(2^8) multiply-accumulate bodies for gfx950 (see the generator's docstring).",
              "#pragma once",
