@@ -44,7 +44,7 @@ OUT = os.environ.get("FEC_GEN_OUT") or os.path.join(HERE, "bitslice_gen.h")
 # must be adjacent, so a lane's 8 words and a repair's 8 accumulator planes sit in the slot order
 # SIG (self-inverse: slot s holds logical word / plane SIG[s]), round 0 writes an 8-register
 # scratch block in natural order, round 1 runs in place there, round 2 writes the destination.
-T64 = os.environ.get("FEC_GEN_T64", "0") != "0"
+T64 = os.environ.get("FEC_GEN_T64", "1") != "0"
 SIG64 = [0, 2, 1, 3, 4, 6, 5, 7]
 SIG = SIG64 if T64 else list(range(8))
 TAIL_HH = os.environ.get("FEC_GEN_TAIL_HH", "0") != "0"

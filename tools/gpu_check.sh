@@ -6,7 +6,7 @@ TAG=${1:-run}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 echo "pytest_rc=$?" >> $OUT/pytest_gpu.log
 tail -3 $OUT/pytest_gpu.log
 grep -q "pytest_rc=0" $OUT/pytest_gpu.log || exit 1
