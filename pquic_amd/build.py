@@ -61,13 +61,14 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     hip, c, _ = sources()
     hipcc = _hipcc()
     objs = []
+    odir = os.path.dirname(target)  # objects next to the target: variant builds may run in parallel
     inc = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     for src in c:  # host C: the protoop adapters stay C (reference language)
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
         _run(["gcc", "-std=c11", "-O2", "-fPIC", "-Wall", "-Wextra", "-c", src, "-o", obj] + inc)
         objs.append(obj)
     for src in hip:
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
         _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj] + inc +
              ["-D" + d for d in defines])
         objs.append(obj)
