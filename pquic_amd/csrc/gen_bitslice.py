@@ -48,6 +48,11 @@ T64 = os.environ.get("FEC_GEN_T64", "1") != "0"
 SIG64 = [0, 2, 1, 3, 4, 6, 5, 7]
 SIG = SIG64 if T64 else list(range(8))
 TAIL_HH = os.environ.get("FEC_GEN_TAIL_HH", "0") != "0"
+# EARLY_PF: the register-prefetch bodies refill a source buffer right after round 0 of its transpose
+# (P sources in flight, the load issued ~1 step earlier) instead of at the start of the next step
+EARLY_PF = T64 and os.environ.get("FEC_GEN_EARLY_PF", "1") != "0"
+# EARLY_CO (with EARLY_PF): a step's coefficient fields are read before its transpose, not after
+EARLY_CO = os.environ.get("FEC_GEN_EARLY_CO", "0") != "0"
 
 
 def table_map(B):
@@ -416,17 +421,18 @@ def body(mode: str, RT: int, VEC: int, P: int):
     # S_T2 = prefetches left (max(0, nsrc - (P - 1)))
     a(f"s_sub_u32 s{S_S}, %[nsrc], 1")
     a(f"s_sub_u32 s{S_J}, %[k], 1")
-    a(f"s_sub_u32 s{S_T2}, %[nsrc], {P - 1}")
+    a(f"s_sub_u32 s{S_T2}, %[nsrc], {P if EARLY_PF else P - 1}")
     a(f"s_cselect_b32 s{S_T2}, 0, s{S_T2}")
     if mode == "enc":
         a(f"s_mov_b32 s{S_JL}, 0")
 
-    def load_source(buf):
+    def load_source(buf, lgkm=0):
         out = []
         if mode == "dec":
             # this source's address was read one source ago (nothing else of the LDS queue is
-            # outstanding here, so the wait is free); then fetch the next one
-            out += ["s_waitcnt lgkmcnt(0)",
+            # outstanding here but, with EARLY_CO, this step's younger coefficient read, so the
+            # wait is free); then fetch the next one
+            out += [f"s_waitcnt lgkmcnt({lgkm})",
                     f"v_readfirstlane_b32 s{S_CUR}, v{NADDR}",
                     f"v_readfirstlane_b32 s{S_CUR + 1}, v{NADDR + 1}",
                     f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}",
@@ -447,7 +453,7 @@ def body(mode: str, RT: int, VEC: int, P: int):
                     f"s_addc_u32 s{S_CUR + 1}, s{S_CUR + 1}, s{S_CQ + 1}"]
         return out
 
-    for q in range(P - 1):  # prologue: sources 0 .. P-2
+    for q in range(P if EARLY_PF else P - 1):  # prologue: sources 0 .. P-1 (P-2 without EARLY_PF)
         a(f"s_cmp_lt_u32 {q}, %[nsrc]")
         a(f"s_cbranch_scc0 .Lpro_done_%=")
         L.extend(load_source(q))
@@ -460,20 +466,38 @@ def body(mode: str, RT: int, VEC: int, P: int):
     # block-end epilogue calls are out of line (after the loop), so a step costs no taken branch
     # besides its case chains
     ool = []
+    early_co = EARLY_PF and EARLY_CO and csb <= 16 and not os.environ.get("FEC_GEN_CONSTCOEF")
     for b in range(P):
         nb = (b + P - 1) % P
         a(f".Lbody{b}_%=:")
         a(f"s_sub_u32 s{S_T2}, s{S_T2}, 1")
         a(f"s_cbranch_scc1 .Lnopf{b}_%=")
-        L.extend(load_source(nb))
-        # FEC_GEN_NOVMWAIT=1 (timing probe only, results are garbage): no wait for the source rows
-        a(f"s_waitcnt vmcnt({63 if os.environ.get('FEC_GEN_NOVMWAIT') else NP * (P - 1)})")
-        a(f".Lpf{b}_%=:")
-        ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
-        if T64:
-            L.extend(transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE)))
+        if EARLY_PF:
+            # source s waits in buffer b; P sources are in flight.  Round 0 of the transpose is the
+            # buffer's only reader, so source s + P is loaded into it right after (SCC still holds
+            # the borrow of the S_T2 decrement: VALU and s_waitcnt leave it alone)
+            a(f"s_waitcnt vmcnt({NP * (P - 1)})")
+            a(f".Lpf{b}_%=:")
+            ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
+            tr = transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE))
+            if early_co:  # the coefficient fields (into CO = TMP, untouched by transpose64) go out first
+                a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
+                a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
+            L.extend(tr[:12])
+            a(f"s_cbranch_scc1 .Lnold{b}_%=")
+            L.extend(load_source(b, 1 if early_co else 0))
+            a(f".Lnold{b}_%=:")
+            L.extend(tr[12:])
         else:
-            L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
+            L.extend(load_source(nb))
+            # FEC_GEN_NOVMWAIT=1 (timing probe only, results are garbage): no wait for the source rows
+            a(f"s_waitcnt vmcnt({63 if os.environ.get('FEC_GEN_NOVMWAIT') else NP * (P - 1)})")
+            a(f".Lpf{b}_%=:")
+            ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
+            if T64:
+                L.extend(transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE)))
+            else:
+                L.extend(transpose_fwd([DATA_BASE + 8 * b + w for w in range(8)]))
         # FEC_GEN_CONSTCOEF=1 (timing probe only, results are garbage): every live field is the
         # case of one fixed coefficient and no coefficient row is read
         constco = bool(os.environ.get("FEC_GEN_CONSTCOEF"))
@@ -485,7 +509,7 @@ def body(mode: str, RT: int, VEC: int, P: int):
                 hi = fld if 2 * w + 1 < RT else 0
                 a(f"s_mov_b32 s{S_C[w]}, 0x{(hi << 16) | lo:08x}")
         # the coefficient fields land in the (now free) transpose temporaries under the combos
-        if not constco:
+        if not constco and not early_co:
             a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
             if csb <= 16:
                 a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
@@ -971,7 +995,7 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     # 2-wave budget for decode: RT=8 needs a larger margin than RT=16 (measured: a 242 budget at
     # RT=8 compiled to 256 VGPRs + 4 AGPRs = 1 wave/SIMD, k32 e8 apply 13 ms -> 7.6 ms at 222)
     budget2 = 256 - margin - (8 if mode == "dec" and RT <= 8 else 0)
-    fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - 1) <= 63
+    fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - (0 if EARLY_PF else 1)) <= 63
     forced = os.environ.get(f"FEC_GEN_LIMIT_{mode.upper()}_RT{RT}") or os.environ.get(f"FEC_GEN_LIMIT_RT{RT}")
     if forced:  # A/B: VGPR limit for this tile size
         return max([P for P in range(2, 33) if fits(P, int(forced) - margin)] or [2])
@@ -1101,7 +1125,7 @@ def main():
                     NP = 32 // VEC
                     margin = int(os.environ.get("FEC_GEN_DEC_MARGIN", "14")) if mode == "dec" else 0
                     P = max(P for P in range(2, 33) if data_base(mode) + 8 * P + 8 * RT <= compact_vgprs(RT) - margin
-                            and NP * (P - 1) <= 63)
+                            and NP * (P - (0 if EARLY_PF else 1)) <= 63)
                 else:
                     P = prefetch_depth(mode, RT, VEC)
                 fn, top = emit_function(mode, RT, VEC, P)
