@@ -773,6 +773,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     nch = max(1, RT // 4)
     base_wait = NDMA * (D - 2)
     ool = []
+    const2 = mode == "enc" and NT == 2 and bool(os.environ.get("FEC_GEN2_PROBE_CONST"))
 
     def data_reads(b):
         return [f"ds_read_b128 v[{PL[0]}:{PL[3]}], %[rd1] offset:{b * S2_SLOT}",
@@ -784,7 +785,8 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"s_cbranch_scc1 .Lnodma{b}_%=")
         a(f"s_cmp_lg_u32 s{S_PEND}, 0")
         a(f"s_cbranch_scc1 .Lbigwait{b}_%=")
-        a(f"s_waitcnt vmcnt({base_wait})")
+        # FEC_GEN2_PROBE_NOVM=1 (timing probe only, results are garbage): no wait for the DMA
+        a(f"s_waitcnt vmcnt({63 if os.environ.get('FEC_GEN2_PROBE_NOVM') else base_wait})")
         a(f".Lgot{b}_%=:")
         L.extend(data_reads(b))
         if mode == "dec":  # the address read one step ago (issued before this step's data reads)
@@ -813,10 +815,13 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
             a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
             a(f"{dsr} {regrange(TMPm[0], ndw)}, v{TMPm[3]}")
             a("s_waitcnt lgkmcnt(1)")
+        elif const2:
+            a("s_waitcnt lgkmcnt(0)")
         else:
             a(f"v_mov_b32 v{TMPm[1]}, s{S_COPTR}")
             a(f"ds_read_b64 v[{TMPm[0]}:{TMPm[1]}], v{TMPm[1]}")
-            a("s_waitcnt lgkmcnt(1)")
+            # FEC_GEN2_PROBE_NOLDS=1 (timing probe only, results are garbage): no wait for the data reads
+            a("s_nop 0" if os.environ.get("FEC_GEN2_PROBE_NOLDS") else "s_waitcnt lgkmcnt(1)")
         if T64:
             L.extend(transpose64([PL[SIG[w]] for w in range(8)], PL, *t64_scratch(T2_BASE)))
         else:
@@ -841,6 +846,17 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                 a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
                 if ch % 2 == 0:
                     a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+        elif const2:
+            # FEC_GEN2_PROBE_CONST=1 (timing probe only, results are garbage): the fields are SGPR
+            # constants (no LDS reads, no readfirstlane) and GPR-index mode stays on across the chains
+            fld = (0x53 + 1) * CASE_BYTES
+            a(f"s_set_gpr_idx_on {acc_base}, gpr_idx(SRC0,DST)")
+            for ch in range(nch):
+                a(f"s_mov_b32 s{S_C[0]}, 0x{(fld << 16) | fld:08x}")
+                a(f"s_mov_b32 s{S_C[1]}, 0x{(fld << 16) | fld:08x}")
+                a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[0]}:{S_C[1]}]")
+                a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
                 a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
         else:
             # two temporaries: each chain's 4 fields (8 B) are read while the previous chain runs
