@@ -1277,19 +1277,20 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
     if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
-      uint16_t *row = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB) + i;  // field i of source j
+      uint16_t *row0 = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB);
+      uint16_t *row = row0 + FEC_BS_FIELD_SLOT(RT, i);  // field i of source j
       if (g < ng && i < rt) {
         Tmt t;
         const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
         tmt_init(t, rlc_seed(f, (uint32_t)(r0w + i)));
-        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = (uint16_t)((tmt_coef(t) + 1u) * FEC_BS_CASE_BYTES);
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD(tmt_coef(t), i);
       } else {
         for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;  // ends the chain: repair i is not live
       }
       if constexpr (RT < 4) {  // the unused fields of a 4-field row end the chain as well
         if (i == 0)
           for (int j = 0; j < k; j++)
-            for (int x = RT; x < 4; x++) row[j * (CSB / 2) + x] = 0;
+            for (int x = RT; x < 4; x++) row0[j * (CSB / 2) + FEC_BS_FIELD_SLOT(RT, x)] = 0;
       }
     }
     __syncthreads();
@@ -1381,7 +1382,7 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
       uint16_t *row = reinterpret_cast<uint16_t *>(S.coef + (size_t)x * RecoverLds<RT>::CSB);
 #pragma unroll
       for (int u = 0; u < NF; u++)  // case offset of D[u][j]; 0 past the live unknowns ends the chain
-        row[u] = (u < rt) ? (uint16_t)((h[WL.off_D + (r0 + u) * k + j] + 1u) * FEC_BS_CASE_BYTES) : (uint16_t)0;
+        row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD(h[WL.off_D + (r0 + u) * k + j], u) : (uint16_t)0;
       const uint32_t sl = h[WL.off_slot + j];
       const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
                                      : src + (b * (uint64_t)k + sl) * (uint64_t)L;
@@ -1648,19 +1649,20 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
     if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0 + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
-      uint16_t *row = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB) + i;
+      uint16_t *row0 = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB);
+      uint16_t *row = row0 + FEC_BS_FIELD_SLOT(RT, i);
       if (g < ng && i < rt) {
         Tmt t;
         const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
         tmt_init(t, rlc_seed(f, (uint32_t)(r0 + i)));
-        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = (uint16_t)((tmt_coef(t) + 1u) * FEC_BS_CASE_BYTES);
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD(tmt_coef(t), i);
       } else {
         for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;
       }
       if constexpr (RT < 4) {
         if (i == 0)
           for (int j = 0; j < k; j++)
-            for (int x = RT; x < 4; x++) row[j * (CSB / 2) + x] = 0;
+            for (int x = RT; x < 4; x++) row0[j * (CSB / 2) + FEC_BS_FIELD_SLOT(RT, x)] = 0;
       }
     }
     __syncthreads();
@@ -1725,7 +1727,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       uint16_t *row = reinterpret_cast<uint16_t *>(S.coef + (size_t)x * RecoverLds<RT>::CSB);
 #pragma unroll
       for (int u = 0; u < NF; u++)
-        row[u] = (u < rt) ? (uint16_t)((h[WL.off_D + (r0 + u) * k + j] + 1u) * FEC_BS_CASE_BYTES) : (uint16_t)0;
+        row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD(h[WL.off_D + (r0 + u) * k + j], u) : (uint16_t)0;
       const uint32_t sl = h[WL.off_slot + j];
       const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
                                      : src + (b * (uint64_t)k + sl) * (uint64_t)L;

@@ -48,6 +48,13 @@ T64 = os.environ.get("FEC_GEN_T64", "1") != "0"
 SIG64 = [0, 2, 1, 3, 4, 6, 5, 7]
 SIG = SIG64 if T64 else list(range(8))
 TAIL_HH = os.environ.get("FEC_GEN_TAIL_HH", "0") != "0"
+# AB: two case tables in one 64 KiB window.  Table A (offset 0) holds the cases of even chain
+# positions, table B (offset TABLE_B) those of odd positions, with the accumulators 8 registers
+# further on.  An A case takes its successor from queue QB (s[S_C2:S_C3]), a B case from queue QA
+# (s[S_C0:S_C1]) and advances M0 by 16: two SALU per A case, three per B case (three each without
+# AB), and the two 64-bit queues hold 8 fields, so an 8-repair tile is one chain (two without AB).
+AB = os.environ.get("FEC_GEN_AB", "0") != "0"
+TABLE_B = 32768
 # EARLY_PF: the register-prefetch bodies refill a source buffer right after round 0 of its transpose
 # (P sources in flight, the load issued ~1 step earlier) instead of at the start of the next step
 EARLY_PF = T64 and os.environ.get("FEC_GEN_EARLY_PF", "1") != "0"
@@ -187,6 +194,32 @@ def emit_table(sym="fec_bs_case_table", tl=None, th=None):
     # entry 0: the chain's end (a zero field) returns to the caller
     lines.append(f"  s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
     lines.append(f"  .org {sym} + {CASE_BYTES}")
+    if AB:
+        assert not TAIL_HH and TABLE_B + 257 * CASE_BYTES <= 65536
+        for half, base in ((0, 0), (1, TABLE_B)):
+            if half:
+                lines.append(f"  .org {sym} + {TABLE_B}")
+                lines.append(f"  s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+            for c in range(256):
+                lines.append(f"  .org {sym} + {base + CASE_BYTES * (c + 1)}")
+                body = []
+                for o, (nl, nh) in enumerate(case_rows(c)):
+                    d = 8 * half + SIG[o]
+                    if nl and nh:
+                        body.append(f"v_bitop3_b32 v{d}, v{d}, {v(tl[nl])}, {v(th[nh])} bitop3:0x96")
+                    elif nl:
+                        body.append(f"v_xor_b32 v{d}, v{d}, {v(tl[nl])}")
+                    elif nh:
+                        body.append(f"v_xor_b32 v{d}, v{d}, {v(th[nh])}")
+                q = S_C[0] if half else S_C[2]  # successor: an A case's is in QB, a B case's in QA
+                body += [f"s_pack_ll_b32_b16 s{S_TGT}, s{q}, s{S_TABHI}",
+                         f"s_lshr_b64 s[{q}:{q + 1}], s[{q}:{q + 1}], 16"]
+                if half:
+                    body.append("s_add_u32 m0, m0, 16")
+                body.append(f"s_setpc_b64 s[{S_TGT}:{S_TGT + 1}]")
+                lines += ["  " + b for b in body]
+        lines.append(f"  .org {sym} + {TABLE_B + CASE_BYTES * 257}")
+        return lines
     for c in range(256):
         body = []
         for o, (nl, nh) in enumerate(case_rows(c)):
@@ -408,6 +441,9 @@ def body(mode: str, RT: int, VEC: int, P: int):
     for r in range(DATA_BASE, DATA_BASE + 8 * P):
         a(f"v_mov_b32 v{r}, 0")
     a(f"v_mov_b32 v{COPTR}, %[coef]")
+    if AB and coef_row_bytes(RT) == 8:  # rows of 4 fields: QA / QB are one dword each
+        a(f"s_mov_b32 s{S_C[1]}, 0")
+        a(f"s_mov_b32 s{S_C[3]}, 0")
     if mode == "enc":
         a(f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], %[src]")
         a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
@@ -514,16 +550,36 @@ def body(mode: str, RT: int, VEC: int, P: int):
             if csb <= 16:
                 a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
         L.extend(combos())
-        if constco:
+        if AB:
+            # QA = s[S_C0:S_C1], QB = s[S_C2:S_C3] (rows of 4 fields: one dword each, the high
+            # dwords stay 0); one chain per 8 fields, entered at QA's first field
+            assert not constco
+            a("s_waitcnt lgkmcnt(0)")
+            for w in range(ndw):
+                a(f"v_readfirstlane_b32 s{S_C[w if ndw == 4 else 2 * w]}, v{CO[w]}")
+            if csb == 32:
+                a(f"ds_read_b128 {regrange(CO[0], 4)}, v{COPTR} offset:16")
+                a(f"v_add_u32 v{COPTR}, 32, v{COPTR}")
+            for ch in range(max(1, RT // 8)):
+                if ch:
+                    a("s_set_gpr_idx_off")
+                    a("s_waitcnt lgkmcnt(0)")
+                    for w in range(4):
+                        a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
+                a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_C[0]}, s{S_TABHI}")
+                a(f"s_lshr_b64 s[{S_C[0]}:{S_C[1]}], s[{S_C[0]}:{S_C[1]}], 16")
+                a(f"s_set_gpr_idx_on {acc_base + 64 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+        elif constco:
             const_fields()
         else:
             a("s_waitcnt lgkmcnt(0)")
             for w in range(ndw):
                 a(f"v_readfirstlane_b32 s{S_C[w]}, v{CO[w]}")
-        if csb == 32 and not constco:  # second half of the offsets lands while the first two chains run
+        if csb == 32 and not constco and not AB:  # second half of the offsets lands while the first two chains run
             a(f"ds_read_b128 {regrange(CO[0], 4)}, v{COPTR} offset:16")
             a(f"v_add_u32 v{COPTR}, 32, v{COPTR}")
-        for ch in range(nch):
+        for ch in range(0 if AB else nch):
             if ch == 2:  # RT = 16: offsets 8..15 (no VALU may run in GPR-index mode)
                 a("s_set_gpr_idx_off")
                 if not constco:
@@ -710,6 +766,9 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     for r in range(acc_base, acc_base + 8 * RT):
         a(f"v_mov_b32 v{r}, 0")
     a(f"s_mov_b32 s{S_COPTR}, %[coef]")
+    if AB:  # QA / QB hold one dword of fields each
+        a(f"s_mov_b32 s{S_C[1]}, 0")
+        a(f"s_mov_b32 s{S_C[3]}, 0")
     if mode == "enc":
         a(f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], %[src]")
         a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
@@ -773,6 +832,15 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     nch = max(1, RT // 4)
     base_wait = NDMA * (D - 2)
     ool = []
+    assert not AB or NT == 2
+
+    def fld_read(ch):
+        """AB: chain ch's QA and QB dwords of the coefficient row (FEC_BS_FIELD_SLOT layout) into T0, T1"""
+        if csb == 8:
+            d0, d1 = 0, 1
+        else:
+            d0, d1 = 4 * (ch // 2) + ch % 2, 4 * (ch // 2) + 2 + ch % 2
+        return [f"v_mov_b32 v{T1}, s{S_COPTR}", f"ds_read2_b32 v[{T0}:{T1}], v{T1} offset0:{d0} offset1:{d1}"]
     const2 = mode == "enc" and NT == 2 and bool(os.environ.get("FEC_GEN2_PROBE_CONST"))
 
     def data_reads(b):
@@ -809,8 +877,10 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         # after the chains), so its fields go out after that read is taken
         if mode == "dec":
             a("s_waitcnt lgkmcnt(0)")
-            a(f"v_mov_b32 v{T1}, s{S_COPTR}")
-            a(f"ds_read_b64 v[{T0}:{T1}], v{T1}")
+            L.extend(fld_read(0) if AB else [f"v_mov_b32 v{T1}, s{S_COPTR}", f"ds_read_b64 v[{T0}:{T1}], v{T1}"])
+        elif AB:
+            L.extend(fld_read(0))
+            a("s_waitcnt lgkmcnt(1)")
         elif NT >= 4:
             a(f"v_mov_b32 v{TMPm[3]}, s{S_COPTR}")
             a(f"{dsr} {regrange(TMPm[0], ndw)}, v{TMPm[3]}")
@@ -858,6 +928,22 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                 a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[0]}:{S_C[1]}]")
                 a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
                 a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+        elif AB:
+            # two temporaries: each chain's QA / QB dwords (2 fields each) are read while the previous
+            # chain runs; QA and QB are s[S_C0:S_C1] and s[S_C2:S_C3], their high dwords 0
+            for ch in range(nch):
+                if ch:
+                    a("s_set_gpr_idx_off")
+                a("s_waitcnt lgkmcnt(0)")
+                a(f"v_readfirstlane_b32 s{S_C[0]}, v{T0}")
+                a(f"v_readfirstlane_b32 s{S_C[2]}, v{T1}")
+                if ch + 1 < nch:
+                    L.extend(fld_read(ch + 1))
+                a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_C[0]}, s{S_TABHI}")
+                a(f"s_lshr_b64 s[{S_C[0]}:{S_C[1]}], s[{S_C[0]}:{S_C[1]}], 16")
+                a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+            a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
         else:
             # two temporaries: each chain's 4 fields (8 B) are read while the previous chain runs
             T0, T1 = TMPm[0], TMPm[1]
@@ -1084,6 +1170,19 @@ def main():
              f"#define FEC_BS_CASE_BYTES {CASE_BYTES}",
              "// LDS coefficient row per source: max(4, RT) u16 fields (c + 1) * FEC_BS_CASE_BYTES, 0 ends a chain",
              "#define FEC_BS_COEF_ROW_BYTES(RT) (2 * ((RT) < 4 ? 4 : (RT)))",
+             f"#define FEC_BS_AB {int(AB)}  // two case tables (even / odd chain positions, gen_bitslice.py AB)",
+             f"#define FEC_BS_TABLE_B {TABLE_B}",
+             "// slot of repair (unknown) i in its row and its field for coefficient c: with AB, each group of",
+             "// g = 8 (RT >= 8) or 4 fields holds the even positions' fields (queue QA) before the odd ones'",
+             "// (queue QB), and odd positions point into table B",
+             "#if FEC_BS_AB",
+             "#define FEC_BS_FIELD_SLOT(RT, i) ((((RT) >= 8 ? 8 : 4) * ((i) / ((RT) >= 8 ? 8 : 4))) + \\",
+             "    (((i) & 1) ? ((RT) >= 8 ? 4 : 2) : 0) + ((i) % ((RT) >= 8 ? 8 : 4)) / 2)",
+             "#define FEC_BS_FIELD(c, i) ((uint16_t)(((c) + 1u) * FEC_BS_CASE_BYTES + (((i) & 1) ? FEC_BS_TABLE_B : 0)))",
+             "#else",
+             "#define FEC_BS_FIELD_SLOT(RT, i) (i)",
+             "#define FEC_BS_FIELD(c, i) ((uint16_t)(((c) + 1u) * FEC_BS_CASE_BYTES))",
+             "#endif",
              "#ifndef FEC_LD_POL",
              "#define FEC_LD_POL \"\"  // symbol loads: default policy (nt loads measured slower for decode)",
              "#endif",
