@@ -2,14 +2,17 @@
  * pquic_amd/csrc/batch.c -- batching adapter for the block FEC framework
  * (include/pquic_fec_batch.h).  Host C, like the framework it serves.
  *
- * Submission only checks the reference's preconditions and records the block in the open "job"
- * (one per operation, scheme, k and r).  A full or overdue job goes through a two-stage
- * pipeline off the caller's thread:
+ * Submission checks the reference's preconditions and records the block in the open "job"
+ * (one per operation, scheme, k and r); a generate submission also allocates the block's r
+ * repair symbols there, on the caller's thread like every allocator call.  A full or overdue
+ * job goes through a pipeline off the caller's thread:
  *   - stager threads (several jobs at once) copy each block into the job's page-locked rows: k
  *     source rows (+ r repair rows for recover) of `stride` bytes, zero-padded like the
  *     reference pads to max_length, plus presence masks;
  *   - the engine thread runs staged jobs through the host-resident entry points (zero-copy
- *     kernels on the page-locked rows).
+ *     kernels on the page-locked rows);
+ *   - for generate, the stager threads copy the repair rows into the symbols allocated at
+ *     submission (the caller's thread was the bound when it copied them itself).
  * Finished jobs are completed on the caller's thread in poll / drain with the same finish
  * halves the synchronous operations use (fec_core.c), so a batched block ends in exactly the
  * state the protocol operation would leave it in.  The caller keeps a block unmodified until
@@ -36,6 +39,7 @@ typedef struct {
     pquic_fec_block_done_fn done;
     void *user;
     uint16_t maxl;
+    int16_t nalloc;                /* generate: repair symbols allocated at submission */
 } entry_t;
 
 typedef struct job {
@@ -49,8 +53,11 @@ typedef struct job {
     size_t seed_bytes;
     uint64_t *sp, *rp, *rec;       /* pinned, 2 words per block */
     entry_t *ent;
+    pquic_repair_symbol_t **reps;  /* generate: [cap][r] symbols allocated at submission */
+    size_t reps_cap;
     uint64_t t_first;
     int rc;
+    int post;                      /* 1 once the engine ran: work items copy repairs out */
     uint32_t next_chunk, chunks_done;  /* staging work items claimed / finished (under the batcher lock) */
 } job_t;
 
@@ -65,7 +72,7 @@ struct pquic_fec_batcher {
     int nstagers;
     pthread_mutex_t mu;
     pthread_cond_t cv_todo, cv_staged, cv_done;
-    job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *done_head, *done_tail;
+    job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *post_head, *post_tail, *done_head, *done_tail;
     int inflight, stop, stagers_done;
     pquic_fec_batch_stats_t stats;
 };
@@ -79,6 +86,7 @@ static void job_free(job_t *j) {
     fecgpu_host_free(j->seeds);
     fecgpu_host_free(j->sp);
     free(j->ent);
+    free(j->reps);
     free(j);
 }
 
@@ -110,6 +118,16 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
             return NULL;
         }
     }
+    if (op == OP_GENERATE && j->reps_cap < (size_t)cap * r) {
+        pquic_repair_symbol_t **nr = realloc(j->reps, sizeof *nr * (size_t)cap * r);
+        if (!nr) {
+            j->next = b->free_jobs;
+            b->free_jobs = j;
+            return NULL;
+        }
+        j->reps = nr;
+        j->reps_cap = (size_t)cap * r;
+    }
     j->rp = j->sp + 2 * (size_t)cap;
     j->rec = j->rp + 2 * (size_t)cap;
     j->next = NULL;
@@ -121,6 +139,7 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
     j->cap = cap;
     j->stride = S;
     j->rc = 0;
+    j->post = 0;
     j->next_chunk = j->chunks_done = 0;
     return j;
 }
@@ -152,31 +171,55 @@ static void stage_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     }
 }
 
+/* Generate, after the engine: repair rows of blocks [i0, i1) into the symbols allocated at
+ * submission (the copy half of fec_generate_finish). */
+static void copy_out_blocks(job_t *j, uint32_t i0, uint32_t i1) {
+    const uint32_t S = j->stride, r = j->r;
+    for (uint32_t i = i0; i < i1; i++) {
+        const entry_t *e = &j->ent[i];
+        for (int x = 0; x < e->nalloc; x++)
+            memcpy(j->reps[(size_t)i * r + x]->data, j->rep + ((size_t)i * r + x) * S, e->maxl);
+    }
+}
+
+static void push(job_t **head, job_t **tail, job_t *j) {
+    j->next = NULL;
+    if (*tail) (*tail)->next = j; else *head = j;
+    *tail = j;
+}
+
 /* Stager threads split every job into work items of STAGE_CHUNK blocks, so several threads copy
  * one job at once (a 4096-block k16 job is 79 MB of rows: one thread alone bounded the saturated
- * rate); the thread finishing a job's last item hands it to the engine thread. */
+ * rate); the thread finishing a job's last item hands it on: a staged job to the engine thread,
+ * a copied-out one to the caller.  Copy-out items go first (they finish jobs). */
 static void *stager_main(void *arg) {
     pquic_fec_batcher_t *b = arg;
     pthread_mutex_lock(&b->mu);
     for (;;) {
-        while (!b->todo_head && !b->stop) pthread_cond_wait(&b->cv_todo, &b->mu);
-        if (!b->todo_head) break;  /* stop requested and nothing left */
-        job_t *j = b->todo_head;
+        while (!b->todo_head && !b->post_head && !b->stop) pthread_cond_wait(&b->cv_todo, &b->mu);
+        job_t **head = b->post_head ? &b->post_head : &b->todo_head;
+        job_t **tail = b->post_head ? &b->post_tail : &b->todo_tail;
+        if (!*head) break;  /* stop requested and nothing left */
+        job_t *j = *head;
         const uint32_t nchunks = (j->n + STAGE_CHUNK - 1) / STAGE_CHUNK;
         const uint32_t c = j->next_chunk++;
         if (j->next_chunk >= nchunks) {  /* every item of this job is claimed: the next job is up */
-            b->todo_head = j->next;
-            if (!b->todo_head) b->todo_tail = NULL;
+            *head = j->next;
+            if (!*head) *tail = NULL;
         }
         pthread_mutex_unlock(&b->mu);
         const uint32_t i0 = c * STAGE_CHUNK, i1 = i0 + STAGE_CHUNK < j->n ? i0 + STAGE_CHUNK : j->n;
-        stage_blocks(j, i0, i1);
+        if (j->post) copy_out_blocks(j, i0, i1); else stage_blocks(j, i0, i1);
         pthread_mutex_lock(&b->mu);
         if (++j->chunks_done == nchunks) {
-            j->next = NULL;
-            if (b->staged_tail) b->staged_tail->next = j; else b->staged_head = j;
-            b->staged_tail = j;
-            pthread_cond_signal(&b->cv_staged);
+            if (j->post) {
+                push(&b->done_head, &b->done_tail, j);
+                b->inflight--;
+                pthread_cond_broadcast(&b->cv_done);
+            } else {
+                push(&b->staged_head, &b->staged_tail, j);
+                pthread_cond_signal(&b->cv_staged);
+            }
         }
     }
     b->stagers_done++;
@@ -215,11 +258,16 @@ static void *worker_main(void *arg) {
         pthread_mutex_unlock(&b->mu);
         run_engine(b, j);
         pthread_mutex_lock(&b->mu);
-        j->next = NULL;
-        if (b->done_tail) b->done_tail->next = j; else b->done_head = j;
-        b->done_tail = j;
-        b->inflight--;
-        pthread_cond_broadcast(&b->cv_done);
+        if (j->op == OP_GENERATE && !j->rc) {  /* the repair rows go to their symbols on the stagers */
+            j->post = 1;
+            j->next_chunk = j->chunks_done = 0;
+            push(&b->post_head, &b->post_tail, j);
+            pthread_cond_broadcast(&b->cv_todo);
+        } else {
+            push(&b->done_head, &b->done_tail, j);
+            b->inflight--;
+            pthread_cond_broadcast(&b->cv_done);
+        }
     }
     pthread_mutex_unlock(&b->mu);
     return NULL;
@@ -350,7 +398,9 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     if (!j) return -1;
     const uint32_t i = j->n;
     j->fbn[i] = fb->fec_block_number & 0xffffffu;  /* rows are copied later, by a stager */
-    j->ent[i] = (entry_t){cnx, fb, done, user, maxl};
+    j->ent[i] = (entry_t){cnx, fb, done, user, maxl, -1};
+    if (op == OP_GENERATE)  /* the protocol operation's allocations, in its order, on this thread */
+        j->ent[i].nalloc = (int16_t)fec_generate_alloc(cnx, fb, maxl, j->reps + (size_t)i * r);
     if (!i) j->t_first = now_us;
     j->n = i + 1;
     b->stats.submitted++;
@@ -382,11 +432,16 @@ static int collect(pquic_fec_batcher_t *b) {
         for (uint32_t i = 0; i < j->n; i++) {
             entry_t *e = &j->ent[i];
             protoop_arg_t ret;
+            pquic_repair_symbol_t **reps = j->op == OP_GENERATE ? j->reps + (size_t)i * j->r : NULL;
             if (j->rc) {
                 FEC_STAT_ADD(errors, 1);
                 ret = PQUIC_FEC_ERR_UNBOUND;
+                for (int x = 0; reps && x < e->nalloc; x++) {  /* nothing reaches the block */
+                    g_fec_api.my_free(e->cnx, reps[x]->data);
+                    g_fec_api.my_free(e->cnx, reps[x]);
+                }
             } else if (j->op == OP_GENERATE) {
-                ret = fec_generate_finish(e->cnx, e->fb, j->rep + (size_t)i * j->r * S, S, e->maxl);
+                ret = fec_generate_attach(e->fb, reps, e->nalloc);
             } else {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);

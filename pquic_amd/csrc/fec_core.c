@@ -65,18 +65,29 @@ void fec_generate_stage(const pquic_fec_block_t *fb, uint8_t *src_rows, uint32_t
     }
 }
 
-protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, const uint8_t *rep_rows,
-                                  uint32_t stride, uint16_t maxl) {
+int fec_generate_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t maxl,
+                       pquic_repair_symbol_t **reps) {
     const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     for (int i = 0; i < fb->total_repair_symbols; i++) {
         /* repair fpid: raw 0, fec_block_number, symbol_number = i, fec_scheme_specific 0
          * (rlc_fec_scheme_generate_gf256.c:57-61; xor_fec_scheme_generate.c:71-75) */
-        pquic_repair_symbol_t *rs = new_repair(cnx, ((uint64_t)fbn << 8) | (uint64_t)(i & 0xff), maxl);
-        if (!rs) return PQUIC_ERROR_MEMORY;
-        memcpy(rs->data, rep_rows + (size_t)i * stride, maxl);
-        fb->repair_symbols[i] = rs;
+        reps[i] = new_repair(cnx, ((uint64_t)fbn << 8) | (uint64_t)(i & 0xff), maxl);
+        if (!reps[i]) return i;
     }
-    return 0;
+    return fb->total_repair_symbols;
+}
+
+protoop_arg_t fec_generate_attach(pquic_fec_block_t *fb, pquic_repair_symbol_t *const *reps, int nalloc) {
+    for (int i = 0; i < nalloc; i++) fb->repair_symbols[i] = reps[i];
+    return nalloc < fb->total_repair_symbols ? PQUIC_ERROR_MEMORY : 0;
+}
+
+protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, const uint8_t *rep_rows,
+                                  uint32_t stride, uint16_t maxl) {
+    pquic_repair_symbol_t *reps[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
+    const int n = fec_generate_alloc(cnx, fb, maxl, reps);
+    for (int i = 0; i < n; i++) memcpy(reps[i]->data, rep_rows + (size_t)i * stride, maxl);
+    return fec_generate_attach(fb, reps, n);
 }
 
 int fec_recover_check(const pquic_fec_block_t *fb, int xor_scheme, uint16_t *maxl) {

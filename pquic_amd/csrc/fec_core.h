@@ -41,6 +41,14 @@ void fec_generate_stage(const pquic_fec_block_t *fb, uint8_t *src_rows, uint32_t
  * fb->repair_symbols with FPID (fbn << 8 | i) (:57-61).  Returns 0 or PQUIC_ERROR_MEMORY. */
 protoop_arg_t fec_generate_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, const uint8_t *rep_rows,
                                   uint32_t stride, uint16_t maxl);
+/* The same in three steps, so the copy can run off the allocator's thread (batch.c):
+ * fec_generate_alloc allocates the r repair symbols (FPIDs and lengths set, data unwritten) into
+ * reps[0..r) and returns how many it got (r, or the index of the first failed allocation);
+ * after their data is written, fec_generate_attach stores them in the block and returns the
+ * operation's value (0, or PQUIC_ERROR_MEMORY when an allocation failed). */
+int fec_generate_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t maxl,
+                       pquic_repair_symbol_t **reps);
+protoop_arg_t fec_generate_attach(pquic_fec_block_t *fb, pquic_repair_symbol_t *const *reps, int nalloc);
 
 /* Recover, before the engine.  Returns FEC_STAGE_OK when the block goes to the engine;
  * otherwise the value the reference operation returns without doing anything
