@@ -40,8 +40,17 @@ static void mh_set_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, pro
     }
 }
 
+static long g_fail_after = -1;  /* allocation-failure injection: the n-th allocation from now fails */
+
+void mh_fail_alloc_after(long n) { g_fail_after = n; }
+
 static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
     (void)cnx;
+    if (g_fail_after == 0) {
+        g_fail_after = -1;
+        return NULL;
+    }
+    if (g_fail_after > 0) g_fail_after--;
     void *p = malloc(size <= 2092 ? 2100 : size);
     if (p) g_live++;
     return p;
@@ -123,6 +132,10 @@ static void free_block(pquic_fec_block_t *fb) {
     free(fb);
 }
 
+static long g_fail_next_op = -1;
+/* the next mh_generate's operation fails its n-th allocation (the block is built before) */
+void mh_fail_next_generate(long n) { g_fail_next_op = n; }
+
 /* Sender side: k sources -> fec_generate_repair_symbols.  Returns the protoop's code;
  * repairs copied to rep_out[i * stride], lengths / raw FPIDs per repair. */
 long mh_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
@@ -141,8 +154,11 @@ long mh_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
     fb->total_source_symbols = (uint8_t)k;      /* block_framework_sender.h:184-185 */
     fb->total_repair_symbols = (uint8_t)r;
     protoop_arg_t in[2] = {(protoop_arg_t)(uintptr_t)fb, schemes[1]};
+    g_fail_after = g_fail_next_op;  /* armed for the operation only (mh_fail_next_generate) */
+    g_fail_next_op = -1;
     ret = run_protoop(&cnx, xor_scheme ? pquic_fec_xor_generate_repair_symbols : pquic_fec_rlc_generate_repair_symbols,
                       2, in, NULL);
+    g_fail_after = -1;
     for (int i = 0; i < r; i++) {
         pquic_repair_symbol_t *rs = fb->repair_symbols[i];
         rep_len[i] = rs ? rs->data_length : 0;
@@ -307,6 +323,8 @@ long mh_batch_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t
     fb->total_source_symbols = (uint8_t)k;
     fb->total_repair_symbols = (uint8_t)r;
     long t = new_ticket(fb, k, r);
+    g_fail_after = g_fail_next_op;  /* armed from here on: the caller disarms after the completion */
+    g_fail_next_op = -1;
     if (pquic_fec_batch_generate(g_batcher, &g_bcnx, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
         free_block(fb);
         g_nt--;

@@ -301,3 +301,41 @@ def test_batch_recover_window_framework_blocks(batch_blocks):
         n += 1
     assert n > 150
     bt.close()
+
+
+@pytest.mark.parametrize("fail_at", [0, 1, 2, 5, 7])
+def test_batch_generate_allocation_failure_matches_sync(fail_at):
+    """An allocator failure during generate (the fail_at-th allocation of the operation; a repair
+    takes two, struct then data) ends a batched block exactly as the synchronous operation ends
+    it: same return value (PICOQUIC_ERROR_MEMORY), the same repairs attached with the same bytes
+    and FPIDs, and nothing leaked (rlc_fec_scheme_generate_gf256.c:50-70 allocates per repair)."""
+    rng = np.random.default_rng(11 + fail_at)
+    k, r, fbn = 16, 4, 321
+    srcs = [rng.integers(0, 256, 1200, dtype=np.uint8) for _ in range(k)]
+    buf = np.stack(srcs)
+    lens = np.full(k, 1200, np.uint16)
+    bt = Batch(1)
+    bt.L.mh_fail_next_generate.argtypes = [C.c_long]
+    bt.L.mh_fail_alloc_after.argtypes = [C.c_long]
+    # synchronous protocol operation with the failure injected
+    rep = np.zeros((r, 1200), np.uint8)
+    rl = np.zeros(r, np.uint16)
+    fp = np.zeros(r, np.uint64)
+    sch = np.zeros(2, np.uint64)
+    bt.L.mh_generate.restype = C.c_long
+    bt.L.mh_fail_next_generate(fail_at)
+    ret_sync = bt.L.mh_generate(0, fbn, k, r, _p(buf), _p(lens, C.c_uint16), 1200, _p(rep), _p(rl, C.c_uint16),
+                                _p(fp, C.c_uint64), 1200, _p(sch, C.c_uint64))
+    # the batched block with the same failure
+    bt.L.mh_fail_next_generate(fail_at)
+    t = bt.generate(False, fbn, srcs, r)
+    bt.L.mh_batch_drain()
+    bt.L.mh_fail_alloc_after(-1)
+    ret_b, calls = bt.status(t)
+    assert ret_sync == 0x405 and (ret_b, calls) == (ret_sync, 1)
+    reps_b, fps_b = bt.repairs(t)
+    n = fail_at // 2  # repairs fully allocated before the failure
+    assert [len(x) for x in reps_b] == [1200] * n + [0] * (r - n) == [int(x) for x in rl]
+    assert fps_b == [int(x) for x in fp]
+    assert all(a.tobytes() == rep[i].tobytes() for i, a in enumerate(reps_b[:n]))
+    bt.close()
