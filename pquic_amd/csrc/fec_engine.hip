@@ -1623,7 +1623,10 @@ __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa,
 // coefficient rows and ring; they read the same source rows close together in time (L2 serves the
 // repeats).  W = 1 unless a tile knob asks for more.
 template <int RT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? 3 : 1)))
+#ifndef FEC_BS2_RT16_WAVES
+#define FEC_BS2_RT16_WAVES 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? FEC_BS2_RT16_WAVES : 1)))
 void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
@@ -1810,7 +1813,9 @@ static inline int bs2_group(int RT, int k, int per_j, int per_block, bool enc, i
 // RT = 8: 4, RT = 16: 2 waves per SIMD).
 // resident waves per CU the LDS budget is sized for (RT = 16 reaches 3 per SIMD only with the
 // two-temporary register map of a FEC_GEN2_BASE=8 build)
-static inline int bs2_waves_per_cu(int RT) { return RT <= 4 ? 20 : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 12 : 8; }
+static inline int bs2_waves_per_cu(int RT) {
+  return RT <= 4 ? 20 : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 4 * FEC_BS2_RT16_WAVES : 8;
+}
 
 template <int RT>
 static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,

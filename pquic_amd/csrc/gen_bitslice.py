@@ -739,6 +739,11 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     PL, TLm, THm, TMPm = R["pl"], R["tl"], R["th"], R["tmp"]
     XT = [TLm[3], TLm[5], TLm[6], TLm[7]]  # dead until the combos: the forward transpose's temporaries
     acc_base = R["acc"]
+    # FEC_GEN2_PROBE_ALIAS=1 (timing probe only, results are garbage): 16-repair encode tiles keep
+    # only 8 repairs' accumulators (repairs 8-15 alias 0-7), so the same instruction stream runs at
+    # 4 waves/SIMD -- the occupancy a 16-repair tile split over two waves would have
+    alias = mode == "enc" and RT == 16 and bool(os.environ.get("FEC_GEN2_PROBE_ALIAS"))
+    NACC = 8 if alias else RT
     assert acc_base + 8 * RT <= 256 and acc_base % 2 == 0
     assert D >= 3 and NDMA * (D - 2) + 2 * RT <= 63, "vmcnt is 6 bits"
     assert (D - 1) * S2_SLOT < 65536, "ds_read offsets are 16 bits"
@@ -763,7 +768,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     a(".Lwtabpc_%=:")
     a(f"s_add_u32 s{S_WTAB}, s{S_WTAB}, .Lwtab_%= - .Lwtabpc_%=")
     a(f"s_addc_u32 s{S_WTAB + 1}, s{S_WTAB + 1}, 0")
-    for r in range(acc_base, acc_base + 8 * RT):
+    for r in range(acc_base, acc_base + 8 * NACC):
         a(f"v_mov_b32 v{r}, 0")
     a(f"s_mov_b32 s{S_COPTR}, %[coef]")
     if AB:  # QA / QB hold one dword of fields each
@@ -915,7 +920,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                 a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[2 * (ch % 2)]}:{S_C[2 * (ch % 2)] + 1}]")
                 a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
                 if ch % 2 == 0:
-                    a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                    a(f"s_set_gpr_idx_on {acc_base + 32 * (ch % 2 if alias else ch)}, gpr_idx(SRC0,DST)")
                 a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
         elif const2:
             # FEC_GEN2_PROBE_CONST=1 (timing probe only, results are garbage): the fields are SGPR
@@ -941,7 +946,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                     L.extend(fld_read(ch + 1))
                 a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_C[0]}, s{S_TABHI}")
                 a(f"s_lshr_b64 s[{S_C[0]}:{S_C[1]}], s[{S_C[0]}:{S_C[1]}], 16")
-                a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_set_gpr_idx_on {acc_base + 32 * (ch % 2 if alias else ch)}, gpr_idx(SRC0,DST)")
                 a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
             a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
         else:
@@ -958,7 +963,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
                     a(f"ds_read_b64 v[{T0}:{T1}], v{T1} offset:{8 * (ch + 1)}")
                 a(f"s_mov_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_C[0]}:{S_C[1]}]")
                 a(f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}")
-                a(f"s_set_gpr_idx_on {acc_base + 32 * ch}, gpr_idx(SRC0,DST)")
+                a(f"s_set_gpr_idx_on {acc_base + 32 * (ch % 2 if alias else ch)}, gpr_idx(SRC0,DST)")
                 a(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
             a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
         a("s_set_gpr_idx_off")
@@ -994,7 +999,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a("s_waitcnt lgkmcnt(0)")
         a(f"v_readfirstlane_b32 s{S_RT}, v{E[0]}")
     for i in range(RT):
-        accs = [acc_base + 8 * i + w for w in range(8)]
+        accs = [acc_base + 8 * (i % NACC) + w for w in range(8)]
         a(f"s_cmp_le_u32 s{S_RT}, {i}")
         a(f"s_cbranch_scc1 .Lepi_done_%=")
         if T64:
@@ -1027,7 +1032,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     a(".Lepi_done_%=:")
     a(f"s_mov_b32 s{S_PRT}, s{S_RT}")
     a(f"s_mov_b32 s{S_PEND}, {D - 1}")
-    for r in range(acc_base, acc_base + 8 * RT):
+    for r in range(acc_base, acc_base + 8 * NACC):
         a(f"v_mov_b32 v{r}, 0")
     if mode == "enc":
         a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rslo]")
@@ -1039,7 +1044,7 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     a("s_waitcnt lgkmcnt(0)")
     a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
     a(f"s_mov_b32 m0, s{S_SAVEM0}")
-    return L, acc_base + 8 * RT
+    return L, acc_base + 8 * NACC
 
 
 def emit_function2(mode, RT, D, NDMA):
@@ -1248,6 +1253,7 @@ def main():
             parts.append(fn)
             parts.append("")
     parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
+    parts.append(f"#define FEC_BS2_RT16_WAVES {4 if os.environ.get('FEC_GEN2_PROBE_ALIAS') else 3}  // 16-repair ring encode waves/SIMD")
     parts.append(f"#define FEC_BS2_SLOT {S2_SLOT}  // ring slot bytes (the bodies address slots by immediates)")
     for mode in ("enc", "dec"):
         for RT in (1, 2, 4, 8, 16):
