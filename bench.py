@@ -603,7 +603,29 @@ def main():
                                      "payload_GiB_s": round(nb2 * k2 * L / (ms * 1e-3) / 2**30, 2),
                                      "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                                      "traffic": load_traffic("rlc_encode_k32_r8", nb2)}
-        del s2, r2t
+        # §8f row 3, the window framework every shipped RLC manifest uses: window blocks carry block
+        # number 0, so all windows share their coefficients and k_rlc_encode_sc codes 2 KiB chunks
+        # of the windows x bytes space per case.  Adjacent windows of 32 (the same bytes as the
+        # k32 r8 block leg) and windows of 32 advancing by 8 (each source in 4 windows).
+        sym = s2.view(-1, L)
+        for wname, wstep in (("adjacent", 32), ("step8", 8)):
+            nw = nb2
+            for _ in range(2):
+                eng.rlc_window_encode(sym, r2t, nw, wstep, k2, r2, L)
+            a.record(stream)
+            for _ in range(5):
+                eng.rlc_window_encode(sym, r2t, nw, wstep, k2, r2, L)
+            b_.record(stream)
+            torch.cuda.synchronize()
+            wms = a.elapsed_time(b_) / 5
+            # bytes a pass must move at least: every source row once, every repair once
+            min_bytes = ((nw - 1) * wstep + k2 + nw * r2) * L
+            wgbs = min_bytes / (wms * 1e-3) / 1e9
+            legs[f"rlc_window_encode_k32_r8_{wname}"] = {
+                "kernel": "k_rlc_encode_sc<8>", "ms": round(wms, 3), "windows": nw, "step": wstep,
+                "window_payload_GiB_s": round(nw * k2 * L / (wms * 1e-3) / 2**30, 2),
+                "min_bytes_GB_s": round(wgbs, 1), "hbm_frac": round(wgbs / HBM_PEAK_GBS, 4)}
+        del s2, r2t, sym
         torch.cuda.empty_cache()
         # configs[4]: jumbo 9000-B symbols, k = 64 r = 16, encode + decode of 16 erasures
         legs["rlc_k64_r16_L9000"] = rlc_leg(torch, eng, dev, 64, 16, 9000, 1 << 16, 16)

@@ -48,9 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ,
-              K_RING, K_N };
+              K_RING, K_WINDOW_SC, K_N };
 static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
-                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring"};
+                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring",
+                                           "window_sc"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -75,6 +76,8 @@ static void knobs_from_env() {
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
   // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair tiles
   g_knob[K_RING] = num(getenv("FECGPU_RING"), 2);
+  // window encode on the shared-coefficient kernel (k_rlc_encode_sc) where it applies
+  g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1) != 0;
 }
 
 static inline int knob(KnobId id) {
@@ -1538,6 +1541,96 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// Shared-coefficient encode (window blocks).  The window framework numbers every block it encodes
+// 0 (malloc_fec_block(cnx, 0), window_framework_sender.h:218), so every window's coefficient rows
+// are seeded by the repair index alone (rlc_fec_scheme_generate_gf256.c:9-17, 57-61) and are the
+// same for all windows.  The windows x bytes space is therefore flattened and cut into 2 KiB
+// chunks, one per wave step: lane l owns the 16-B pieces at chunk offsets 16 l and 1024 + 16 l,
+// which may lie in two different windows (their sources sit step * L apart, their repairs r * L
+// apart, hence separate load and store offsets).  One case per coefficient then covers all 64
+// lanes, where a block-at-a-time wave covers ceil(L / 32) of them (38 at L = 1200).
+// ---------------------------------------------------------------------------------------------
+#define BS_CALL_ENCSC(RT)                                                                          \
+  bs_encsc_r##RT##_v16(sp, rpp, (uint32_t)L, 0u, 0u, (uint64_t)L, (uint64_t)L, (uint32_t)k, (uint32_t)k,  \
+                       (uint32_t)rt, lds_addr(lds), off[0], off[1], so[0], so[1], vm[0], vm[1])
+template <int RT>
+__global__ __launch_bounds__(64) void k_rlc_encode_sc(const uint8_t *__restrict__ sym, uint8_t *__restrict__ rep,
+                                                      uint64_t nwin, int k, int r, int L, uint64_t step_bytes,
+                                                      int r0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
+  const int lane = threadIdx.x;
+  const int rt = r - r0 < RT ? r - r0 : RT;
+  if (lane < RT) {  // coefficient rows of repairs r0 .. r0 + rt - 1, seed (0 << 8) | i
+    uint16_t *row0 = reinterpret_cast<uint16_t *>(lds);
+    uint16_t *row = row0 + FEC_BS_FIELD_SLOT(RT, lane);
+    if (lane < rt) {
+      Tmt t;
+      tmt_init(t, rlc_seed(0u, (uint32_t)(r0 + lane)));
+      for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD(tmt_coef(t), lane);
+    } else {
+      for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;
+    }
+    if constexpr (RT < 4) {
+      if (lane == 0)
+        for (int j = 0; j < k; j++)
+          for (int x = RT; x < 4; x++) row0[j * (CSB / 2) + FEC_BS_FIELD_SLOT(RT, x)] = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t F = nwin * (uint64_t)L;
+  const uint64_t nch = (F + 2047) / 2048;
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t F0 = c * 2048, w0 = F0 / (uint64_t)L;
+    uint32_t off[2], so[2];
+    uint64_t vm[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint64_t p = F0 + 16u * (uint32_t)(lane + 64 * q);
+      const bool ok = p < F;
+      const uint64_t w = p / (uint64_t)L;
+      const uint32_t t = (uint32_t)(p - w * (uint64_t)L);
+      off[q] = ok ? (uint32_t)((w - w0) * step_bytes + t) : 0u;  // a piece past the end reads row 0
+      so[q] = ok ? (uint32_t)((w - w0) * (uint64_t)r * (uint64_t)L + t) : 0u;
+      vm[q] = __ballot(ok);
+    }
+    const uint64_t sp = (uint64_t)(uintptr_t)(sym + w0 * step_bytes);
+    const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (w0 * (uint64_t)r + (uint64_t)r0) * (uint64_t)L);
+    if constexpr (RT == 1) BS_CALL_ENCSC(1);
+    else if constexpr (RT == 2) BS_CALL_ENCSC(2);
+    else if constexpr (RT == 4) BS_CALL_ENCSC(4);
+    else BS_CALL_ENCSC(8);
+  }
+}
+
+// The shared-coefficient path takes 16-B pieces (L % 16 == 0, 16-B aligned rows) and offsets that
+// fit 32 bits; returns false (the block-at-a-time path then runs) otherwise.
+static bool launch_encode_sc(const uint8_t *sym, uint8_t *rep, uint64_t nwin, int k, int r, int L,
+                             uint64_t step_bytes, hipStream_t s) {
+  if (!knob(K_WINDOW_SC) || L % 16 || ((uintptr_t)sym | (uintptr_t)rep) % 16) return false;
+  const uint64_t span = (2048u / (uint32_t)L + 2u) * (step_bytes > (uint64_t)r * L ? step_bytes : (uint64_t)r * L);
+  if (span + (uint64_t)L >= (1ull << 31)) return false;
+  const uint64_t nch = (nwin * (uint64_t)L + 2047) / 2048;
+  for (int r0 = 0; r0 < r; r0 += 8) {
+    const int rt = r - r0 < 8 ? r - r0 : 8;
+    const size_t lds = (size_t)k * FEC_BS_COEF_ROW_BYTES(8);
+    if (rt >= 5)
+      hipLaunchKernelGGL((k_rlc_encode_sc<8>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
+                         step_bytes, r0);
+    else if (rt >= 3)
+      hipLaunchKernelGGL((k_rlc_encode_sc<4>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
+                         step_bytes, r0);
+    else if (rt == 2)
+      hipLaunchKernelGGL((k_rlc_encode_sc<2>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
+                         step_bytes, r0);
+    else
+      hipLaunchKernelGGL((k_rlc_encode_sc<1>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
+                         step_bytes, r0);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // LDS-ring data path (bs2_* bodies, gen_bitslice.py body2): the sources of a group stream into a
 // per-wave LDS ring by LDS-DMA, D-1 rows ahead (up to 1 KiB per wave-instruction, linear in memory
 // and in LDS); each step reads its 32 B per lane from the ring into the plane registers.  The rows
@@ -2334,9 +2427,13 @@ int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t st
   if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const int rt = pick_rt(r);
-  for (int r0 = 0; r0 < (int)r; r0 += rt) {
-    FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)symbols, (uint8_t *)rep, nwindows, (int)k, (int)r,
-                    (int)symbol_size, cfg, 0u, nullptr, r0, 1, (uint64_t)step * symbol_size, 0u, (hipStream_t)stream)
+  if (!launch_encode_sc((const uint8_t *)symbols, (uint8_t *)rep, nwindows, (int)k, (int)r, (int)symbol_size,
+                        (uint64_t)step * symbol_size, (hipStream_t)stream)) {
+    for (int r0 = 0; r0 < (int)r; r0 += rt) {
+      FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)symbols, (uint8_t *)rep, nwindows, (int)k, (int)r,
+                      (int)symbol_size, cfg, 0u, nullptr, r0, 1, (uint64_t)step * symbol_size, 0u,
+                      (hipStream_t)stream)
+    }
   }
   HIPCHK(hipGetLastError());
   g_stats[0]++;

@@ -404,7 +404,7 @@ def regrange(base, n):
     return f"v{base}" if n == 1 else f"v[{base}:{base + n - 1}]"
 
 
-def body(mode: str, RT: int, VEC: int, P: int):
+def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     """Inline-asm text for one group of blocks x one column chunk.
 
     The sources of all blocks of the group form ONE stream (flattened index s = g*k + j),
@@ -636,7 +636,7 @@ def body(mode: str, RT: int, VEC: int, P: int):
             a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{TMP[3]}")
         for q in range(NP):
             a(f"s_mov_b64 exec, %[vm{q}]")
-            a(f"{st} %[off{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
+            a(f"{st} %[{'so' if sc else 'off'}{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
         a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
         if mode == "enc":
             a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
@@ -667,11 +667,16 @@ def cstring(lines):
     return "\n".join(out)
 
 
-def emit_function(mode, RT, VEC, P):
-    lines, top = body(mode, RT, VEC, P)
+def emit_function(mode, RT, VEC, P, sc=False):
+    """sc: the shared-coefficient encode (window blocks, fbn 0): separate per-piece store offsets
+    so0.. (a lane's pieces may belong to different windows, whose sources and repairs are laid
+    out with different strides)."""
+    lines, top = body(mode, RT, VEC, P, sc)
     NP = 32 // VEC
-    name = f"bs_{mode}_r{RT}_v{VEC}"
+    name = f"bs_{mode}{'sc' if sc else ''}_r{RT}_v{VEC}"
     offs = ", ".join(f"uint32_t off{q}" for q in range(NP))
+    if sc:
+        offs += ", " + ", ".join(f"uint32_t so{q}" for q in range(NP))
     vms = ", ".join(f"uint64_t vm{q}" for q in range(NP))
     if mode == "enc":
         sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rslo, "
@@ -684,6 +689,8 @@ def emit_function(mode, RT, VEC, P):
         ins = ['[intab] "v"(intab)', '[outtab] "v"(outtab)']
     ins += ['[nsrc] "s"(nsrc)', '[k] "s"(k)', '[coef] "v"(coef)']
     ins += [f'[off{q}] "v"(off{q})' for q in range(NP)]
+    if sc:
+        ins += [f'[so{q}] "v"(so{q})' for q in range(NP)]
     ins += [f'[vm{q}] "s"(vm{q})' for q in range(NP)]
     clob = [f'"v{r}"' for r in range(T_BASE, top)] + [f'"s{r}"' for r in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
     out = [sig + " {", "  asm volatile(", cstring(lines), "      :",
@@ -1252,6 +1259,13 @@ def main():
             tops[(mode, RT, VEC, P)] = top
             parts.append(fn)
             parts.append("")
+    # shared-coefficient encode bodies (window blocks): wide register map, 16-B pieces
+    for RT in (1, 2, 4, 8):
+        P = prefetch_depth("enc", RT, 16)
+        fn, top = emit_function("enc", RT, 16, P, sc=True)
+        tops[("encsc", RT, 16, P)] = top
+        parts.append(fn)
+        parts.append("")
     parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
     parts.append(f"#define FEC_BS2_RT16_WAVES {4 if os.environ.get('FEC_GEN2_PROBE_ALIAS') else 3}  // 16-repair ring encode waves/SIMD")
     parts.append(f"#define FEC_BS2_SLOT {S2_SLOT}  // ring slot bytes (the bodies address slots by immediates)")

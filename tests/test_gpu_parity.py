@@ -402,6 +402,50 @@ def test_window_encode_vs_oracle(eng, oracle, k, r, step, L, nw):
             assert np.array_equal(got[w, i], want[i]), (w, i)
 
 
+@pytest.mark.parametrize("k,r,step,L,nw", [(30, 4, 10, 1200, 57), (30, 8, 1, 1200, 41), (32, 8, 32, 1200, 64),
+                                           (5, 1, 2, 16, 900), (7, 2, 3, 48, 300), (12, 3, 15, 2048, 9),
+                                           (9, 6, 4, 2064, 11), (16, 11, 16, 1200, 23), (30, 16, 10, 1200, 19),
+                                           (3, 5, 1, 9008, 5), (1, 1, 1, 1200, 3)])
+def test_window_encode_shared_coefficients_vs_oracle(eng, oracle, k, r, step, L, nw):
+    """The shared-coefficient window kernel (k_rlc_encode_sc: every window's coefficients are
+    seeded by the repair index, so 2 KiB chunks of the flattened windows x bytes space share one
+    case per coefficient; a lane's two 16-B pieces may sit in different windows).  Shapes cover
+    one-piece symbols, windows smaller and larger than a chunk, partial last chunks, overlapping,
+    adjacent and gapped windows, r split into tiles of 8 with remainders 1..7."""
+    assert L % 16 == 0
+    nsym = (nw - 1) * step + k
+    sym_h = synth_bytes(nsym * L, 777 + k + r + step).reshape(nsym, L)
+    rep = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_window_encode(to_dev(sym_h), rep, nw, step, k, r, L)
+    torch.cuda.synchronize()
+    got = rep.cpu().numpy()
+    for w in range(nw):
+        want = oracle.rlc_encode_block(0, list(sym_h[w * step: w * step + k]), r)[1]
+        for i in range(r):
+            assert np.array_equal(got[w, i], want[i]), (w, i)
+
+
+def test_window_encode_shared_coefficients_vs_block_path(eng):
+    """At scale (2^17 windows of k=32, r=8, 1200-B symbols, adjacent and overlapping), the
+    shared-coefficient kernel and the block-at-a-time kernel (knob window_sc=0) agree byte for byte."""
+    for k, r, step, nw in ((32, 8, 32, 1 << 17), (30, 4, 7, 1 << 17)):
+        L = 1200
+        nsym = (nw - 1) * step + k
+        sym = torch.empty((nsym, L), dtype=torch.uint8, device=DEV)
+        eng.synth_fill(sym, sym.numel(), 31 + step, 0)
+        a = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
+        b = torch.empty_like(a)
+        eng.rlc_window_encode(sym, a, nw, step, k, r, L)
+        old = eng.get_knob("window_sc")
+        try:
+            eng.set_knob("window_sc", 0)
+            eng.rlc_window_encode(sym, b, nw, step, k, r, L)
+        finally:
+            eng.set_knob("window_sc", old)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (k, r, step)
+
+
 def test_window_decode_vs_oracle(eng, oracle):
     """Window receiver (window_framework_receiver.h): each window's received symbols gathered
     into a block with fec_block_number 0 and decoded; the engine's per-block block-number array
