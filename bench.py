@@ -604,9 +604,10 @@ def main():
                                      "algorithmic_GB_s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                                      "traffic": load_traffic("rlc_encode_k32_r8", nb2)}
         # §8f row 3, the window framework every shipped RLC manifest uses: window blocks carry block
-        # number 0, so all windows share their coefficients and k_rlc_encode_sc codes 2 KiB chunks
-        # of the windows x bytes space per case.  Adjacent windows of 32 (the same bytes as the
-        # k32 r8 block leg) and windows of 32 advancing by 8 (each source in 4 windows).
+        # number 0, so all windows share their coefficients; overlapping windows run on
+        # k_rlc_encode_sc (2 KiB chunks of the windows x bytes space per case), windows that do not
+        # overlap on the block kernel.  Windows of 32 advancing by 8 (each source in 4 windows) and
+        # adjacent windows (the same bytes as the k32 r8 block leg).
         sym = s2.view(-1, L)
         for wname, wstep in (("adjacent", 32), ("step8", 8)):
             nw = nb2
@@ -622,7 +623,8 @@ def main():
             min_bytes = ((nw - 1) * wstep + k2 + nw * r2) * L
             wgbs = min_bytes / (wms * 1e-3) / 1e9
             legs[f"rlc_window_encode_k32_r8_{wname}"] = {
-                "kernel": "k_rlc_encode_sc<8>", "ms": round(wms, 3), "windows": nw, "step": wstep,
+                "kernel": "k_rlc_encode_sc<8>" if wstep < k2 else "k_rlc_encode_bs<8,16>", "ms": round(wms, 3),
+                "windows": nw, "step": wstep,
                 "window_payload_GiB_s": round(nw * k2 * L / (wms * 1e-3) / 2**30, 2),
                 "min_bytes_GB_s": round(wgbs, 1), "hbm_frac": round(wgbs / HBM_PEAK_GBS, 4)}
         del s2, r2t, sym

@@ -191,8 +191,8 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
  * "plan" (0 auto, 1 wave, 2 lane, 3 reg, 4 tile), "interleave" (0/1), "group" (0 = defaults, else
  * a cap on blocks per group), "enc_tile_rt" / "enc_tile_waves" (0 = default tiling), "xor_generic",
  * "xor_idx64", "zc_read" (0/1), "ring" (the LDS-ring data path: 0 never, 1 wherever it applies,
- * 2 = default, 16-repair encode and 16-unknown decode tiles), "window_sc" (1 = default: window
- * encode on the shared-coefficient kernel where it applies).  Returns FECGPU_OK or
+ * 2 = default, 16-repair encode and 16-unknown decode tiles), "window_sc" (window encode on the
+ * shared-coefficient kernel: 0 never, 1 = default for overlapping windows, 2 wherever it applies).  Returns FECGPU_OK or
  * FECGPU_ERR_INVALID for an unknown name. */
 int fecgpu_set_knob(const char *name, int value);
 int fecgpu_get_knob(const char *name, int *value);

@@ -76,8 +76,9 @@ static void knobs_from_env() {
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
   // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair tiles
   g_knob[K_RING] = num(getenv("FECGPU_RING"), 2);
-  // window encode on the shared-coefficient kernel (k_rlc_encode_sc) where it applies
-  g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1) != 0;
+  // window encode on the shared-coefficient kernel (k_rlc_encode_sc): 0 never, 1 (default) for
+  // overlapping windows, 2 wherever it applies (tests)
+  g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1);
 }
 
 static inline int knob(KnobId id) {
@@ -1603,11 +1604,17 @@ __global__ __launch_bounds__(64) void k_rlc_encode_sc(const uint8_t *__restrict_
   }
 }
 
-// The shared-coefficient path takes 16-B pieces (L % 16 == 0, 16-B aligned rows) and offsets that
-// fit 32 bits; returns false (the block-at-a-time path then runs) otherwise.
+// The shared-coefficient path runs for overlapping windows (step < k): there a source row serves
+// k / step windows, which neighbouring chunks code close together in time, and the 2 KiB cases
+// pay off (2^21 windows of k30 r4 step 10: 14.25 -> 11.62 ms; k32 r8 step 8: 18.75 -> 13.87 ms;
+// k30 r4 step 1: 14.17 -> 8.21 ms).  Windows that do not overlap are independent blocks, and the
+// block kernel's interleaved groups stream them better (k32 r8 step 32: 18.96 vs 20.37 ms;
+// profiles/r02_ab_window_sc.log).  It takes 16-B pieces (L % 16 == 0, 16-B aligned rows) and
+// offsets that fit 32 bits; returns false (the block-at-a-time path then runs) otherwise.
 static bool launch_encode_sc(const uint8_t *sym, uint8_t *rep, uint64_t nwin, int k, int r, int L,
                              uint64_t step_bytes, hipStream_t s) {
   if (!knob(K_WINDOW_SC) || L % 16 || ((uintptr_t)sym | (uintptr_t)rep) % 16) return false;
+  if (step_bytes >= (uint64_t)k * (uint64_t)L && knob(K_WINDOW_SC) != 2) return false;  // 2: force (tests)
   const uint64_t span = (2048u / (uint32_t)L + 2u) * (step_bytes > (uint64_t)r * L ? step_bytes : (uint64_t)r * L);
   if (span + (uint64_t)L >= (1ull << 31)) return false;
   const uint64_t nch = (nwin * (uint64_t)L + 2047) / 2048;

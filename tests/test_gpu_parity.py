@@ -416,7 +416,12 @@ def test_window_encode_shared_coefficients_vs_oracle(eng, oracle, k, r, step, L,
     nsym = (nw - 1) * step + k
     sym_h = synth_bytes(nsym * L, 777 + k + r + step).reshape(nsym, L)
     rep = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
-    eng.rlc_window_encode(to_dev(sym_h), rep, nw, step, k, r, L)
+    old = eng.get_knob("window_sc")
+    try:
+        eng.set_knob("window_sc", 2)  # also for windows that do not overlap
+        eng.rlc_window_encode(to_dev(sym_h), rep, nw, step, k, r, L)
+    finally:
+        eng.set_knob("window_sc", old)
     torch.cuda.synchronize()
     got = rep.cpu().numpy()
     for w in range(nw):
@@ -435,9 +440,10 @@ def test_window_encode_shared_coefficients_vs_block_path(eng):
         eng.synth_fill(sym, sym.numel(), 31 + step, 0)
         a = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
         b = torch.empty_like(a)
-        eng.rlc_window_encode(sym, a, nw, step, k, r, L)
         old = eng.get_knob("window_sc")
         try:
+            eng.set_knob("window_sc", 2)
+            eng.rlc_window_encode(sym, a, nw, step, k, r, L)
             eng.set_knob("window_sc", 0)
             eng.rlc_window_encode(sym, b, nw, step, k, r, L)
         finally:

@@ -96,6 +96,14 @@ for spec in (a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")):  
 if "--only" in sys.argv:
     CASES = CASES[3:]
 for (k, r, nb, mode, L) in CASES:
+    if mode.startswith("win"):  # window encode, mode "win<step>": nb windows over one symbol stream
+        step = int(mode[3:])
+        sym = torch.empty((((nb - 1) * step + k), L), dtype=torch.uint8, device=dev)
+        eng.synth_fill(sym, sym.numel(), 3, 0)
+        wrep = torch.empty((nb, r, L), dtype=torch.uint8, device=dev)
+        cases.append((f"win s{step} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L,
+                      (sym, wrep, None, None, None, None, None)))
+        continue
     bufs = setup(k, r, nb, min(k, r), L)
     cases.append((f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L, bufs))
 
@@ -104,6 +112,8 @@ def run(case, eng):
     _, k, r, nb, mode, L, (src, rep, sp, rp, st, rec, ws) = case
     if mode == "enc":
         eng.rlc_encode(src, rep, k, r, L)
+    elif mode.startswith("win"):
+        eng.rlc_window_encode(src, rep, nb, int(mode[3:]), k, r, L)
     elif mode == "xenc":
         eng.xor_encode(src, rep, k, L)
     elif mode == "xdec":
@@ -129,7 +139,7 @@ for cyc in range(cycles):
             e.set_knob(kn, want.get(kn, defaults[(name, kn)]))
         for c in cases:
             run(c, e)  # warm
-            if c[4] == "enc":  # every variant must produce the same repair bytes
+            if c[4] == "enc" or c[4].startswith("win"):  # every variant must produce the same repair bytes
                 rep = c[6][1]
                 sub = rep[::61].contiguous().view(torch.int32).view(-1).to(torch.int64)
                 h = (sub * (torch.arange(sub.numel(), device=dev) % 65521 + 1)).sum().item()
