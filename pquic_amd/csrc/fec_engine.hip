@@ -48,10 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ,
-              K_RING, K_WINDOW_SC, K_N };
+              K_RING, K_WINDOW_SC, K_SMALL_PLAN, K_N };
 static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
                                            "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring",
-                                           "window_sc"};
+                                           "window_sc", "small_plan"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -79,6 +79,9 @@ static void knobs_from_env() {
   // window encode on the shared-coefficient kernel (k_rlc_encode_sc): 0 never, 1 (default) for
   // overlapping windows, 2 wherever it applies (tests)
   g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1);
+  // one-launch decode of a few blocks: 0 (default) the wave plan, 1 the lane-register plan when k <= 32
+  // and e <= 8 (one-block recover hook p50 53 us against 37: its single lane's dependent chain is long)
+  g_knob[K_SMALL_PLAN] = num(getenv("FECGPU_SMALL_PLAN"), 0);
 }
 
 static inline int knob(KnobId id) {
@@ -678,6 +681,153 @@ __device__ __forceinline__ uint64_t gf_mulc_row(uint64_t x, const PermTab &t) {
 
 __device__ __forceinline__ uint32_t col8(uint64_t row, int i) { return (uint32_t)(row >> (8 * i)) & 0xffu; }
 
+// One block's register plan (the lane that calls it holds the whole system); the record goes to h
+// in the workspace layout.  EXP / LOG: the log/exp tables (LDS).
+template <int KD, int EM>
+__device__ __forceinline__ void plan_reg_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
+                                               const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp,
+                                               uint8_t *h, const uint8_t *EXP, const uint8_t *LOG) {
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int em = (int)L.em;
+  const uint64_t kmask = k < 64 ? (1ull << k) - 1 : ~0ull;
+  const uint64_t s0 = sp[2 * b] & kmask;  // k <= 32: the high word never matters
+  uint64_t q0 = rp[2 * b], q1 = rp[2 * b + 1];
+  clip128(q0, q1, r);
+  const int cur_ss = __popcll(s0);
+  const int cur_rs = __popcll(q0) + __popcll(q1);
+  if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
+    h[0] = FECGPU_BLOCK_NOTHING;
+    h[1] = 0;
+    return;
+  }
+  const int n = k - cur_ss;  // <= em <= EM
+  const uint64_t miss = ~s0 & kmask;
+  uint64_t U = 0, S = 0;  // unknown source ids / selected repair ids, one byte each
+  {
+    int u = 0;
+    for (int j = 0; j < k; j++)
+      if ((miss >> j) & 1) U |= (uint64_t)j << (8 * u++);
+    int e = 0;
+    for (int i = 0; i < r && e < n; i++)
+      if (bit128(q0, q1, i)) S |= (uint64_t)i << (8 * e++);
+  }
+  uint64_t A[EM];
+  uint32_t V[EM][KD];
+#pragma unroll
+  for (int e = 0; e < EM; e++) {
+    A[e] = 0;
+#pragma unroll
+    for (int d = 0; d < KD; d++) V[e][d] = 0;
+  }
+  const uint32_t f = block_fbn(b, fbn_base, fbn);
+#pragma unroll
+  for (int e = 0; e < EM; e++) {  // system rows, :194-212
+    if (e < n) {
+      Tmt t;
+      tmt_init(t, repair_seed(seeds, b, r, f, col8(S, e)));
+      int u = 0;
+#pragma unroll
+      for (int j = 0; j < 4 * KD; j++) {
+        if (j < k) {
+          const uint32_t c = tmt_coef(t);
+          const bool ms = (miss >> j) & 1;
+          V[e][j >> 2] |= (ms ? (uint32_t)(u == e) : c) << (8 * (j & 3));
+          if (ms) A[e] |= (uint64_t)c << (8 * u++);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < EM; i++) {  // sort_system :28-40 (first maximum wins; rows swapped in place)
+    if (i < n) {
+      int mx = i;
+      uint32_t best = col8(A[i], i);
+#pragma unroll
+      for (int j = i + 1; j < EM; j++)
+        if (j < n && best < col8(A[j], i)) { best = col8(A[j], i); mx = j; }
+#pragma unroll
+      for (int j = i + 1; j < EM; j++) {
+        if (j == mx) {
+          const uint64_t ta = A[i]; A[i] = A[j]; A[j] = ta;
+#pragma unroll
+          for (int d = 0; d < KD; d++) { const uint32_t tv = V[i][d]; V[i][d] = V[j][d]; V[j][d] = tv; }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < EM - 1; i++) {  // elimination without re-pivoting :54-70
+    const uint32_t piv = col8(A[i], i);
+    if (i < n - 1 && piv) {
+      const uint32_t lip = 255u - LOG[piv];
+#pragma unroll
+      for (int kk = i + 1; kk < EM; kk++) {
+        const uint32_t a = col8(A[kk], i);
+        if (kk < n && a) {
+          const PermTab T = perm_table(EXP[LOG[a] + lip]);  // a / piv
+          A[kk] ^= gf_mulc_row<EM>(A[i], T);
+#pragma unroll
+          for (int d = 0; d < KD; d++)
+            if (4 * d < k) V[kk][d] ^= gf_mulc(V[i][d], T);
+        }
+      }
+    }
+  }
+  bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
+#pragma unroll
+  for (int i = 0; i < EM; i++) ub |= i < n && col8(A[i], i) == 0;
+  if (ub) {
+    h[0] = FECGPU_BLOCK_REF_UB;
+    h[1] = 0;
+    return;
+  }
+#pragma unroll
+  for (int i = EM - 1; i >= 0; i--) {  // back substitution :71-114; X_i replaces row i
+    if (i < n) {
+#pragma unroll
+      for (int u = i + 1; u < EM; u++) {
+        const uint32_t a = col8(A[i], u);
+        if (u < n && a) {
+          const PermTab T = perm_table(a);
+#pragma unroll
+          for (int d = 0; d < KD; d++)
+            if (4 * d < k) V[i][d] ^= gf_mulc(V[u][d], T);
+        }
+      }
+      const PermTab T = perm_table(EXP[255u - LOG[col8(A[i], i)]]);  // 1 / diagonal
+#pragma unroll
+      for (int d = 0; d < KD; d++)
+        if (4 * d < k) V[i][d] = gf_mulc(V[i][d], T);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < EM; i++) {
+    if (i < n) {
+      uint8_t *D = h + L.off_D + i * k;
+      if ((k & 3) == 0) {  // D + 4d is 4-byte aligned: the packed V row as dwords
+#pragma unroll
+        for (int d = 0; d < KD; d++)
+          if (4 * d < k) reinterpret_cast<uint32_t *>(D)[d] = V[i][d];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4 * KD; j++)
+          if (j < k) D[j] = (uint8_t)(V[i][j >> 2] >> (8 * (j & 3)));
+      }
+      for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && col8(A[i], u) != 0;
+      h[L.off_nz + i] = 0;
+      h[L.off_unk + i] = (uint8_t)col8(U, i);
+      h[L.off_sel + i] = (uint8_t)col8(S, i);
+    }
+  }
+  {
+    int u = 0;
+    for (int j = 0; j < k; j++)
+      h[L.off_slot + j] = ((miss >> j) & 1) ? (uint8_t)(0x80 | col8(S, u++)) : (uint8_t)j;
+  }
+  h[0] = FECGPU_BLOCK_RECOVERED;
+  h[1] = (uint8_t)n;
+}
+
 template <int KD, int EM>
 __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, int r, uint32_t fbn_base,
                                                      const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
@@ -685,153 +835,14 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
-  const int em = (int)L.em;
   const uint8_t *EXP = lds, *LOG = lds + 512;
   for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
   __syncthreads();
   const uint32_t orow = plan_out_row(L.stride);
   uint8_t *h = lds + 768 + (size_t)lane * orow;  // this lane's workspace record (LDS copy)
-  const uint64_t kmask = k < 64 ? (1ull << k) - 1 : ~0ull;
   for (uint64_t base = (uint64_t)blockIdx.x * 64; base < nblocks; base += (uint64_t)gridDim.x * 64) {
     const uint64_t b = base + lane;
-    if (b < nblocks) do {
-      const uint64_t s0 = sp[2 * b] & kmask;  // k <= 32: the high word never matters
-      uint64_t q0 = rp[2 * b], q1 = rp[2 * b + 1];
-      clip128(q0, q1, r);
-      const int cur_ss = __popcll(s0);
-      const int cur_rs = __popcll(q0) + __popcll(q1);
-      if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {  // rlc_fec_scheme_gf256.c:140-144
-        h[0] = FECGPU_BLOCK_NOTHING;
-        h[1] = 0;
-        break;
-      }
-      const int n = k - cur_ss;  // <= em <= EM
-      const uint64_t miss = ~s0 & kmask;
-      uint64_t U = 0, S = 0;  // unknown source ids / selected repair ids, one byte each
-      {
-        int u = 0;
-        for (int j = 0; j < k; j++)
-          if ((miss >> j) & 1) U |= (uint64_t)j << (8 * u++);
-        int e = 0;
-        for (int i = 0; i < r && e < n; i++)
-          if (bit128(q0, q1, i)) S |= (uint64_t)i << (8 * e++);
-      }
-      uint64_t A[EM];
-      uint32_t V[EM][KD];
-#pragma unroll
-      for (int e = 0; e < EM; e++) {
-        A[e] = 0;
-#pragma unroll
-        for (int d = 0; d < KD; d++) V[e][d] = 0;
-      }
-      const uint32_t f = block_fbn(b, fbn_base, fbn);
-#pragma unroll
-      for (int e = 0; e < EM; e++) {  // system rows, :194-212
-        if (e < n) {
-          Tmt t;
-          tmt_init(t, repair_seed(seeds, b, r, f, col8(S, e)));
-          int u = 0;
-#pragma unroll
-          for (int j = 0; j < 4 * KD; j++) {
-            if (j < k) {
-              const uint32_t c = tmt_coef(t);
-              const bool ms = (miss >> j) & 1;
-              V[e][j >> 2] |= (ms ? (uint32_t)(u == e) : c) << (8 * (j & 3));
-              if (ms) A[e] |= (uint64_t)c << (8 * u++);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < EM; i++) {  // sort_system :28-40 (first maximum wins; rows swapped in place)
-        if (i < n) {
-          int mx = i;
-          uint32_t best = col8(A[i], i);
-#pragma unroll
-          for (int j = i + 1; j < EM; j++)
-            if (j < n && best < col8(A[j], i)) { best = col8(A[j], i); mx = j; }
-#pragma unroll
-          for (int j = i + 1; j < EM; j++) {
-            if (j == mx) {
-              const uint64_t ta = A[i]; A[i] = A[j]; A[j] = ta;
-#pragma unroll
-              for (int d = 0; d < KD; d++) { const uint32_t tv = V[i][d]; V[i][d] = V[j][d]; V[j][d] = tv; }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < EM - 1; i++) {  // elimination without re-pivoting :54-70
-        const uint32_t piv = col8(A[i], i);
-        if (i < n - 1 && piv) {
-          const uint32_t lip = 255u - LOG[piv];
-#pragma unroll
-          for (int kk = i + 1; kk < EM; kk++) {
-            const uint32_t a = col8(A[kk], i);
-            if (kk < n && a) {
-              const PermTab T = perm_table(EXP[LOG[a] + lip]);  // a / piv
-              A[kk] ^= gf_mulc_row<EM>(A[i], T);
-#pragma unroll
-              for (int d = 0; d < KD; d++)
-                if (4 * d < k) V[kk][d] ^= gf_mulc(V[i][d], T);
-            }
-          }
-        }
-      }
-      bool ub = false;  // candidate walks to -1 iff a diagonal entry is zero (:74-77)
-#pragma unroll
-      for (int i = 0; i < EM; i++) ub |= i < n && col8(A[i], i) == 0;
-      if (ub) {
-        h[0] = FECGPU_BLOCK_REF_UB;
-        h[1] = 0;
-        break;
-      }
-#pragma unroll
-      for (int i = EM - 1; i >= 0; i--) {  // back substitution :71-114; X_i replaces row i
-        if (i < n) {
-#pragma unroll
-          for (int u = i + 1; u < EM; u++) {
-            const uint32_t a = col8(A[i], u);
-            if (u < n && a) {
-              const PermTab T = perm_table(a);
-#pragma unroll
-              for (int d = 0; d < KD; d++)
-                if (4 * d < k) V[i][d] ^= gf_mulc(V[u][d], T);
-            }
-          }
-          const PermTab T = perm_table(EXP[255u - LOG[col8(A[i], i)]]);  // 1 / diagonal
-#pragma unroll
-          for (int d = 0; d < KD; d++)
-            if (4 * d < k) V[i][d] = gf_mulc(V[i][d], T);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < EM; i++) {
-        if (i < n) {
-          uint8_t *D = h + L.off_D + i * k;
-          if ((k & 3) == 0) {  // D + 4d is 4-byte aligned: the packed V row as dwords
-#pragma unroll
-            for (int d = 0; d < KD; d++)
-              if (4 * d < k) reinterpret_cast<uint32_t *>(D)[d] = V[i][d];
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4 * KD; j++)
-              if (j < k) D[j] = (uint8_t)(V[i][j >> 2] >> (8 * (j & 3)));
-          }
-          for (int u = 0; u < n; u++) h[L.off_dep + i * em + u] = (u > i) && col8(A[i], u) != 0;
-          h[L.off_nz + i] = 0;
-          h[L.off_unk + i] = (uint8_t)col8(U, i);
-          h[L.off_sel + i] = (uint8_t)col8(S, i);
-        }
-      }
-      {
-        int u = 0;
-        for (int j = 0; j < k; j++)
-          h[L.off_slot + j] = ((miss >> j) & 1) ? (uint8_t)(0x80 | col8(S, u++)) : (uint8_t)j;
-      }
-      h[0] = FECGPU_BLOCK_RECOVERED;
-      h[1] = (uint8_t)n;
-    } while (0);
+    if (b < nblocks) plan_reg_block<KD, EM>(b, k, r, fbn_base, fbn, seeds, sp, rp, h, EXP, LOG);
     __syncthreads();
     const uint32_t nrows = nblocks - base < 64 ? (uint32_t)(nblocks - base) : 64u;
     copy_records(reinterpret_cast<uint32_t *>(ws + base * (uint64_t)L.stride),
@@ -1423,9 +1434,12 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
         BsLanes<VEC> ln(lane, cb);
 #pragma unroll
         for (int q = 0; q < BsLanes<VEC>::NP; q++) ln.off[q] += (uint32_t)c0;  // chunk offset
+        // nsrc and k go to SGPRs: readfirstlane states their uniformity (a plan inlined into a
+        // one-lane branch before this call can leave the compiler unsure of it)
         if (lane < ln.active)
-          bs_dec_call<RT, VEC>(lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), (uint32_t)k,
-                               lds_addr(S.coef), ln);
+          bs_dec_call<RT, VEC>(lds_addr(S.intab), lds_addr(S.rec),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(nact * k),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(k), lds_addr(S.coef), ln);
       }
     }
     __syncthreads();
@@ -1479,22 +1493,30 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
 
 // Decode of a few blocks in ONE launch (the synchronous hooks decode one block per call): each
 // workgroup plans its block with the wave plan, then runs the single-pass data pass on it.  The
-// plan's workspace record goes through global memory (the fence makes it visible to the loads).
-template <int RT, int VEC>
+// plan's record stays in LDS (past both phases' scratch, at rec_off): both phases address a record
+// as ws + b * stride, so they get a base that puts block b's record there, and no global round trip
+// or fence sits between the plan and the data pass.
+template <int RT, int VEC, bool PLANREG>
 __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                          uint64_t nblocks, int k, int r, int L, int nchunks,
                                                          int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
                                                          const uint32_t *seeds, const uint64_t *sp,
-                                                         const uint64_t *rp, uint8_t *ws, uint8_t *status,
+                                                         const uint64_t *rp, uint32_t rec_off, uint8_t *status,
                                                          uint64_t *recovered, uint8_t *dst) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint64_t stride = ws_layout((uint32_t)k, (uint32_t)r).stride;
   for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    uint8_t *wsx = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(lds + rec_off) - b * stride);
     __syncthreads();
     plan_load_tables(lds);
-    plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
-    __threadfence();
+    if constexpr (PLANREG) {  // k <= 32, e <= 8: lane 0 holds the whole system (k_rlc_plan_reg's replay)
+      __syncthreads();
+      if (threadIdx.x == 0) plan_reg_block<8, 8>(b, k, r, fbn_base, fbn, seeds, sp, rp, lds + rec_off, lds, lds + 512);
+    } else {
+      plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
+    }
     __syncthreads();
-    recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, 0, 1, status,
+    recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, wsx, 0, 1, status,
                               recovered, 0, dst, lds);
   }
 }
@@ -2651,8 +2673,19 @@ static void launch_decode_small(uint8_t *src, const uint8_t *rep, uint64_t nb, i
                                 const uint64_t *rp, uint8_t *ws, uint8_t *status, uint64_t *recovered, uint8_t *dst,
                                 hipStream_t s) {
   const size_t pl = plan_lds_bytes((uint32_t)k, (uint32_t)r), rl = RecoverLds<RT>::bytes(1, k);
-  hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC>), dim3((uint32_t)nb), dim3(64), pl > rl ? pl : rl, s, src, rep,
-                     nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, ws, status, recovered, dst);
+  const uint32_t rec_off = pad16((uint32_t)(pl > rl ? pl : rl));  // the plan record, past both phases' scratch
+  (void)ws;  // the record never leaves the workgroup
+  const size_t lds = rec_off + pad16(ws_layout((uint32_t)k, (uint32_t)r).stride);
+  if constexpr (RT <= 8) {
+    if (k <= 32 && knob(K_SMALL_PLAN) == 1) {  // the lane-register plan: its system fits one lane
+      hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, true>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k,
+                         r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered,
+                         dst);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, false>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k, r,
+                     L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered, dst);
 }
 }  // extern "C++"
 

@@ -212,7 +212,8 @@ def test_decode_vs_oracle(eng, oracle, k, r, L, nb, emax):
 
 
 @pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 1), (16, 4, 1200, 64), (32, 8, 1200, 7), (5, 5, 20, 33),
-                                      (64, 16, 9000, 3), (20, 16, 2052, 9), (3, 1, 4, 2)])
+                                      (64, 16, 9000, 3), (20, 16, 2052, 9), (3, 1, 4, 2), (32, 9, 1200, 5),
+                                      (1, 1, 16, 3), (31, 8, 100, 17)])
 def test_small_batch_decode_one_launch(eng, oracle, k, r, L, nb):
     """Up to 64 blocks decode in one launch (wave plan + data pass per workgroup, as the
     synchronous hooks run); same bytes, statuses and masks as the oracle and as the two-launch
@@ -231,13 +232,17 @@ def test_small_batch_decode_one_launch(eng, oracle, k, r, L, nb):
     work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     with eng.knob("plan", 1):  # the wave plan as its own launch, then the data pass
         _, got2, st2, rec2 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+    with eng.knob("small_plan", 1):  # one launch with the lane-register plan (k <= 32, e <= 8; else the wave plan)
+        _, got3, st3, rec3 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     ref = work.copy()
     st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
     assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)
     assert np.array_equal(st2, st_ref) and np.array_equal(rec2, rec_ref)
+    assert np.array_equal(st3, st_ref) and np.array_equal(rec3, rec_ref)
     for b in range(nb):
         for j in bits(rec[b], k):
             assert np.array_equal(got[b, j], src_h[b, j]) and np.array_equal(got2[b, j], src_h[b, j])
+            assert np.array_equal(got3[b, j], src_h[b, j])
 
 
 def test_decode_zero_symbol_propagation(eng, oracle):
