@@ -192,8 +192,10 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
  * a cap on blocks per group), "enc_tile_rt" / "enc_tile_waves" (0 = default tiling), "xor_generic",
  * "xor_idx64", "zc_read" (0/1), "ring" (the LDS-ring data path: 0 never, 1 wherever it applies,
  * 2 = default, 16-repair encode and 16-unknown decode tiles), "window_sc" (window encode on the
- * shared-coefficient kernel: 0 never, 1 = default for overlapping windows, 2 wherever it applies), "small_plan" (one-launch decode of <= 64 blocks:
- * 0 = default, the wave plan; 1 the lane-register plan when k <= 32 and e <= 8).  Returns FECGPU_OK or
+ * shared-coefficient kernel: 0 never, 1 = default for overlapping windows, 2 wherever it applies),
+ * "small_plan" (one-launch decode of <= 64 blocks: 0 = default, the wave plan; 1 the lane-register
+ * plan when k <= 32 and e <= 8), "min_groups" (batches with fewer block groups than this stream fewer
+ * blocks per wave; default 1024, 0 = the per-shape group sizes at any batch size).  Returns FECGPU_OK or
  * FECGPU_ERR_INVALID for an unknown name. */
 int fecgpu_set_knob(const char *name, int value);
 int fecgpu_get_knob(const char *name, int *value);

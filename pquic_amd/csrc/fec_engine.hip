@@ -48,10 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ,
-              K_RING, K_WINDOW_SC, K_SMALL_PLAN, K_N };
+              K_RING, K_WINDOW_SC, K_SMALL_PLAN, K_MIN_GROUPS, K_N };
 static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
                                            "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring",
-                                           "window_sc", "small_plan"};
+                                           "window_sc", "small_plan", "min_groups"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -82,6 +82,9 @@ static void knobs_from_env() {
   // one-launch decode of a few blocks: 0 (default) the wave plan, 1 the lane-register plan when k <= 32
   // and e <= 8 (one-block recover hook p50 53 us against 37: its single lane's dependent chain is long)
   g_knob[K_SMALL_PLAN] = num(getenv("FECGPU_SMALL_PLAN"), 0);
+  // batches too small to fill the chip stream fewer blocks per wave: groups of blocks shrink until
+  // there are at least this many groups (0: the per-shape group sizes at every batch size)
+  g_knob[K_MIN_GROUPS] = num(getenv("FECGPU_MIN_GROUPS"), 1024);
 }
 
 static inline int knob(KnobId id) {
@@ -1243,7 +1246,12 @@ __device__ __forceinline__ void bs_dec_call(uint32_t ia, uint32_t oa, uint32_t n
 //   -2.3 %, decode -8.3 %: the chunk passes then revisit one block's rows);
 // - everything else: 64 / RT.
 // Knob "group" (FECGPU_GROUP=N) replaces the defaults with a plain cap (A/B experiments).
-static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, bool enc, int nchunks) {
+// - batches of fewer than min_groups (default 1024, one wave per SIMD) groups: halved until there
+//   are that many groups or one block per group.  A group is streamed by one wave, so a batch of 8
+//   k32 r8 blocks took 137 us in one group against 22 us for one block
+//   (profiles/r02_small_kernel_probe.log).
+static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, bool enc, int nchunks,
+                           uint64_t nb) {
   int g = 64 / RT;
   if (const int cap = knob(K_GROUP)) {
     while (g > 1 && g > cap) g >>= 1;
@@ -1253,6 +1261,8 @@ static inline int bs_group(int RT, int k, int per_j_bytes, int per_block_bytes, 
     g = enc ? 2 : 8;
   }
   while (g > 1 && g * (k * per_j_bytes + per_block_bytes) > 32768) g >>= 1;
+  if (const uint64_t ming = (uint64_t)knob(K_MIN_GROUPS))
+    while (g > 1 && (nb + g - 1) / g < ming) g >>= 1;
   return g;
 }
 
@@ -1545,7 +1555,7 @@ template <int RT, int VEC>
 static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                              hipStream_t s) {
-  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks) : 1;
+  const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, nb) : 1;
   const size_t lds = (size_t)W * G * k * FEC_BS_COEF_ROW_BYTES(RT);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
@@ -1556,7 +1566,7 @@ template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                               uint8_t *dst) {
-  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks);
+  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, nb);
   const size_t lds = RecoverLds<RT>::bytes(G, k);
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
@@ -1924,8 +1934,8 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
 // Groups for the ring path: as bs_group, then halved until the workgroup's LDS (coefficient rows or
 // decode staging + the ring) leaves room for `waves` waves per CU (160 KiB of LDS per CU).
 static inline int bs2_group(int RT, int k, int per_j, int per_block, bool enc, int nchunks, size_t ring_bytes,
-                            int waves) {
-  int g = bs_group(RT, k, per_j, per_block, enc, nchunks);
+                            int waves, uint64_t nb) {
+  int g = bs_group(RT, k, per_j, per_block, enc, nchunks, nb);
   const size_t budget = (size_t)160 * 1024 / (size_t)waves;
   while (g > 1 && (size_t)g * (k * per_j + per_block) + 256 + ring_bytes > budget) g >>= 1;
   return g;
@@ -1946,7 +1956,8 @@ static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth<RT>::enc * slotb;
   const int G = sbs == (uint64_t)k * L
-                    ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT))
+                    ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT),
+                                nb)
                     : 1;
   const size_t lds = (size_t)W * (pad16((uint32_t)(G * k * FEC_BS_COEF_ROW_BYTES(RT))) + ring_bytes);
   const uint64_t groups = (nb + G - 1) / G;
@@ -1961,7 +1972,7 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth<RT>::dec * slotb;
   const int G = bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, ring_bytes,
-                          bs2_waves_per_cu(RT));
+                          bs2_waves_per_cu(RT), nb);
   const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + ring_bytes;
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs2<RT>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r, L,
@@ -2503,7 +2514,10 @@ static int decode_args(const void *src, const void *rep, uint64_t nblocks, uint3
   return FECGPU_OK;
 }
 
-constexpr uint64_t kPlanWaveMaxBlocks = 64;  // below this many blocks a wave per block plans fastest
+// Up to this many blocks a wave per block plans fastest: the lane-parallel plans (reg / tile / lane)
+// take one lane's dependent chain whatever the batch, e.g. k32 e8 70 us against the wave plan's 27-38
+// us at 65-4096 blocks; they win from ~4096 blocks on (profiles/r02_plan_crossover.log).
+constexpr uint64_t kPlanWaveMaxBlocks = 2048;
 
 static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
                             const uint32_t *seeds, const uint64_t *src_present, const uint64_t *rep_present,
@@ -2519,9 +2533,9 @@ static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t f
   // compare the plan kernels on the same inputs through fecgpu_set_knob)
   int force = knob(K_PLAN);
   const uint32_t em = ws_layout(k, r).em;
-  // a few blocks (the synchronous hooks run one): every block gets its own wave and the wave plan's
-  // row-parallel elimination, instead of a lane's serial replay -- one-block recover hook
-  // 47 -> 40 us (profiles/r02_hook_plan.log)
+  // up to kPlanWaveMaxBlocks blocks (the synchronous hooks run one): every block gets its own wave
+  // and the wave plan's row-parallel elimination, instead of a lane's serial replay -- one-block
+  // recover hook 47 -> 40 us (profiles/r02_hook_plan.log)
   if (force == 0 && nblocks <= kPlanWaveMaxBlocks && plan_lds_bytes(k, r) <= 65536) force = PLAN_WAVE;
   if ((force == 0 || force == 3) && k <= 32 && em <= 8) {
     const size_t reg_lds = 768 + 64 * (size_t)plan_out_row(ws_layout(k, r).stride);

@@ -611,6 +611,55 @@ def test_plan_kernels_agree(eng, k, r, nb):
     assert DEC_RECOVERED in sts
 
 
+@pytest.mark.parametrize("k,r,nb", [(16, 4, 300), (32, 8, 300), (64, 16, 90), (10, 3, 513), (16, 8, 200)])
+def test_small_batch_group_sizes_agree(eng, k, r, nb):
+    """Batches below min_groups groups stream fewer blocks per wave (down to one); the bytes,
+    statuses and recovered masks equal the per-shape group sizes (min_groups=0), for encode and for
+    decode with the wave plan that small batches take and with the lane plans."""
+    L = 1200
+    rng = np.random.default_rng(k * 7 + r)
+    src = to_dev(synth_bytes(nb * k * L, k + r).reshape(nb, k, L))
+    outs = {}
+    for mg in (0, 1024):
+        with eng.knob("min_groups", mg):
+            rep = torch.zeros((nb, r, L), dtype=torch.uint8, device=DEV)
+            eng.rlc_encode(src, rep, k, r, L, fbn_base=77)
+            outs[mg] = rep
+    assert torch.equal(outs[0], outs[1024])
+    rep = outs[0]
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        e = int(rng.integers(0, min(k, r) + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        rp[b] = masks_from_lists(1, r, [rng.choice(r, int(rng.integers(max(0, e - 1), r + 1)),
+                                                   replace=False).tolist()])[0]
+    work = src.cpu().numpy().copy()
+    for b in range(nb):
+        for j in range(k):
+            if not (int(sp[b, j // 64]) >> (j % 64)) & 1:
+                work[b, j] = 0xA5
+    res = {}
+    for mg, plan in ((0, 0), (1024, 0), (1024, 1), (1024, 2)):
+        with eng.knob("min_groups", mg), eng.knob("plan", plan):
+            w = to_dev(work)
+            st = torch.full((nb,), 0xEE, dtype=torch.uint8, device=DEV)
+            rec = torch.full((nb, 2), -1, dtype=torch.int64, device=DEV)
+            eng.rlc_decode(w, rep, to_dev(sp), to_dev(rp), st, rec, k, r, L, fbn_base=77)
+            torch.cuda.synchronize()
+            res[(mg, plan)] = (w.cpu(), st.cpu(), rec.cpu())
+    base = res[(0, 0)]
+    got, st, rec = base[0].numpy(), base[1].numpy(), base[2].numpy().view(np.uint64)
+    src_h = src.cpu().numpy()
+    for b in range(nb):
+        for j in bits(rec[b], k):
+            assert np.array_equal(got[b, j], src_h[b, j]), (b, j)
+    for key, v in res.items():
+        assert all(torch.equal(a, b) for a, b in zip(v, base)), key
+    assert int((base[1] == DEC_RECOVERED).sum()) > 0
+
+
 def test_decode_apply_to_separate_buffer(eng, oracle):
     """fecgpu_rlc_decode_apply_to: recovered rows land in dst at their [block][j] slots, every
     other dst byte is untouched, and src is only read."""
