@@ -426,25 +426,34 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       __syncthreads();
     }
     // forward elimination without re-pivoting (:54-70): row_pk -= (A[pk][i] / A[pi][i]) row_pi for all
-    // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below)
+    // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below).  A lane owns a
+    // column (of A from i on, then of V) and walks the rows below: the pivot row's entry and its log
+    // stay in registers, each row's term log is a broadcast LDS read, and the row updates are
+    // independent (no division, no dependent chain across rows).
     for (int i = 0; i < n - 1; i++) {
       const int pi = perm[i];
       const uint32_t piv = A[pi * empad + i];
       const int below = n - 1 - i;
+      const uint32_t lpiv = LOG[piv];
       for (int x = lane; x < below; x += 64) {  // log of the term, 255 = zero term
         const uint32_t a = A[perm[i + 1 + x] * empad + i];
-        terms[x] = (piv && a) ? (uint8_t)EXP[LOG[a] + 255u - LOG[piv]] : (uint8_t)0;
+        const int d = (int)LOG[a] - (int)lpiv;
+        terms[x] = (piv && a) ? (uint8_t)(d < 0 ? d + 255 : d) : (uint8_t)255;
       }
       __syncthreads();
       const int wa = n - i, w = wa + k;  // columns i..n-1 of A, then all of V
-      for (int x = lane; x < below * w; x += 64) {
-        const int rr = x / w, c = x - rr * w;
-        const uint32_t t = terms[rr];
-        if (!t) continue;
-        const int pk = perm[i + 1 + rr];
-        const uint32_t lt = LOG[t];
-        if (c < wa) A[pk * empad + i + c] ^= (uint8_t)mul_l(A[pi * empad + i + c], lt);
-        else V[pk * kpad + c - wa] ^= (uint8_t)mul_l(V[pi * kpad + c - wa], lt);
+      for (int c = lane; c < w; c += 64) {
+        const bool ina = c < wa;
+        const uint32_t pv = ina ? A[pi * empad + i + c] : V[pi * kpad + c - wa];
+        if (!pv) continue;
+        const uint32_t lp = LOG[pv];
+        uint8_t *col = ina ? A + i + c : V + (c - wa);
+        const int rs = ina ? empad : kpad;
+        for (int rr = 0; rr < below; rr++) {
+          const uint32_t t = terms[rr];
+          if (t == 255u) continue;
+          col[perm[i + 1 + rr] * rs] ^= EXP[lp + t];
+        }
       }
       __syncthreads();
     }
@@ -456,21 +465,24 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       if (lane == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
       return;
     }
-    // back substitution (:71-114), column-oriented: x_i = V[pi] / A[pi][i], then V[pm] -= A[pm][i] x_i
+    // back substitution (:71-114), column-oriented: x_i = V[pi] / A[pi][i], then V[pm] -= A[pm][i] x_i.
+    // A lane owns column j of V and X throughout, so the steps need no barrier.
     for (int i = n - 1; i >= 0; i--) {
       const int pi = perm[i];
       const uint32_t li = 255u - LOG[A[pi * empad + i]];
-      for (int j = lane; j < k; j += 64) X[i * kpad + j] = (uint8_t)mul_l(V[pi * kpad + j], li);
-      __syncthreads();
-      for (int x = lane; x < i * k; x += 64) {
-        const int m = x / k, j = x - m * k;
-        const int pm = perm[m];
-        const uint32_t a = A[pm * empad + i];
-        const uint32_t xv = X[i * kpad + j];
-        if (a && xv) V[pm * kpad + j] ^= (uint8_t)EXP[LOG[a] + LOG[xv]];
+      for (int j = lane; j < k; j += 64) {
+        const uint32_t xv = mul_l(V[pi * kpad + j], li);
+        X[i * kpad + j] = (uint8_t)xv;
+        if (!xv) continue;
+        const uint32_t lx = LOG[xv];
+        for (int m = 0; m < i; m++) {
+          const int pm = perm[m];
+          const uint32_t a = A[pm * empad + i];
+          if (a) V[pm * kpad + j] ^= EXP[LOG[a] + lx];
+        }
       }
-      __syncthreads();
     }
+    __syncthreads();
     for (int x = lane; x < n * n; x += 64) {
       const int i = x / n, u = x - i * n;
       h[L.off_dep + i * em + u] = (u > i) && A[perm[i] * empad + u] != 0;
