@@ -188,7 +188,7 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
 /* Experiment knobs (A/B runs, cross-checks of alternative kernels in the tests).  Every knob has
  * a measured default; the environment variable named in DESIGN.md §6.1 seeds it ONCE per process
  * (first engine call), after which only these calls change it.  Names: "datapath_perm" (0/1),
- * "plan" (0 auto, 1 wave, 2 lane, 3 reg, 4 tile), "interleave" (0/1), "group" (0 = defaults, else
+ * "plan" (0 auto, 1 wave in LDS, 2 lane, 3 reg, 4 tile, 5 wave in registers where it fits), "interleave" (0/1), "group" (0 = defaults, else
  * a cap on blocks per group), "enc_tile_rt" / "enc_tile_waves" (0 = default tiling), "xor_generic",
  * "xor_idx64", "zc_read" (0/1), "ring" (the LDS-ring data path: 0 never, 1 wherever it applies,
  * 2 = default, 16-repair encode and 16-unknown decode tiles), "window_sc" (window encode on the

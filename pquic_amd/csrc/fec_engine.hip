@@ -52,7 +52,7 @@ enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GE
 static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
                                            "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring",
                                            "window_sc", "small_plan", "min_groups"};
-enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4 };
+enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
 
@@ -62,7 +62,8 @@ static void knobs_from_env() {
   g_knob[K_PERM] = (e = getenv("FECGPU_DATAPATH")) && !strcmp(e, "perm");
   e = getenv("FECGPU_PLAN");
   g_knob[K_PLAN] = !e ? PLAN_AUTO : !strcmp(e, "wave") ? PLAN_WAVE : !strcmp(e, "lane") ? PLAN_LANE
-                 : !strcmp(e, "reg") ? PLAN_REG : !strcmp(e, "tile") ? PLAN_TILE : PLAN_AUTO;
+                 : !strcmp(e, "reg") ? PLAN_REG : !strcmp(e, "tile") ? PLAN_TILE
+                 : !strcmp(e, "wreg") ? PLAN_WREG : PLAN_AUTO;
   g_knob[K_INTERLEAVE] = num(getenv("FECGPU_INTERLEAVE"), 1) != 0;
   g_knob[K_GROUP] = num(getenv("FECGPU_GROUP"), 0);  // 0: the measured per-shape defaults
   int a = 0, b = 0;
@@ -349,6 +350,62 @@ __device__ __forceinline__ void plan_load_tables(uint8_t *lds) {
   for (int i = threadIdx.x; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
 }
 
+// Common start of the wave plans: the block's unknowns (unk[u] = u-th missing source), its equations
+// (sel[e] = e-th present repair, :194-212) and their TinyMT32 coefficient rows X[e][0..k) in LDS.
+// Returns n, the number of unknowns, or 0 after writing the "nothing to do" record (:140-144).
+__device__ __forceinline__ int plan_wave_setup(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
+                                               const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp,
+                                               uint8_t *h, const PlanLds &P, int kpad, uint64_t &m0,
+                                               uint64_t &m1) {
+  const int lane = threadIdx.x;
+  uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
+  clip128(s0, s1, k);
+  clip128(q0, q1, r);
+  const int cur_ss = __popcll(s0) + __popcll(s1);
+  const int cur_rs = __popcll(q0) + __popcll(q1);
+  __syncthreads();
+  // rlc_fec_scheme_gf256.c:140-144
+  if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {
+    if (lane == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
+    return 0;
+  }
+  const int n = k - cur_ss;  // unknowns == equations (n_eq = min(n_unk, cur_rs) = n_unk)
+  m0 = ~s0;
+  m1 = ~s1;
+  clip128(m0, m1, k);
+  for (int j = lane; j < k; j += 64)
+    if (bit128(m0, m1, j)) P.unk[rank128(m0, m1, j)] = j;
+  for (int i = lane; i < r; i += 64)
+    if (bit128(q0, q1, i)) {
+      const int e = rank128(q0, q1, i);
+      if (e < n) P.sel[e] = i;
+    }
+  __syncthreads();
+  const uint32_t f = block_fbn(b, fbn_base, fbn);
+  for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
+    Tmt t;
+    tmt_init(t, repair_seed(seeds, b, r, f, (uint32_t)P.sel[e]));
+    for (int j = 0; j < k; j++) P.X[e * kpad + j] = tmt_coef(t);
+  }
+  __syncthreads();
+  return n;
+}
+
+// Record fields every wave plan writes the same way: unknowns, equations, slot map, status.
+__device__ __forceinline__ void plan_wave_finish(uint8_t *h, const WsLayout &L, const PlanLds &P, int k, int n,
+                                                 uint64_t m0, uint64_t m1) {
+  const int lane = threadIdx.x;
+  for (int u = lane; u < n; u += 64) {
+    h[L.off_nz + u] = 0;
+    h[L.off_unk + u] = (uint8_t)P.unk[u];
+    h[L.off_sel + u] = (uint8_t)P.sel[u];
+  }
+  // slot map: input j = source j if present, else the repair selected for its unknown
+  for (int j = lane; j < k; j += 64)
+    h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | P.sel[rank128(m0, m1, j)]) : (uint8_t)j;
+  if (lane == 0) { h[0] = FECGPU_BLOCK_RECOVERED; h[1] = (uint8_t)n; }
+}
+
 __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
                                 const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *ws,
                                 uint8_t *lds) {
@@ -359,41 +416,14 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
   const int empad = (int)pad16((uint32_t)em);
   const PlanLds P = plan_carve(lds, em, kpad, empad);
   uint8_t *A = P.A, *V = P.V, *X = P.X, *EXP = P.exp, *LOG = P.log, *terms = P.terms;
-  int *unk = P.unk, *sel = P.sel, *perm = P.perm;
+  int *unk = P.unk, *perm = P.perm;
   // x * y with y != 0 given as log y
   auto mul_l = [&](uint32_t x, uint32_t ly) -> uint32_t { return x ? EXP[LOG[x] + ly] : 0u; };
   {
     uint8_t *h = ws + b * (uint64_t)L.stride;
-    uint64_t s0 = sp[2 * b], s1 = sp[2 * b + 1], q0 = rp[2 * b], q1 = rp[2 * b + 1];
-    clip128(s0, s1, k);
-    clip128(q0, q1, r);
-    const int cur_ss = __popcll(s0) + __popcll(s1);
-    const int cur_rs = __popcll(q0) + __popcll(q1);
-    __syncthreads();
-    // rlc_fec_scheme_gf256.c:140-144
-    if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {
-      if (lane == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
-      return;
-    }
-    const int n = k - cur_ss;  // unknowns == equations (n_eq = min(n_unk, cur_rs) = n_unk)
-    uint64_t m0 = ~s0, m1 = ~s1;
-    clip128(m0, m1, k);
-    // unknown u -> u-th missing source; equation e -> e-th present repair (:194-212)
-    for (int j = lane; j < k; j += 64)
-      if (bit128(m0, m1, j)) unk[rank128(m0, m1, j)] = j;
-    for (int i = lane; i < r; i += 64)
-      if (bit128(q0, q1, i)) {
-        const int e = rank128(q0, q1, i);
-        if (e < n) sel[e] = i;
-      }
-    __syncthreads();
-    const uint32_t f = block_fbn(b, fbn_base, fbn);
-    for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
-      Tmt t;
-      tmt_init(t, repair_seed(seeds, b, r, f, (uint32_t)sel[e]));
-      for (int j = 0; j < k; j++) X[e * kpad + j] = tmt_coef(t);
-    }
-    __syncthreads();
+    uint64_t m0 = 0, m1 = 0;
+    const int n = plan_wave_setup(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
+    if (!n) return;
     // A[e][u] = row_e[unk[u]];  V[e][j] = present j ? row_e[j] : (j == unk[e])
     for (int x = lane; x < n * n; x += 64) {
       const int e = x / n, u = x - e * n;
@@ -491,16 +521,175 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       const int i = x / k, j = x - i * k;
       h[L.off_D + i * k + j] = X[i * kpad + j];
     }
-    for (int u = lane; u < n; u += 64) {
-      h[L.off_nz + u] = 0;
-      h[L.off_unk + u] = (uint8_t)unk[u];
-      h[L.off_sel + u] = (uint8_t)sel[u];
-    }
-    // slot map: input j = source j if present, else the repair selected for its unknown
-    for (int j = lane; j < k; j += 64)
-      h[L.off_slot + j] = bit128(m0, m1, j) ? (uint8_t)(0x80 | sel[rank128(m0, m1, j)]) : (uint8_t)j;
-    if (lane == 0) { h[0] = FECGPU_BLOCK_RECOVERED; h[1] = (uint8_t)n; }
+    plan_wave_finish(h, L, P, k, n, m0, m1);
   }
+}
+
+// Register wave plan (n <= EM unknowns, n + k <= 64 C columns): the same elimination as
+// plan_wave_block with the system in VGPRs.  Lane c owns column c (A column c for c < n, V column
+// c - n after it; a second column at c + 64 when C = 2) as EM row registers; rows are swapped in
+// place by the sort, so row i is perm[i] of the LDS plan.  Every row index is a compile-time
+// constant of the unrolled loops and the per-row scalars (pivot terms, A[m][i]) come from the
+// owning lane through readlane, so the only LDS traffic is the log/exp lookups, which are
+// independent across rows.  Same record bytes (test_plan_kernels_agree).
+template <int EM, int C>
+__device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
+                                const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *ws,
+                                uint8_t *lds) {
+  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
+  const int lane = threadIdx.x;
+  const int kpad = (int)pad16((uint32_t)k);
+  const PlanLds P = plan_carve(lds, (int)L.em, kpad, (int)pad16(L.em));
+  const uint8_t *EXP = P.exp, *LOG = P.log, *X = P.X;
+  uint8_t *h = ws + b * (uint64_t)L.stride;
+  uint64_t m0 = 0, m1 = 0;
+  const int n = plan_wave_setup(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
+  if (!n) return;
+  uint32_t col[C][EM];
+  bool isv[C], live[C];
+  int jv[C];
+#pragma unroll
+  for (int q = 0; q < C; q++) {
+    const int c = lane + 64 * q;
+    isv[q] = c >= n;
+    live[q] = c < n + k;
+    const int j = isv[q] ? c - n : P.unk[c < n ? c : 0];
+    jv[q] = j;
+    const bool present = live[q] && isv[q] && bit128(~m0, ~m1, j);
+#pragma unroll
+    for (int e = 0; e < EM; e++) {
+      uint32_t v = 0;
+      if (e < n && live[q]) v = (isv[q] && !present) ? (uint32_t)(P.unk[e] == j) : X[e * kpad + j];
+      col[q][e] = v;
+    }
+  }
+  // sort_system (:28-40): position i takes the first row j >= i with the largest A[j][i]; lane i
+  // holds column i, so it finds the row and every lane swaps rows i and mx in its registers
+#pragma unroll
+  for (int i = 0; i < EM; i++) {
+    if (i >= n) break;
+    uint32_t key = 0;
+#pragma unroll
+    for (int j = i; j < EM; j++)
+      if (j < n) {
+        const uint32_t kj = (col[0][j] << 8) | (uint32_t)(255 - j);
+        key = kj > key ? kj : key;
+      }
+    const int mx = 255 - (int)(__builtin_amdgcn_readlane(key, i) & 0xffu);
+    if (mx != i) {
+#pragma unroll
+      for (int q = 0; q < C; q++) {
+        uint32_t vm = 0;
+#pragma unroll
+        for (int j = i + 1; j < EM; j++) vm = j == mx ? col[q][j] : vm;
+#pragma unroll
+        for (int j = i + 1; j < EM; j++) col[q][j] = j == mx ? col[q][i] : col[q][j];
+        col[q][i] = vm;
+      }
+    }
+  }
+  // forward elimination without re-pivoting (:54-70): rows below i -= (A[rr][i] / A[i][i]) row i,
+  // on A columns >= i and all of V; a zero pivot makes every term zero
+#pragma unroll
+  for (int i = 0; i < EM - 1; i++) {
+    if (i >= n - 1) break;
+    const uint32_t lpiv = LOG[col[0][i]];
+    const bool pz = col[0][i] == 0;
+    uint32_t tl[EM];
+#pragma unroll
+    for (int rr = i + 1; rr < EM; rr++) {
+      const uint32_t a = col[0][rr];
+      const int d = (int)LOG[a] - (int)lpiv;
+      const uint32_t t = (pz || !a) ? 255u : (uint32_t)(d < 0 ? d + 255 : d);
+      tl[rr] = __builtin_amdgcn_readlane(t, i);
+    }
+#pragma unroll
+    for (int q = 0; q < C; q++) {
+      const uint32_t pv = col[q][i];
+      const bool act = live[q] && (isv[q] || lane >= i) && pv != 0;
+      const uint32_t lp = LOG[pv];
+#pragma unroll
+      for (int rr = i + 1; rr < EM; rr++)
+        if (rr < n && tl[rr] != 255u && act) col[q][rr] ^= EXP[lp + tl[rr]];
+    }
+  }
+  // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
+  bool ub = false;
+#pragma unroll
+  for (int i = 0; i < EM; i++)
+    if (i < n) ub |= __builtin_amdgcn_readlane(col[0][i], i) == 0;
+  if (ub) {
+    if (lane == 0) { h[0] = FECGPU_BLOCK_REF_UB; h[1] = 0; }
+    return;
+  }
+  // dependency flags of the upper-triangular system: A lane u writes column u
+  if (lane < n) {
+#pragma unroll
+    for (int i = 0; i < EM; i++)
+      if (i < n) h[L.off_dep + i * L.em + lane] = (lane > i) && col[0][i] != 0;
+  }
+  // back substitution (:71-114): x_i = V[i] / A[i][i], then V[m] -= A[m][i] x_i for m < i
+#pragma unroll
+  for (int i = EM - 1; i >= 0; i--) {
+    if (i >= n) continue;
+    const uint32_t li = 255u - LOG[__builtin_amdgcn_readlane(col[0][i], i)];
+    uint32_t la[EM];
+#pragma unroll
+    for (int m = 0; m < i; m++) {
+      const uint32_t a = __builtin_amdgcn_readlane(col[0][m], i);
+      la[m] = a ? (uint32_t)LOG[a] : 255u;
+    }
+#pragma unroll
+    for (int q = 0; q < C; q++) {
+      if (!(isv[q] && live[q])) continue;
+      const uint32_t xv = col[q][i] ? (uint32_t)EXP[LOG[col[q][i]] + li] : 0u;
+      col[q][i] = xv;
+      const uint32_t lx = LOG[xv];
+#pragma unroll
+      for (int m = 0; m < i; m++)
+        if (la[m] != 255u && xv) col[q][m] ^= EXP[la[m] + lx];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < C; q++)
+    if (isv[q] && live[q]) {
+#pragma unroll
+      for (int i = 0; i < EM; i++)
+        if (i < n) h[L.off_D + i * k + jv[q]] = (uint8_t)col[q][i];
+    }
+  plan_wave_finish(h, L, P, k, n, m0, m1);
+}
+
+// Wave plan for one block: the register plan when the system fits (em <= 16, k + em <= 64) and
+// wreg is set, else the LDS plan.  (Two columns per lane for k + em <= 128 measured slower than the
+// LDS plan: k64 e16 180 vs 83 us, profiles/r02_plan_crossover_wreg.log.)
+__device__ __forceinline__ bool plan_wreg_fits(int k, int r) {
+  const int em = k < r ? k : r;
+  return em <= 16 && k + em <= 64;
+}
+__device__ __forceinline__ void plan_wave_any(int wreg, uint64_t b, int k, int r, uint32_t fbn_base,
+                                              const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
+                                              const uint64_t *rp, uint8_t *ws, uint8_t *lds) {
+  const int em = k < r ? k : r;
+  if (wreg && plan_wreg_fits(k, r)) {
+    if (em <= 4) plan_wreg_block<4, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    else if (em <= 8) plan_wreg_block<8, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    else plan_wreg_block<16, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    return;
+  }
+  plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+}
+
+// The register wave plan as its own kernel (k_rlc_plan keeps the LDS plan's smaller register
+// footprint for the batches where occupancy counts).
+template <int EM>
+__global__ __launch_bounds__(64) void k_rlc_plan_wreg(uint64_t nblocks, int k, int r, uint32_t fbn_base,
+                                                      const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
+                                                      const uint64_t *rp, uint8_t *ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  plan_load_tables(lds);
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    plan_wreg_block<EM, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
 }
 
 __global__ __launch_bounds__(64) void k_rlc_plan(uint64_t nblocks, int k, int r, uint32_t fbn_base,
@@ -1524,7 +1713,7 @@ __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ s
                                                          int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
                                                          const uint32_t *seeds, const uint64_t *sp,
                                                          const uint64_t *rp, uint32_t rec_off, uint8_t *status,
-                                                         uint64_t *recovered, uint8_t *dst) {
+                                                         uint64_t *recovered, uint8_t *dst, int wreg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t stride = ws_layout((uint32_t)k, (uint32_t)r).stride;
   for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
@@ -1535,7 +1724,7 @@ __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ s
       __syncthreads();
       if (threadIdx.x == 0) plan_reg_block<8, 8>(b, k, r, fbn_base, fbn, seeds, sp, rp, lds + rec_off, lds, lds + 512);
     } else {
-      plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
+      plan_wave_any(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
     }
     __syncthreads();
     recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, wsx, 0, 1, status,
@@ -2527,9 +2716,10 @@ static int decode_args(const void *src, const void *rep, uint64_t nblocks, uint3
 }
 
 // Up to this many blocks a wave per block plans fastest: the lane-parallel plans (reg / tile / lane)
-// take one lane's dependent chain whatever the batch, e.g. k32 e8 70 us against the wave plan's 27-38
-// us at 65-4096 blocks; they win from ~4096 blocks on (profiles/r02_plan_crossover.log).
-constexpr uint64_t kPlanWaveMaxBlocks = 2048;
+// take one lane's dependent chain whatever the batch, e.g. k32 e8 70 us against the register wave
+// plan's 17-26 us at 65-4096 blocks; they win from ~8192 blocks on
+// (profiles/r02_plan_crossover_wreg.log).
+constexpr uint64_t kPlanWaveMaxBlocks = 4096;
 
 static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t fbn_base, const uint32_t *fbn,
                             const uint32_t *seeds, const uint64_t *src_present, const uint64_t *rep_present,
@@ -2544,6 +2734,9 @@ static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t f
   // knob "plan" (FECGPU_PLAN=reg|tile|lane|wave) overrides the size rule (A/B experiments; the tests
   // compare the plan kernels on the same inputs through fecgpu_set_knob)
   int force = knob(K_PLAN);
+  // the wave kernel takes the register plan wherever it fits unless the LDS wave plan is forced
+  const int wreg = force != PLAN_WAVE;
+  if (force == PLAN_WREG) force = PLAN_WAVE;
   const uint32_t em = ws_layout(k, r).em;
   // up to kPlanWaveMaxBlocks blocks (the synchronous hooks run one): every block gets its own wave
   // and the wave plan's row-parallel elimination, instead of a lane's serial replay -- one-block
@@ -2601,8 +2794,18 @@ static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t f
         raised = true;
       }
     }
-    hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
-                       fbn_base, fbn, seeds, src_present, rep_present, ws);
+    if (wreg && em <= 16 && k + em <= 64) {
+#define FEC_PLAN_WREG(EM)                                                                                  \
+  hipLaunchKernelGGL((k_rlc_plan_wreg<EM>), dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, \
+                     (int)r, fbn_base, fbn, seeds, src_present, rep_present, ws)
+      if (em <= 4) FEC_PLAN_WREG(4);
+      else if (em <= 8) FEC_PLAN_WREG(8);
+      else FEC_PLAN_WREG(16);
+#undef FEC_PLAN_WREG
+    } else {
+      hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,
+                         fbn_base, fbn, seeds, src_present, rep_present, ws);
+    }
   }
   HIPCHK(hipGetLastError());
   return FECGPU_OK;
@@ -2706,12 +2909,13 @@ static void launch_decode_small(uint8_t *src, const uint8_t *rep, uint64_t nb, i
     if (k <= 32 && knob(K_SMALL_PLAN) == 1) {  // the lane-register plan: its system fits one lane
       hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, true>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k,
                          r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered,
-                         dst);
+                         dst, 0);
       return;
     }
   }
   hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, false>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered, dst);
+                     L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered, dst,
+                     knob(K_PLAN) != PLAN_WAVE);
 }
 }  // extern "C++"
 

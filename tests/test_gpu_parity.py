@@ -575,10 +575,11 @@ def _ws_fields(ws, k, r, n_blocks):
 
 @pytest.mark.parametrize("k,r,nb", [(1, 1, 64), (4, 1, 300), (16, 4, 2000), (12, 6, 700), (16, 8, 500),
                                     (30, 3, 400), (32, 8, 600), (9, 9, 300), (64, 16, 300), (40, 12, 200),
-                                    (61, 16, 100), (20, 16, 150)])
+                                    (61, 16, 100), (20, 16, 150), (60, 8, 300), (100, 8, 100), (112, 16, 50),
+                                    (113, 16, 40)])
 def test_plan_kernels_agree(eng, k, r, nb):
     """The plan kernels (register lane-per-block, tiled register, LDS lane-per-block,
-    wave-per-block) write identical decode records -- same unknowns, repair selection, solution
+    wave-per-block in LDS and in registers) write identical decode records -- same unknowns, repair selection, solution
     rows D, dependency flags, and the same reference-crash verdicts -- on random erasure
     patterns.  Kernels whose size limits exclude (k, r) are skipped."""
     rng = np.random.default_rng(k * 1000 + r)
@@ -595,8 +596,8 @@ def test_plan_kernels_agree(eng, k, r, nb):
     res = {}
     em = min(k, r)
     kinds = [x for x, ok in (("reg", k <= 32 and em <= 8), ("tile", k <= 64 and em <= 16), ("lane", True),
-                             ("wave", True)) if ok]
-    plan_id = {"wave": 1, "lane": 2, "reg": 3, "tile": 4}
+                             ("wave", True), ("wreg", em <= 16 and k + em <= 64)) if ok]
+    plan_id = {"wave": 1, "lane": 2, "reg": 3, "tile": 4, "wreg": 5}
     for kind in kinds:
         with eng.knob("plan", plan_id[kind]):
             ws = eng.alloc_workspace(nb, k, r)

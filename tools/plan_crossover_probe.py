@@ -1,6 +1,7 @@
 """Decode plan kernel time per launch: the wave plan (a wave per block, row-parallel elimination;
-knob plan=1) against the automatic choice above 64 blocks (lane-parallel plans: reg / tile / lane),
-over batch sizes, to place the crossover.  usage: python tools/plan_crossover_probe.py"""
+knob plan=1 in LDS, plan=5 in registers where the system fits) against the automatic choice
+(lane-parallel plans: reg / tile / lane above the wave-plan threshold), over batch sizes, to place
+the crossover.  usage: python tools/plan_crossover_probe.py"""
 import os
 import sys
 
@@ -27,7 +28,7 @@ def dev_us(fn, n):
 
 
 for k, r, e in [(16, 4, 4), (16, 4, 1), (32, 8, 8), (32, 8, 2), (64, 16, 16), (64, 16, 4)]:
-    for nb in (65, 256, 1024, 4096, 16384, 65536):
+    for nb in (65, 256, 1024, 2048, 4096, 8192, 16384, 65536):
         g = torch.Generator().manual_seed(nb + k)
         sp = torch.zeros((nb, 2), dtype=torch.int64)
         full = (1 << k) - 1
@@ -45,6 +46,8 @@ for k, r, e in [(16, 4, 4), (16, 4, 1), (32, 8, 8), (32, 8, 2), (64, 16, 16), (6
         with eng.knob("plan", 1):
             tw = dev_us(lambda: eng.rlc_decode_plan(sp, rp, k, r, nb, ws), n)
             wsw = ws.clone()
+        with eng.knob("plan", 5):
+            tr = dev_us(lambda: eng.rlc_decode_plan(sp, rp, k, r, nb, ws), n)
         ta = dev_us(lambda: eng.rlc_decode_plan(sp, rp, k, r, nb, ws), n)
-        same = "" if torch.equal(wsw, ws) else " (workspaces differ)"
-        print(f"k{k:<3d} r{r:<2d} e{e:<2d} blocks {nb:6d}: wave {tw:9.1f} us   auto {ta:9.1f} us{same}", flush=True)
+        print(f"k{k:<3d} r{r:<2d} e{e:<2d} blocks {nb:6d}: wave {tw:9.1f} us   wave-reg {tr:9.1f} us   "
+              f"auto {ta:9.1f} us", flush=True)
