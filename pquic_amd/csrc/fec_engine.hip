@@ -525,7 +525,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
   }
 }
 
-// Register wave plan (n <= EM unknowns, n + k <= 64 C columns): the same elimination as
+// Register wave plan (n <= EM unknowns, n + k <= 64 C columns; used with EM <= 8, C = 1): the same elimination as
 // plan_wave_block with the system in VGPRs.  Lane c owns column c (A column c for c < n, V column
 // c - n after it; a second column at c + 64 when C = 2) as EM row registers; rows are swapped in
 // place by the sort, so row i is perm[i] of the LDS plan.  Every row index is a compile-time
@@ -570,8 +570,8 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
     if (i >= n) break;
     uint32_t key = 0;
 #pragma unroll
-    for (int j = i; j < EM; j++)
-      if (j < n) {
+    for (int j = 0; j < EM; j++)
+      if (j >= i && j < n) {
         const uint32_t kj = (col[0][j] << 8) | (uint32_t)(255 - j);
         key = kj > key ? kj : key;
       }
@@ -581,9 +581,11 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       for (int q = 0; q < C; q++) {
         uint32_t vm = 0;
 #pragma unroll
-        for (int j = i + 1; j < EM; j++) vm = j == mx ? col[q][j] : vm;
+        for (int j = 0; j < EM; j++)
+          if (j > i) vm = j == mx ? col[q][j] : vm;
 #pragma unroll
-        for (int j = i + 1; j < EM; j++) col[q][j] = j == mx ? col[q][i] : col[q][j];
+        for (int j = 0; j < EM; j++)
+          if (j > i) col[q][j] = j == mx ? col[q][i] : col[q][j];
         col[q][i] = vm;
       }
     }
@@ -597,7 +599,8 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
     const bool pz = col[0][i] == 0;
     uint32_t tl[EM];
 #pragma unroll
-    for (int rr = i + 1; rr < EM; rr++) {
+    for (int rr = 0; rr < EM; rr++) {
+      if (rr <= i) continue;
       const uint32_t a = col[0][rr];
       const int d = (int)LOG[a] - (int)lpiv;
       const uint32_t t = (pz || !a) ? 255u : (uint32_t)(d < 0 ? d + 255 : d);
@@ -609,8 +612,8 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       const bool act = live[q] && (isv[q] || lane >= i) && pv != 0;
       const uint32_t lp = LOG[pv];
 #pragma unroll
-      for (int rr = i + 1; rr < EM; rr++)
-        if (rr < n && tl[rr] != 255u && act) col[q][rr] ^= EXP[lp + tl[rr]];
+      for (int rr = 0; rr < EM; rr++)
+        if (rr > i && rr < n && tl[rr] != 255u && act) col[q][rr] ^= EXP[lp + tl[rr]];
     }
   }
   // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
@@ -635,7 +638,8 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
     const uint32_t li = 255u - LOG[__builtin_amdgcn_readlane(col[0][i], i)];
     uint32_t la[EM];
 #pragma unroll
-    for (int m = 0; m < i; m++) {
+    for (int m = 0; m < EM; m++) {
+      if (m >= i) continue;
       const uint32_t a = __builtin_amdgcn_readlane(col[0][m], i);
       la[m] = a ? (uint32_t)LOG[a] : 255u;
     }
@@ -646,8 +650,8 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       col[q][i] = xv;
       const uint32_t lx = LOG[xv];
 #pragma unroll
-      for (int m = 0; m < i; m++)
-        if (la[m] != 255u && xv) col[q][m] ^= EXP[la[m] + lx];
+      for (int m = 0; m < EM; m++)
+        if (m < i && la[m] != 255u && xv) col[q][m] ^= EXP[la[m] + lx];
     }
   }
 #pragma unroll
@@ -660,12 +664,13 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
   plan_wave_finish(h, L, P, k, n, m0, m1);
 }
 
-// Wave plan for one block: the register plan when the system fits (em <= 16, k + em <= 64) and
-// wreg is set, else the LDS plan.  (Two columns per lane for k + em <= 128 measured slower than the
-// LDS plan: k64 e16 180 vs 83 us, profiles/r02_plan_crossover_wreg.log.)
+// Wave plan for one block: the register plan when the system fits (em <= 8, k + em <= 64) and wreg
+// is set, else the LDS plan.  Two columns per lane (k + em <= 128) measured slower than the LDS plan
+// (k64 e16 180 vs 83 us); 16 rows leave part of the system in scratch (the unrolled elimination
+// exceeds the compiler's full-unroll budget), so em <= 8.
 __device__ __forceinline__ bool plan_wreg_fits(int k, int r) {
   const int em = k < r ? k : r;
-  return em <= 16 && k + em <= 64;
+  return em <= 8 && k + em <= 64;
 }
 __device__ __forceinline__ void plan_wave_any(int wreg, uint64_t b, int k, int r, uint32_t fbn_base,
                                               const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
@@ -673,8 +678,7 @@ __device__ __forceinline__ void plan_wave_any(int wreg, uint64_t b, int k, int r
   const int em = k < r ? k : r;
   if (wreg && plan_wreg_fits(k, r)) {
     if (em <= 4) plan_wreg_block<4, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
-    else if (em <= 8) plan_wreg_block<8, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
-    else plan_wreg_block<16, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    else plan_wreg_block<8, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
     return;
   }
   plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
@@ -2794,13 +2798,12 @@ static int decode_plan_impl(uint64_t nblocks, uint32_t k, uint32_t r, uint32_t f
         raised = true;
       }
     }
-    if (wreg && em <= 16 && k + em <= 64) {
+    if (wreg && em <= 8 && k + em <= 64) {
 #define FEC_PLAN_WREG(EM)                                                                                  \
   hipLaunchKernelGGL((k_rlc_plan_wreg<EM>), dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, \
                      (int)r, fbn_base, fbn, seeds, src_present, rep_present, ws)
       if (em <= 4) FEC_PLAN_WREG(4);
-      else if (em <= 8) FEC_PLAN_WREG(8);
-      else FEC_PLAN_WREG(16);
+      else FEC_PLAN_WREG(8);
 #undef FEC_PLAN_WREG
     } else {
       hipLaunchKernelGGL(k_rlc_plan, dim3(grid_for(nblocks)), dim3(64), plan_lds, s, nblocks, (int)k, (int)r,

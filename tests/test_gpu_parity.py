@@ -596,7 +596,7 @@ def test_plan_kernels_agree(eng, k, r, nb):
     res = {}
     em = min(k, r)
     kinds = [x for x, ok in (("reg", k <= 32 and em <= 8), ("tile", k <= 64 and em <= 16), ("lane", True),
-                             ("wave", True), ("wreg", em <= 16 and k + em <= 64)) if ok]
+                             ("wave", True), ("wreg", em <= 8 and k + em <= 64)) if ok]
     plan_id = {"wave": 1, "lane": 2, "reg": 3, "tile": 4, "wreg": 5}
     for kind in kinds:
         with eng.knob("plan", plan_id[kind]):
