@@ -280,7 +280,7 @@ __global__ __launch_bounds__(64) void k_rlc_encode(const uint32_t *__restrict__ 
 // RLC decode: plan (coefficients only), recover (data), finalize (zero propagation)
 // =============================================================================================
 // GF(2^8)/0x11D log/exp tables (exp doubled so exp[log a + log b] needs no reduction).
-struct GfLogExp { uint8_t exp[512]; uint8_t log[256]; };
+struct alignas(16) GfLogExp { uint8_t exp[512]; uint8_t log[256]; };
 
 constexpr GfLogExp make_logexp() {
   GfLogExp t{};
@@ -346,8 +346,11 @@ __device__ __forceinline__ void clip128(uint64_t &m0, uint64_t &m1, int n) {
 
 // One block's plan by one wave (row-parallel elimination).  `lds` holds the log/exp tables at 0
 // (plan_load_tables) and room for plan_lds_bytes(k, r).  Every lane of the wave must call it.
+// (48 lanes, one 16-B load each: one memory round trip, which a one-block decode waits for)
 __device__ __forceinline__ void plan_load_tables(uint8_t *lds) {
-  for (int i = threadIdx.x; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  static_assert(sizeof(GfLogExp) == 48 * 16, "log/exp tables: 48 x 16 B");
+  if (threadIdx.x < 48)
+    reinterpret_cast<uint4 *>(lds)[threadIdx.x] = reinterpret_cast<const uint4 *>(&kLogExp)[threadIdx.x];
 }
 
 // Common start of the wave plans: the block's unknowns (unk[u] = u-th missing source), its equations
@@ -747,7 +750,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_lane(uint64_t nblocks, int k, i
   const int lane = threadIdx.x;
   const int em = (int)L.em;
   uint8_t *EXP = lds, *LOG = lds + 512;
-  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  plan_load_tables(lds);
   __syncthreads();
   uint8_t *my = lds + 768 + lane;
   const uint32_t orow = plan_out_row(L.stride);
@@ -1044,7 +1047,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_reg(uint64_t nblocks, int k, in
   const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   const uint8_t *EXP = lds, *LOG = lds + 512;
-  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  plan_load_tables(lds);
   __syncthreads();
   const uint32_t orow = plan_out_row(L.stride);
   uint8_t *h = lds + 768 + (size_t)lane * orow;  // this lane's workspace record (LDS copy)
@@ -1083,7 +1086,7 @@ __global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, i
   uint8_t *CO = lds + 768;                                   // [BPW][EM][kpad] coefficient rows
   const uint32_t orow = plan_out_row(L.stride);
   uint8_t *OUTR = CO + (size_t)BPW * EM * kpad;             // [BPW][orow] records
-  for (int i = lane; i < 768; i += 64) lds[i] = reinterpret_cast<const uint8_t *>(&kLogExp)[i];
+  plan_load_tables(lds);
   uint8_t *h = OUTR + (size_t)g * orow;
   const uint8_t *crow = CO + (size_t)g * EM * kpad;
   const int c0 = q * CW;
