@@ -79,8 +79,27 @@ void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *c) {
   delete c;
 }
 
+// Page-locked allocations made through fecgpu_host_alloc, with their device addresses, so the
+// per-call lookups of the library's own staging buffers (the synchronous hooks pass seven pointers
+// per recover) skip hipPointerGetAttributes.  fecgpu_host_free removes an entry before freeing,
+// so a stale entry can never describe memory that is no longer page-locked.
+namespace {
+struct PinnedRange { uintptr_t base; size_t size; uint8_t *dev; };
+constexpr int kPinnedMax = 64;
+PinnedRange g_pinned[kPinnedMax];
+int g_npinned = 0;
+std::mutex g_pinned_mu;
+}  // namespace
+
 // Device address of page-locked host memory (hipHostMalloc'd or registered), else nullptr.
 static uint8_t *mapped_host(const void *p) {
+  if (!p) return nullptr;
+  {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    for (int i = 0; i < g_npinned; i++)
+      if (a - g_pinned[i].base < g_pinned[i].size) return g_pinned[i].dev + (a - g_pinned[i].base);
+  }
   hipPointerAttribute_t pa;
   if (p && hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer)
     return (uint8_t *)pa.devicePointer;
@@ -295,10 +314,26 @@ extern "C" {
 void *fecgpu_host_alloc(size_t bytes) {
   void *p = nullptr;
   if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  hipPointerAttribute_t pa;
+  if (hipPointerGetAttributes(&pa, p) == hipSuccess && pa.devicePointer) {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    if (g_npinned < kPinnedMax) g_pinned[g_npinned++] = {(uintptr_t)p, bytes ? bytes : 1, (uint8_t *)pa.devicePointer};
+  } else {
+    (void)hipGetLastError();
+  }
   return p;
 }
 
 void fecgpu_host_free(void *p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    for (int i = 0; i < g_npinned; i++)
+      if (g_pinned[i].base == (uintptr_t)p) {
+        g_pinned[i] = g_pinned[--g_npinned];
+        break;
+      }
+  }
+  (void)hipHostFree(p);
 }
 }  // extern "C"
