@@ -51,6 +51,11 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe end-to-end legs")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-blocks", type=int, default=0,
+                   help="CPU-baseline sample size in blocks (0: about 300 MiB of source payload)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher / rendezvous check without a GPU: ranks time an empty step on gloo; "
+                        "value is 0 and the line says dry_run (tests only)")
     return p.parse_args()
 
 
@@ -222,39 +227,40 @@ def host_cpu_share():
     return cores, aff, quota
 
 
-def cpu_baseline(args, ncores):
+def cpu_baseline(args, ncores, k, r, e, L):
     """The reference's own plugins/fec scheme pluglets (rlc_fec_scheme_generate_gf256.c,
     rlc_fec_scheme_gf256.c compiled natively from the reference sources into
     oracle/_ref/libfecref.so; kind "reference") on every core of this process's CPU share, one
-    fork()ed worker per core, over a bounded sample of the same workload: RLC encode k=16 r=4 of
-    every block, then decode with 4 erasures.  The reference segfaults on ~1 % of erasure patterns
-    (SURVEY §8a A9); those blocks are screened out of its decode (untimed, by the CPU port) and the
-    value still counts their payload, so the reference number is, if anything, flattering.  The
-    port (oracle/fec_oracle.c, bit-exact) is timed beside it on as many threads; their ratio is
-    reported.  Runs before the process touches the GPU (the workers are forks)."""
+    fork()ed worker per core, over a bounded sample of the same workload: RLC encode of every
+    block, then (e > 0) decode with e erasures.  The reference segfaults on ~1-5 % of erasure
+    patterns; those blocks are screened out of its decode (untimed, by the CPU
+    port) and the value still counts their payload, so the reference number is, if anything,
+    flattering.  The port (oracle/fec_oracle.c, bit-exact) is timed beside it on as many threads;
+    their ratio is reported.  Runs before the process touches the GPU (the workers are forks)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes as C
     import numpy as np
     from oracle_py import Oracle, synth_bytes
     o = Oracle()
-    k, r, L, e = args.k, args.r, args.symbol, args.erasures
-    nb = 1 << 14  # 300 MiB of payload: larger than the host caches
+    nb = args.cpu_blocks or max(16, (300 << 20) // (k * L))  # ~300 MiB of payload: beyond the host caches
     src = synth_bytes(nb * k * L, 0x5EEDF3C0).reshape(nb, k, L)
     rng = np.random.default_rng(1)
     sp = np.zeros((nb, 2), np.uint64)
     rp = np.zeros((nb, 2), np.uint64)
-    full = (1 << k) - 1
     for b in range(nb):
-        m = full
-        for j in rng.choice(k, e, replace=False):
-            m &= ~(1 << int(j))
-        sp[b, 0] = m
-        rp[b, 0] = (1 << r) - 1
-    # screen: which patterns the reference survives (the port flags its x[-1] crash exactly)
-    rep0 = o.rlc_encode_batch(src, r, 0, ncores)
-    st, _ = o.rlc_decode_batch(src.copy(), rep0, sp, rp, 0, ncores)
-    skip = (st == 2).astype(np.uint8)
-    del rep0
+        m = [(1 << min(k, 64)) - 1, (1 << max(k - 64, 0)) - 1]
+        for j in (rng.choice(k, e, replace=False) if e else ()):
+            m[int(j) >> 6] &= ~(1 << (int(j) & 63))
+        sp[b] = m
+        rp[b] = [(1 << min(r, 64)) - 1, (1 << max(r - 64, 0)) - 1]
+    if e:  # screen: which patterns the reference survives (the port flags its x[-1] crash exactly)
+        rep0 = o.rlc_encode_batch(src, r, 0, ncores)
+        st, _ = o.rlc_decode_batch(src.copy(), rep0, sp, rp, 0, ncores)
+        skip = (st == 2).astype(np.uint8)
+        del rep0
+    else:  # encode-only workload: every block skips the reference's decode half
+        skip = np.ones(nb, np.uint8)
+    what = f"RLC encode{' + decode' if e else ''} pluglets"
     out = {"unit": "GiB/s", "cores": ncores, "kind": "reference"}
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
     gib_pass = nb * k * L / 2**30
@@ -269,9 +275,10 @@ def cpu_baseline(args, ncores):
         assert lib.ref_cpu_baseline(ncores, src.ctypes.data, nb, k, r, L, 0, sp.ctypes.data, skip.ctypes.data,
                                     passes, res) == 0, "reference CPU workers failed"
         out["value"] = round(passes * gib_pass / res[0], 4)
-        out["sample"] = (f"{passes} passes x {nb} blocks, k={k} r={r} L={L}: the reference's RLC encode + decode "
-                         f"pluglets (native gcc -O2), {ncores} fork()ed workers, {res[0]:.1f} s wall; "
-                         f"{int(skip.sum())} of {nb} erasure patterns crash the reference and are not decoded")
+        out["sample"] = (f"{passes} passes x {nb} blocks, k={k} r={r} e={e} L={L}: the reference's {what} "
+                         f"(native gcc -O2), {ncores} fork()ed workers, {res[0]:.1f} s wall"
+                         + (f"; {int(skip.sum())} of {nb} erasure patterns crash the reference and are not decoded"
+                            if e else ""))
     else:  # the reference build is absent: the port stands in (and says so)
         out["kind"] = "port"
     # the port on the same sample and thread count (second number, and its ratio to the reference)
@@ -280,7 +287,8 @@ def cpu_baseline(args, ncores):
         work = src.copy()
         t0 = time.perf_counter()
         rep = o.rlc_encode_batch(work, r, 0, ncores)
-        o.rlc_decode_batch(work, rep, sp, rp, 0, ncores)
+        if e:
+            o.rlc_decode_batch(work, rep, sp, rp, 0, ncores)
         t_total += time.perf_counter() - t0
         passes_p += 1
     port = round(passes_p * gib_pass / t_total, 4)
@@ -292,6 +300,85 @@ def cpu_baseline(args, ncores):
         out["value"] = port
         out["sample"] = out["port"]["sample"]
     return out
+
+
+def workload_cfg(args):
+    cfg = dict(CONFIGS[args.config])
+    if args.config == "k16":  # the legacy flags still shape the default workload
+        cfg.update(k=args.k, r=args.r, e=args.erasures, L=args.symbol, per_rank=args.blocks)
+    return cfg
+
+
+def measure_cpu_baseline(args, cfg):
+    """cpu_baseline for this workload (computed once per job, before any process touches the GPU)."""
+    ncores, aff, quota = host_cpu_share()
+    cpu = cpu_baseline(args, ncores, cfg["k"], cfg["r"], cfg["e"], cfg["L"])
+    cpu["host"] = {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+    return cpu
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment): this process never touches
+    the GPU.  It measures cpu_baseline first (its workers are fork()ed), then starts N child processes
+    of this script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), hands
+    them the baseline through a file, waits for all of them and exits with the first failure's code.
+    Rank 0 prints the JSON line.  No exec: the children are started as new processes."""
+    import signal
+    import subprocess
+    import tempfile
+    n = args.gpus
+    if not args.dry_run and os.environ.get("PQUIC_BENCH_SHARE_GPU") != "1":
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cfg = workload_cfg(args)
+    env = dict(os.environ)
+    tmp = None
+    if not args.no_cpu:
+        cpu = measure_cpu_baseline(args, cfg)
+        fd, tmp = tempfile.mkstemp(prefix="pquic_bench_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cpu, f)
+        env["PQUIC_BENCH_CPU_JSON"] = tmp
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), PQUIC_BENCH_LAUNCHED="1")
+    procs = []
+    try:
+        for i in range(n):
+            env_i = dict(env, RANK=str(i), LOCAL_RANK=str(i))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env_i))
+        rc = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for q in live:  # one rank failed: the others would wait at a barrier forever
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        if tmp:
+            os.unlink(tmp)
 
 
 def pcie_legs(torch, args, dev):
@@ -420,14 +507,61 @@ CONFIGS = {
 }
 
 
+def dry_run_rank(args, world, rank, cpu):
+    """--dry-run: the rank plumbing without a GPU (gloo): barrier, an empty timed region,
+    max-over-ranks and per-rank gather, then rank 0's line with value 0."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
+    per_rank = None
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        allr = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(allr, torch.tensor([elapsed], dtype=torch.float64))
+        per_rank = [float(x.item()) for x in allr]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "cpu_baseline": cpu,
+                          "per_rank_ms_per_step": per_rank}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    import torch
-    from pquic_amd import Engine
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # parent: starts one child process per GPU, never touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU "
+              f"(torchrun --nproc-per-node {args.gpus}, or plain `python bench.py --gpus {args.gpus}`)",
+              file=sys.stderr)
+        sys.exit(2)
+    cfg = workload_cfg(args)
+    k, r, e, L = cfg["k"], cfg["r"], cfg["e"], cfg["L"]
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        path = os.environ.get("PQUIC_BENCH_CPU_JSON")
+        if path:  # measured by the launcher before it started the ranks
+            with open(path) as f:
+                cpu = json.load(f)
+        else:  # before any HIP call: the reference's workers are fork()ed from this process
+            cpu = measure_cpu_baseline(args, cfg)
+    if args.dry_run:
+        dry_run_rank(args, world, rank, cpu)
+        return
+    import torch
+    from pquic_amd import Engine
+
     dist = None
     # rehearsal knobs for a box with fewer GPUs than ranks (never set by the driver):
     # PQUIC_BENCH_SHARE_GPU=1 maps rank -> device local % count, PQUIC_BENCH_BACKEND=gloo
@@ -439,16 +573,6 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
-    cfg = dict(CONFIGS[args.config])
-    if args.config == "k16":  # the legacy flags still shape the default workload
-        cfg.update(k=args.k, r=args.r, e=args.erasures, L=args.symbol, per_rank=args.blocks)
-    k, r, e, L = cfg["k"], cfg["r"], cfg["e"], cfg["L"]
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "k16":
-        # before any HIP call: the reference's workers are fork()ed from this process
-        ncores, aff, quota = host_cpu_share()
-        cpu = cpu_baseline(args, ncores)
-        cpu["host"] = {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     eng = Engine(local)
@@ -525,7 +649,7 @@ def main():
     seg = [sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / args.steps for i in range(3)]
     enc_ms, plan_ms, apply_ms = seg  # first pass of a step; apply includes the zero/undetermined rule
     dec_ms = plan_ms + apply_ms
-    per_rank = None
+    per_rank = rank_devices = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -534,6 +658,10 @@ def main():
         allr = [torch.zeros_like(tr) for _ in range(world)]
         dist.all_gather(allr, tr)
         per_rank = [round(float(x.item()) / args.steps * 1e3, 3) for x in allr]
+        dv = torch.tensor([float(local)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        alld = [torch.zeros_like(dv) for _ in range(world)]
+        dist.all_gather(alld, dv)
+        rank_devices = [int(x.item()) for x in alld]
 
     total_blocks = world * share if cfg["scaling"] == "weak" else cfg["total"]
     value = total_blocks * k * L * args.steps / elapsed / 2**30
@@ -666,6 +794,8 @@ def main():
                "config": conf, "roofline": roof, "cpu_baseline": cpu, "legs": legs}
         if per_rank:
             out["per_rank_ms_per_step"] = per_rank
+            out["per_rank_device"] = rank_devices
+            out["launcher"] = "bench.py child processes" if os.environ.get("PQUIC_BENCH_LAUNCHED") else "torchrun"
         print(json.dumps(out))
     if dist:
         dist.barrier()

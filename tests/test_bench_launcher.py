@@ -1,0 +1,60 @@
+"""bench.py's multi-GPU launch paths, without a GPU (CPU suite).
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment must drive N ranks itself: the
+parent measures cpu_baseline (the reference pluglets on the host cores) and starts N child
+processes, never touching a GPU; rank 0's line carries n_gpus == N, the baseline and every rank's
+step time.  --dry-run swaps the device work for an empty timed region on gloo, so the launcher,
+rendezvous, max-over-ranks reduction and baseline hand-off run here.  A WORLD_SIZE that disagrees
+with --gpus is refused."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+ORACLE = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.skipif(not os.path.exists(ORACLE), reason="oracle not built (make -C oracle)")
+@pytest.mark.parametrize("config", ["k16", "k32r8"])
+def test_spawn_path_two_ranks(config):
+    p = _run(["--gpus", "2", "--config", config, "--dry-run", "--steps", "2", "--warmup", "1",
+              "--cpu-blocks", "64", "--cpu-seconds", "0.5"], {"PQUIC_BENCH_SHARE_GPU": "1"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    assert d["n_gpus"] == 2 and d["dry_run"] is True
+    assert len(d["per_rank_ms_per_step"]) == 2
+    cpu = d["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
+    if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libfecref.so")):
+        assert cpu["kind"] == "reference"
+        assert ("decode" in cpu["sample"]) == (config == "k16")
+
+
+def test_world_size_must_match_gpus():
+    p = _run(["--gpus", "4", "--dry-run", "--no-cpu"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert p.returncode == 2
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_single_gpu_dry_run_line():
+    p = _run(["--gpus", "1", "--dry-run", "--no-cpu"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _line(p.stdout)
+    assert d["n_gpus"] == 1 and d["cpu_baseline"] is None
