@@ -180,6 +180,14 @@ int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, ui
  * C need no HIP headers.  NULL on failure. */
 void *fecgpu_host_alloc(size_t bytes);
 void fecgpu_host_free(void *p);
+/* Page-lock and map an existing host range (hipHostRegister, mapped) so the kernels read and write
+ * it in place -- e.g. a FEC plugin instance's memory arena (picoquic_internal.h:576, char
+ * memory[PLUGIN_MEMORY], carved into 2100-B slots by picoquic/memory.c:181-191), which holds every
+ * symbol the framework hands over.  Unregister before the range is freed.  fecgpu_host_device_address
+ * gives the device address of [p, p + bytes) when all of it lies in page-locked memory. */
+int fecgpu_host_register(void *p, size_t bytes);
+int fecgpu_host_unregister(void *p);
+int fecgpu_host_device_address(const void *p, size_t bytes, uint64_t *dev);
 
 /* Synthetic payload generator (bench/tests): byte o of dst = byte (o mod 8) of
  * splitmix64(seed + (o/8 + 1) * 0x9e3779b97f4a7c15), o counted from `offset`. */
@@ -187,16 +195,15 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
 
 /* Experiment knobs (A/B runs, cross-checks of alternative kernels in the tests).  Every knob has
  * a measured default; the environment variable named in DESIGN.md §6.1 seeds it ONCE per process
- * (first engine call), after which only these calls change it.  Names: "datapath_perm" (0/1),
- * "plan" (0 auto, 1 wave in LDS, 2 lane, 3 reg, 4 tile, 5 wave in registers where it fits), "interleave" (0/1), "group" (0 = defaults, else
- * a cap on blocks per group), "enc_tile_rt" / "enc_tile_waves" (0 = default tiling), "xor_generic",
- * "xor_idx64", "zc_read" (0/1), "ring" (the LDS-ring data path: 0 never, 1 wherever it applies,
- * 2 = default, 16-repair encode and 16-unknown decode tiles), "window_sc" (window encode on the
+ * (first engine call), after which only these calls change it.  Names and accepted values:
+ * "plan" (0 auto, 1 wave in LDS, 2 lane, 3 reg, 4 tile, 5 wave in registers where it fits),
+ * "interleave" (0/1), "group" (0 = defaults, else a cap on blocks per group), "enc_tile_rt" (0 =
+ * default tiling, else 1/2/4/8/16) / "enc_tile_waves" (0..4), "zc_read" (0/1), "ring" (the LDS-ring
+ * data path of 16-repair / 16-unknown tiles: 2 = default, 0 off), "window_sc" (window encode on the
  * shared-coefficient kernel: 0 never, 1 = default for overlapping windows, 2 wherever it applies),
- * "small_plan" (one-launch decode of <= 64 blocks: 0 = default, the wave plan; 1 the lane-register
- * plan when k <= 32 and e <= 8), "min_groups" (batches with fewer block groups than this stream fewer
- * blocks per wave; default 1024, 0 = the per-shape group sizes at any batch size).  Returns FECGPU_OK or
- * FECGPU_ERR_INVALID for an unknown name. */
+ * "min_groups" (batches with fewer block groups than this stream fewer blocks per wave; default
+ * 1024, 0 = the per-shape group sizes at any batch size).  Returns FECGPU_OK, or FECGPU_ERR_INVALID
+ * for an unknown name or a value outside its range. */
 int fecgpu_set_knob(const char *name, int value);
 int fecgpu_get_knob(const char *name, int *value);
 
@@ -205,6 +212,9 @@ int fecgpu_get_knob(const char *name, int *value);
 typedef struct {
     uint64_t encode_calls, encode_blocks;
     uint64_t decode_calls, decode_blocks;
+    /* host path: page-locked buffers found in the library's registry of its own fecgpu_host_alloc /
+     * fecgpu_host_register ranges, and those that needed a hipPointerGetAttributes query instead */
+    uint64_t pinned_registry_hits, pinned_registry_misses;
 } fecgpu_stats_t;
 void fecgpu_get_stats(fecgpu_stats_t *out);
 

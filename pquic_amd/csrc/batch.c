@@ -93,10 +93,10 @@ static void job_free(job_t *j) {
 /* A job for (op, scheme, k, r), from the free list when one is big enough. */
 static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
     const uint32_t cap = b->cfg.batch_blocks, S = b->stride;
-    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S, eb = (size_t)cap * (r ? r : 1) * 4;
+    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
     job_t **pp = &b->free_jobs;
     for (; *pp; pp = &(*pp)->next)
-        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb && (*pp)->seed_bytes >= eb) break;
+        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb) break;
     job_t *j = *pp;
     if (j) {
         *pp = j->next;
@@ -105,18 +105,28 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         if (!j) return NULL;
         j->src_bytes = sb;
         j->rep_bytes = rb;
-        j->seed_bytes = eb;
-        j->seeds = fecgpu_host_alloc(eb);
         j->src = fecgpu_host_alloc(sb);
         j->rep = fecgpu_host_alloc(rb ? rb : 4);
         j->st = fecgpu_host_alloc(cap);
         j->fbn = fecgpu_host_alloc((size_t)cap * 4);
         j->sp = fecgpu_host_alloc((size_t)cap * 48);  /* sp | rp | rec, 2 words each per block */
         j->ent = calloc(cap, sizeof *j->ent);
-        if (!j->src || !j->rep || !j->st || !j->fbn || !j->seeds || !j->sp || !j->ent) {
+        if (!j->src || !j->rep || !j->st || !j->fbn || !j->sp || !j->ent) {
             job_free(j);
             return NULL;
         }
+    }
+    /* recover only: the repairs' FPID seeds, [cap][r] (grown on reuse like the repair table) */
+    const size_t eb = (size_t)cap * (r ? r : 1) * 4;
+    if (op == OP_RECOVER && j->seed_bytes < eb) {
+        fecgpu_host_free(j->seeds);
+        j->seed_bytes = 0;
+        if (!(j->seeds = fecgpu_host_alloc(eb))) {
+            j->next = b->free_jobs;
+            b->free_jobs = j;
+            return NULL;
+        }
+        j->seed_bytes = eb;
     }
     if (op == OP_GENERATE && j->reps_cap < (size_t)cap * r) {
         pquic_repair_symbol_t **nr = realloc(j->reps, sizeof *nr * (size_t)cap * r);

@@ -47,11 +47,10 @@ static std::atomic<uint64_t> g_stats[4];
 // measured best.  They are read from the environment ONCE, on first use, so the engine's behaviour
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
-enum KnobId { K_PERM, K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_XOR_GENERIC, K_XOR_IDX64, K_ZC_READ,
-              K_RING, K_WINDOW_SC, K_SMALL_PLAN, K_MIN_GROUPS, K_N };
-static const char *const kKnobName[K_N] = {"datapath_perm", "plan", "interleave", "group", "enc_tile_rt",
-                                           "enc_tile_waves", "xor_generic", "xor_idx64", "zc_read", "ring",
-                                           "window_sc", "small_plan", "min_groups"};
+enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
+              K_N };
+static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
+                                           "zc_read", "ring", "window_sc", "min_groups"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -59,7 +58,6 @@ static std::once_flag g_knob_once;
 static void knobs_from_env() {
   auto num = [](const char *v, int def) { return v ? atoi(v) : def; };
   const char *e;
-  g_knob[K_PERM] = (e = getenv("FECGPU_DATAPATH")) && !strcmp(e, "perm");
   e = getenv("FECGPU_PLAN");
   g_knob[K_PLAN] = !e ? PLAN_AUTO : !strcmp(e, "wave") ? PLAN_WAVE : !strcmp(e, "lane") ? PLAN_LANE
                  : !strcmp(e, "reg") ? PLAN_REG : !strcmp(e, "tile") ? PLAN_TILE
@@ -72,17 +70,12 @@ static void knobs_from_env() {
     g_knob[K_ENC_RT] = a;
     g_knob[K_ENC_W] = b;
   }
-  g_knob[K_XOR_GENERIC] = num(getenv("FECGPU_XOR_GENERIC"), 0) != 0;
-  g_knob[K_XOR_IDX64] = num(getenv("FECGPU_XOR_IDX64"), 0) != 0;
   g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
-  // LDS-ring data path (bs2 bodies): 0 never, 1 wherever it applies, 2 (default) 16-repair tiles
-  g_knob[K_RING] = num(getenv("FECGPU_RING"), 2);
+  // LDS-ring data path (bs2 bodies) for 16-repair / 16-unknown tiles: 2 (default) on, 0 off
+  g_knob[K_RING] = num(getenv("FECGPU_RING"), 2) ? 2 : 0;
   // window encode on the shared-coefficient kernel (k_rlc_encode_sc): 0 never, 1 (default) for
   // overlapping windows, 2 wherever it applies (tests)
   g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1);
-  // one-launch decode of a few blocks: 0 (default) the wave plan, 1 the lane-register plan when k <= 32
-  // and e <= 8 (one-block recover hook p50 53 us against 37: its single lane's dependent chain is long)
-  g_knob[K_SMALL_PLAN] = num(getenv("FECGPU_SMALL_PLAN"), 0);
   // batches too small to fill the chip stream fewer blocks per wave: groups of blocks shrink until
   // there are at least this many groups (0: the per-shape group sizes at every batch size)
   g_knob[K_MIN_GROUPS] = num(getenv("FECGPU_MIN_GROUPS"), 1024);
@@ -146,135 +139,6 @@ __device__ __forceinline__ uint32_t repair_seed(const uint32_t *seeds, uint64_t 
 }
 
 static uint32_t grid_for(uint64_t units);
-
-constexpr int KT = 16;  // sources per LDS table stage
-
-// LDS carve for the data kernels: coefficient bytes [RT][kpad] then tables [KT][RT].
-template <int RT>
-struct DataLds {
-  static __device__ __forceinline__ uint8_t *coef(uint8_t *lds) { return lds; }
-  static __device__ __forceinline__ uint4 *t01(uint8_t *lds, int kpad) {
-    return reinterpret_cast<uint4 *>(lds + pad16(RT * kpad));
-  }
-  static __device__ __forceinline__ uint32_t *t2(uint8_t *lds, int kpad) {
-    return reinterpret_cast<uint32_t *>(lds + pad16(RT * kpad) + KT * RT * 16);
-  }
-  static __host__ __device__ size_t bytes(int k) {
-    int kpad = (int)pad16((uint32_t)k);
-    return pad16(RT * kpad) + KT * RT * 20;
-  }
-};
-
-// Build perm tables for sources [jt, jt+KT) from the coefficient bytes in LDS.
-template <int RT>
-__device__ __forceinline__ void stage_tables(uint8_t *lds, int kpad, int k, int jt, int lane) {
-  uint8_t *coef = DataLds<RT>::coef(lds);
-  uint4 *t01 = DataLds<RT>::t01(lds, kpad);
-  uint32_t *t2 = DataLds<RT>::t2(lds, kpad);
-  for (int e = lane; e < KT * RT; e += 64) {
-    int jj = e / RT, i = e % RT;
-    int j = jt + jj;
-    uint32_t c = j < k ? coef[i * kpad + j] : 0u;
-    PermTab t = perm_table(c);
-    t01[e] = t.t01;
-    t2[e] = t.t2;
-  }
-}
-
-// The multiply-accumulate sweep shared by encode and recover: acc[i][w] += coef(i, j) * in_j.
-// in_ptr(j) returns the dword row of input j (already offset to this chunk).
-template <int RT, int W, typename InPtr>
-__device__ __forceinline__ void mac_sweep(uint8_t *lds, int kpad, int k, int rt, int cn, int lane,
-                                          InPtr in_ptr, uint32_t (&acc)[RT][W]) {
-  uint4 *t01 = DataLds<RT>::t01(lds, kpad);
-  uint32_t *t2 = DataLds<RT>::t2(lds, kpad);
-  uint32_t nxt[W];
-  {
-    const uint32_t *p = in_ptr(0);
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      int idx = lane + 64 * w;
-      nxt[w] = idx < cn ? __builtin_nontemporal_load(p + idx) : 0u;
-    }
-  }
-  for (int jt = 0; jt < k; jt += KT) {
-    __syncthreads();
-    stage_tables<RT>(lds, kpad, k, jt, lane);
-    __syncthreads();
-    int jn = k - jt < KT ? k - jt : KT;
-    for (int jj = 0; jj < jn; jj++) {
-      int j = jt + jj;
-      Sel sel[W];
-#pragma unroll
-      for (int w = 0; w < W; w++) sel[w] = perm_selectors(nxt[w]);
-      if (j + 1 < k) {
-        const uint32_t *p = in_ptr(j + 1);
-#pragma unroll
-        for (int w = 0; w < W; w++) {
-          int idx = lane + 64 * w;
-          nxt[w] = idx < cn ? __builtin_nontemporal_load(p + idx) : 0u;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < RT; i++) {
-        if (i < rt) {
-          uint4 ta = t01[jj * RT + i];
-          uint32_t tb = t2[jj * RT + i];
-#pragma unroll
-          for (int w = 0; w < W; w++) acc[i][w] = gf_mac(acc[i][w], sel[w], ta, tb);
-        }
-      }
-    }
-  }
-}
-
-// =============================================================================================
-// RLC encode
-// =============================================================================================
-template <int RT, int W>
-__global__ __launch_bounds__(64) void k_rlc_encode(const uint32_t *__restrict__ src,
-                                                   uint32_t *__restrict__ rep, uint64_t nblocks,
-                                                   int k, int r, int Ldw, int nchunks, int chunk_dw,
-                                                   uint32_t fbn_base, const uint32_t *fbn, int r0) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
-  const int kpad = (int)pad16((uint32_t)k);
-  const int rt = r - r0 < RT ? r - r0 : RT;
-  const uint64_t units = nblocks * (uint64_t)nchunks;
-  for (uint64_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
-    const uint64_t b = unit / (uint64_t)nchunks;
-    const int ch = (int)(unit - b * (uint64_t)nchunks);
-    const uint32_t f = block_fbn(b, fbn_base, fbn);
-    __syncthreads();
-    if (lane < rt) {
-      Tmt t;
-      tmt_init(t, rlc_seed(f, (uint32_t)(r0 + lane)));
-      uint8_t *coef = DataLds<RT>::coef(lds) + lane * kpad;
-      for (int j = 0; j < k; j++) coef[j] = tmt_coef(t);
-    }
-    const int c0 = ch * chunk_dw;
-    const int cn = Ldw - c0 < chunk_dw ? Ldw - c0 : chunk_dw;
-    uint32_t acc[RT][W];
-#pragma unroll
-    for (int i = 0; i < RT; i++)
-#pragma unroll
-      for (int w = 0; w < W; w++) acc[i][w] = 0;
-    const uint32_t *sb = src + (b * (uint64_t)k) * (uint64_t)Ldw + c0;
-    auto in_ptr = [&](int j) { return sb + (uint64_t)j * Ldw; };
-    mac_sweep<RT, W>(lds, kpad, k, rt, cn, lane, in_ptr, acc);
-    uint32_t *rb = rep + (b * (uint64_t)r + r0) * (uint64_t)Ldw + c0;
-#pragma unroll
-    for (int i = 0; i < RT; i++) {
-      if (i < rt) {
-#pragma unroll
-        for (int w = 0; w < W; w++) {
-          int idx = lane + 64 * w;
-          if (idx < cn) __builtin_nontemporal_store(acc[i][w], rb + (uint64_t)i * Ldw + idx);
-        }
-      }
-    }
-  }
-}
 
 // =============================================================================================
 // RLC decode: plan (coefficients only), recover (data), finalize (zero propagation)
@@ -1266,59 +1130,6 @@ __global__ __launch_bounds__(64) void k_rlc_plan_tile(uint64_t nblocks, int k, i
   }
 }
 
-template <int RT, int W>
-__global__ __launch_bounds__(64) void k_rlc_recover(uint32_t *__restrict__ src,
-                                                    const uint32_t *__restrict__ rep, uint64_t nblocks,
-                                                    int k, int r, int Ldw, int nchunks, int chunk_dw,
-                                                    uint8_t *ws, int r0, uint32_t *dst) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const WsLayout L = ws_layout((uint32_t)k, (uint32_t)r);
-  const int lane = threadIdx.x;
-  const int kpad = (int)pad16((uint32_t)k);
-  const uint64_t units = nblocks * (uint64_t)nchunks;
-  for (uint64_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
-    const uint64_t b = unit / (uint64_t)nchunks;
-    const int ch = (int)(unit - b * (uint64_t)nchunks);
-    uint8_t *h = ws + b * (uint64_t)L.stride;
-    const int status = h[0], e = h[1];
-    if (status != FECGPU_BLOCK_RECOVERED || e <= r0) continue;  // uniform per wave
-    const int rt = e - r0 < RT ? e - r0 : RT;
-    __syncthreads();
-    for (int x = lane; x < RT * kpad; x += 64) {
-      int i = x / kpad, j = x - i * kpad;
-      DataLds<RT>::coef(lds)[x] = (i < rt && j < k) ? h[L.off_D + (r0 + i) * k + j] : 0;
-    }
-    const int c0 = ch * chunk_dw;
-    const int cn = Ldw - c0 < chunk_dw ? Ldw - c0 : chunk_dw;
-    uint32_t acc[RT][W];
-#pragma unroll
-    for (int i = 0; i < RT; i++)
-#pragma unroll
-      for (int w = 0; w < W; w++) acc[i][w] = 0;
-    const uint8_t *slot = h + L.off_slot;
-    auto in_ptr = [&](int j) {
-      uint32_t s = slot[j];
-      const uint32_t *base = (s & 0x80) ? rep + (b * (uint64_t)r + (s & 0x7f)) * (uint64_t)Ldw
-                                        : src + (b * (uint64_t)k + s) * (uint64_t)Ldw;
-      return base + c0;
-    };
-    mac_sweep<RT, W>(lds, kpad, k, rt, cn, lane, in_ptr, acc);
-#pragma unroll
-    for (int i = 0; i < RT; i++) {
-      if (i < rt) {
-        uint32_t *ob = dst + (b * (uint64_t)k + h[L.off_unk + r0 + i]) * (uint64_t)Ldw + c0;
-        uint32_t any = 0;
-#pragma unroll
-        for (int w = 0; w < W; w++) {
-          int idx = lane + 64 * w;
-          if (idx < cn) { ob[idx] = acc[i][w]; any |= acc[i][w]; }
-        }
-        if (__any(any != 0) && lane == 0) h[L.off_nz + r0 + i] = 1;  // idempotent across chunks
-      }
-    }
-  }
-}
-
 // per-block decode record in LDS (layout shared with gen_bitslice.py): 16 output addresses |
 // ws non-zero-flag address @128 | rt @136 | non-zero flags @144 (written by the asm body)
 constexpr int kDecRec = 160, kDecRecNzPtr = 16, kDecRecRt = 34, kDecRecNz = 144;
@@ -1714,7 +1525,7 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
 // plan's record stays in LDS (past both phases' scratch, at rec_off): both phases address a record
 // as ws + b * stride, so they get a base that puts block b's record there, and no global round trip
 // or fence sits between the plan and the data pass.
-template <int RT, int VEC, bool PLANREG>
+template <int RT, int VEC>
 __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                          uint64_t nblocks, int k, int r, int L, int nchunks,
                                                          int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
@@ -1727,12 +1538,7 @@ __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ s
     uint8_t *wsx = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(lds + rec_off) - b * stride);
     __syncthreads();
     plan_load_tables(lds);
-    if constexpr (PLANREG) {  // k <= 32, e <= 8: lane 0 holds the whole system (k_rlc_plan_reg's replay)
-      __syncthreads();
-      if (threadIdx.x == 0) plan_reg_block<8, 8>(b, k, r, fbn_base, fbn, seeds, sp, rp, lds + rec_off, lds, lds + 512);
-    } else {
-      plan_wave_any(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
-    }
+    plan_wave_any(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
     __syncthreads();
     recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, wsx, 0, 1, status,
                               recovered, 0, dst, lds);
@@ -1886,11 +1692,8 @@ static bool launch_encode_sc(const uint8_t *sym, uint8_t *rep, uint64_t nwin, in
 // ---------------------------------------------------------------------------------------------
 #define FEC_BS2_D(MODE, RT) FEC_BS2_D_##MODE##_RT##RT
 
-template <int RT> struct Bs2Depth;
-#define FEC_BS2_DEPTH(RT) \
-  template <> struct Bs2Depth<RT> { static constexpr int enc = FEC_BS2_D(ENC, RT), dec = FEC_BS2_D(DEC, RT); };
-FEC_BS2_DEPTH(1) FEC_BS2_DEPTH(2) FEC_BS2_DEPTH(4) FEC_BS2_DEPTH(8) FEC_BS2_DEPTH(16)
-#undef FEC_BS2_DEPTH
+// ring depths (sources in flight + 1) of the shipped ring bodies: 16-repair / 16-unknown tiles
+struct Bs2Depth16 { static constexpr int enc = FEC_BS2_D(ENC, 16), dec = FEC_BS2_D(DEC, 16); };
 
 // Lane geometry of one chunk of cb bytes (cb >= 16) as 16-B pieces, the last pulled back to end at cb.
 // DMA: instruction 1 moves pieces 0..63 (lane = piece), instruction 2 pieces 64.. (lane = piece - 64);
@@ -1930,33 +1733,15 @@ static inline uint32_t bs2_slot_bytes(int) { return FEC_BS2_SLOT; }  // the bodi
 #define BS2_CALL_DEC(RT, ND) \
   bs2_dec_r##RT##_d##ND(ia, oa, nsrc, (uint32_t)k, ca, ring, BS2_LANE_ARGS)
 
-template <int RT>
 __device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp, int L, uint32_t rslo, uint32_t rshi,
                                              uint64_t sdl, uint64_t ll, int rt, uint32_t nsrc, int k, uint32_t ca,
                                              uint32_t ring, const Bs2Lanes &ln) {
-  if (two) {
-    if constexpr (RT == 1) BS2_CALL_ENC(1, 2); else if constexpr (RT == 2) BS2_CALL_ENC(2, 2);
-    else if constexpr (RT == 4) BS2_CALL_ENC(4, 2); else if constexpr (RT == 8) BS2_CALL_ENC(8, 2);
-    else BS2_CALL_ENC(16, 2);
-  } else {
-    if constexpr (RT == 1) BS2_CALL_ENC(1, 1); else if constexpr (RT == 2) BS2_CALL_ENC(2, 1);
-    else if constexpr (RT == 4) BS2_CALL_ENC(4, 1); else if constexpr (RT == 8) BS2_CALL_ENC(8, 1);
-    else BS2_CALL_ENC(16, 1);
-  }
+  if (two) BS2_CALL_ENC(16, 2); else BS2_CALL_ENC(16, 1);
 }
 
-template <int RT>
 __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa, uint32_t nsrc, int k, uint32_t ca,
                                              uint32_t ring, const Bs2Lanes &ln) {
-  if (two) {
-    if constexpr (RT == 1) BS2_CALL_DEC(1, 2); else if constexpr (RT == 2) BS2_CALL_DEC(2, 2);
-    else if constexpr (RT == 4) BS2_CALL_DEC(4, 2); else if constexpr (RT == 8) BS2_CALL_DEC(8, 2);
-    else BS2_CALL_DEC(16, 2);
-  } else {
-    if constexpr (RT == 1) BS2_CALL_DEC(1, 1); else if constexpr (RT == 2) BS2_CALL_DEC(2, 1);
-    else if constexpr (RT == 4) BS2_CALL_DEC(4, 1); else if constexpr (RT == 8) BS2_CALL_DEC(8, 1);
-    else BS2_CALL_DEC(16, 1);
-  }
+  if (two) BS2_CALL_DEC(16, 2); else BS2_CALL_DEC(16, 1);
 }
 
 // W waves per workgroup split a group's repairs (wave w: repairs r0 + w RT ..), each with its own
@@ -1976,7 +1761,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
-  constexpr int D = Bs2Depth<RT>::enc;
+  constexpr int D = Bs2Depth16::enc;
   const uint32_t per_wave = pad16((uint32_t)(G * k * CSB)) + D * slotb;
   uint8_t *lds = lds_all + (size_t)wave * per_wave;
   const uint32_t ring = lds_addr(lds) + pad16((uint32_t)(G * k * CSB));
@@ -2020,7 +1805,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
       const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;
       const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
       const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
-      bs2_enc_call<RT>(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
+      bs2_enc_call(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
                        ln);
     }
   }
@@ -2104,7 +1889,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
         const Bs2Lanes ln(lane, cb, (uint32_t)c0, ring);
-        bs2_dec_call<RT>(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
+        bs2_dec_call(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
                          lds_addr(S.coef), ring, ln);
       }
     }
@@ -2162,7 +1947,7 @@ static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int
                               uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                               hipStream_t s) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
-  const size_t ring_bytes = (size_t)Bs2Depth<RT>::enc * slotb;
+  const size_t ring_bytes = (size_t)Bs2Depth16::enc * slotb;
   const int G = sbs == (uint64_t)k * L
                     ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT),
                                 nb)
@@ -2178,7 +1963,7 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
                                uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                                uint8_t *dst) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
-  const size_t ring_bytes = (size_t)Bs2Depth<RT>::dec * slotb;
+  const size_t ring_bytes = (size_t)Bs2Depth16::dec * slotb;
   const int G = bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, ring_bytes,
                           bs2_waves_per_cu(RT), nb);
   const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + ring_bytes;
@@ -2187,29 +1972,15 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
                      c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, slotb);
 }
 
-// The ring path applies to 16-B pieces (symbol_size >= 16) and blocks of at least D sources (one
-// epilogue in any wait window, see gen_bitslice.py body2).
-static int bs2_depth(int RT, bool enc) {
-  switch (RT) {
-    case 1: return enc ? Bs2Depth<1>::enc : Bs2Depth<1>::dec;
-    case 2: return enc ? Bs2Depth<2>::enc : Bs2Depth<2>::dec;
-    case 4: return enc ? Bs2Depth<4>::enc : Bs2Depth<4>::dec;
-    case 8: return enc ? Bs2Depth<8>::enc : Bs2Depth<8>::dec;
-    default: return enc ? Bs2Depth<16>::enc : Bs2Depth<16>::dec;
-  }
-}
+// The ring path applies to 16-repair / 16-unknown tiles of 16-B pieces (symbol_size >= 16) and blocks
+// of at least D sources (one epilogue in any wait window, see gen_bitslice.py body2); knob ring = 0
+// keeps those tiles on the register-prefetch body (A/B).
 static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
-  const int m = knob(K_RING);
-  if (m == 0 || cfg.vec != 16 || (int)k < bs2_depth(rt, enc)) return false;
-  return m == 1 || rt == 16;
+  if (knob(K_RING) == 0 || rt != 16 || cfg.vec != 16) return false;
+  return (int)k >= (enc ? Bs2Depth16::enc : Bs2Depth16::dec);
 }
 
-#define FEC_BS2_DISPATCH(FN, ...)                                                               \
-  switch (rt) {                                                                                \
-    case 1: FN<1>(__VA_ARGS__); break;  case 2: FN<2>(__VA_ARGS__); break;                    \
-    case 4: FN<4>(__VA_ARGS__); break;  case 8: FN<8>(__VA_ARGS__); break;                    \
-    default: FN<16>(__VA_ARGS__); break;                                                       \
-  }
+#define FEC_BS2_DISPATCH(FN, ...) FN<16>(__VA_ARGS__);
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
   switch (rt * 100 + cfg.vec) {                                                    \
@@ -2249,8 +2020,6 @@ static int bs_table_check() {
   if (st < 0) return set_err(FECGPU_ERR_HIP, "%s", "GF(256) case table is not 64 KiB-aligned in device memory");
   return FECGPU_OK;
 }
-
-static bool use_perm_path() { return knob(K_PERM) != 0; }  // the v_perm data path (A/B, tests)
 
 // =============================================================================================
 // XOR scheme
@@ -2351,14 +2120,11 @@ static void xor_dispatch_k(uint32_t k, uint32_t grid, hipStream_t s, A... a) {
     default: OP::template go<V, 0, I>(grid, s, a...); break;
   }
 }
-template <typename V, typename OP, typename... A>
-static void xor_dispatch(uint32_t k, uint64_t total, uint32_t grid, hipStream_t s, A... a) {
-  if (knob(K_XOR_GENERIC)) return xor_dispatch_k<V, OP, uint64_t>(0, grid, s, a...);  // A/B: runtime k, 64-bit index
-  // knob xor_idx64 (tests): the 64-bit-index instantiations at small sizes
-  if (total < (1ull << 32) - (uint64_t)grid * 256 && !knob(K_XOR_IDX64))
-    xor_dispatch_k<V, OP, uint32_t>(k, grid, s, a...);
-  else
-    xor_dispatch_k<V, OP, uint64_t>(k, grid, s, a...);
+// 32-bit element indices: a batch with more index positions than that runs as several launches
+// (xor_sub_batch), so one instantiation per (vector width, k) serves every size.
+static uint64_t xor_sub_batch(uint64_t nblocks, int Lv, uint32_t grid) {
+  const uint64_t lim = ((1ull << 32) - 1 - (uint64_t)grid * 256) / (uint64_t)Lv;
+  return nblocks < lim ? nblocks : lim;
 }
 
 // FEC frames for batched repair symbols (the block framework's get_repair_payload_from_queue +
@@ -2492,67 +2258,12 @@ __global__ void k_synth_fill(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint6
 // =============================================================================================
 // Launch configuration
 // =============================================================================================
-struct DataCfg { int W, nchunks, chunk_dw; };
-
-// Choose lane words W (1..8) and the column chunking that wastes the fewest lane slots.
-static DataCfg pick_data_cfg(int Ldw) {
-  DataCfg best{1, 1, 64};
-  double best_eff = -1;
-  for (int W = 8; W >= 1; W--) {
-    int nch = (Ldw + 64 * W - 1) / (64 * W);
-    int chunk = (Ldw + nch - 1) / nch;
-    int wneed = (chunk + 63) / 64;
-    double eff = (double)Ldw / ((double)nch * 64.0 * wneed);
-    // prefer fewer chunks (fewer coefficient regenerations) at equal efficiency
-    if (eff > best_eff + 1e-9) { best_eff = eff; best = DataCfg{wneed, nch, chunk}; }
-  }
-  return best;
-}
-
 static int pick_rt(uint32_t r) { return r >= 16 ? 16 : r >= 8 ? 8 : r >= 4 ? 4 : r >= 2 ? 2 : 1; }
 
 static uint32_t grid_for(uint64_t units) {
   const uint64_t cap = 1u << 22;
   return (uint32_t)(units < cap ? (units ? units : 1) : cap);
 }
-
-template <int RT, int W>
-static void launch_encode(const uint32_t *src, uint32_t *rep, uint64_t nb, int k, int r, int Ldw,
-                          const DataCfg &c, uint32_t fbn_base, const uint32_t *fbn, int r0,
-                          hipStream_t s) {
-  size_t lds = DataLds<RT>::bytes(k);
-  hipLaunchKernelGGL((k_rlc_encode<RT, W>), dim3(grid_for(nb * c.nchunks)), dim3(64), lds, s, src, rep,
-                     nb, k, r, Ldw, c.nchunks, c.chunk_dw, fbn_base, fbn, r0);
-}
-
-template <int RT, int W>
-static void launch_recover(uint32_t *src, const uint32_t *rep, uint64_t nb, int k, int r, int Ldw,
-                           const DataCfg &c, uint8_t *ws, int r0, hipStream_t s, uint32_t *dst) {
-  size_t lds = DataLds<RT>::bytes(k);
-  hipLaunchKernelGGL((k_rlc_recover<RT, W>), dim3(grid_for(nb * c.nchunks)), dim3(64), lds, s, src,
-                     rep, nb, k, r, Ldw, c.nchunks, c.chunk_dw, ws, r0, dst);
-}
-
-#define FEC_DISPATCH_W(FN, RT, ...)                       \
-  switch (cfg.W) {                                        \
-    case 1: FN<RT, 1>(__VA_ARGS__); break;                \
-    case 2: FN<RT, 2>(__VA_ARGS__); break;                \
-    case 3: FN<RT, 3>(__VA_ARGS__); break;                \
-    case 4: FN<RT, 4>(__VA_ARGS__); break;                \
-    case 5: FN<RT, 5>(__VA_ARGS__); break;                \
-    case 6: FN<RT, 6>(__VA_ARGS__); break;                \
-    case 7: FN<RT, 7>(__VA_ARGS__); break;                \
-    default: FN<RT, 8>(__VA_ARGS__); break;               \
-  }
-
-#define FEC_DISPATCH_RT(FN, ...)                          \
-  switch (rt) {                                           \
-    case 1: FEC_DISPATCH_W(FN, 1, __VA_ARGS__) break;     \
-    case 2: FEC_DISPATCH_W(FN, 2, __VA_ARGS__) break;     \
-    case 4: FEC_DISPATCH_W(FN, 4, __VA_ARGS__) break;     \
-    case 8: FEC_DISPATCH_W(FN, 8, __VA_ARGS__) break;     \
-    default: FEC_DISPATCH_W(FN, 16, __VA_ARGS__) break;   \
-  }
 
 static int check_common(const void *a, const void *b, uint64_t nblocks, uint32_t k, uint32_t r,
                         uint32_t L) {
@@ -2590,10 +2301,26 @@ int fecgpu_init(int device) {
   return rc;
 }
 
+// The values each knob accepts (the same ranges knobs_from_env admits): a tile of 3 repairs would
+// dispatch a 16-repair body while stepping r0 by 3, a negative group cap would become a huge
+// unsigned one.
+static bool knob_value_ok(int id, int v) {
+  switch (id) {
+    case K_PLAN: return v >= PLAN_AUTO && v <= PLAN_WREG;
+    case K_ENC_RT: return v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16;
+    case K_ENC_W: return v >= 0 && v <= 4;
+    case K_RING: return v == 0 || v == 2;
+    case K_WINDOW_SC: return v >= 0 && v <= 2;
+    case K_GROUP: case K_MIN_GROUPS: return v >= 0;
+    default: return v == 0 || v == 1;  // on / off knobs
+  }
+}
+
 int fecgpu_set_knob(const char *name, int value) {
   std::call_once(g_knob_once, knobs_from_env);
   for (int i = 0; i < K_N; i++)
     if (name && !strcmp(name, kKnobName[i])) {
+      if (!knob_value_ok(i, value)) return set_err(FECGPU_ERR_INVALID, "value out of range for knob %s", name);
       g_knob[i].store(value, std::memory_order_relaxed);
       return FECGPU_OK;
     }
@@ -2610,11 +2337,14 @@ int fecgpu_get_knob(const char *name, int *value) {
   return set_err(FECGPU_ERR_INVALID, "unknown knob %s", name ? name : "(null)");
 }
 
+void fecgpu_host_registry_stats(uint64_t *hits, uint64_t *misses);  // host_path.hip (library-internal)
+
 void fecgpu_get_stats(fecgpu_stats_t *out) {
   out->encode_calls = g_stats[0].load();
   out->encode_blocks = g_stats[1].load();
   out->decode_calls = g_stats[2].load();
   out->decode_blocks = g_stats[3].load();
+  fecgpu_host_registry_stats(&out->pinned_registry_hits, &out->pinned_registry_misses);
 }
 
 // Encode tiling: repairs per wave (RT) and waves per workgroup sharing the source stream.
@@ -2636,29 +2366,19 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   int rc = check_common(src, rep, nblocks, k, r, symbol_size);
   if (rc || nblocks == 0 || r == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
-  const int rt = pick_rt(r);
-  if (use_perm_path()) {
-    const int Ldw = (int)(symbol_size / 4);
-    const DataCfg cfg = pick_data_cfg(Ldw);
-    for (int r0 = 0; r0 < (int)r; r0 += rt) {
-      FEC_DISPATCH_RT(launch_encode, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                      cfg, fbn_base, fbn, r0, s)
+  if (int rc2 = bs_table_check()) return rc2;
+  const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+  const EncTile et = pick_enc_tile(r);
+  const int rt = et.rt;
+  if (use_ring(rt, k, cfg, true)) {
+    for (int r0 = 0; r0 < (int)r; r0 += rt * et.waves) {
+      FEC_BS2_DISPATCH(launch_encode_bs2, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
+                       (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
     }
   } else {
-    if (int rc2 = bs_table_check()) return rc2;
-    const BsCfg cfg = pick_bs_cfg((int)symbol_size);
-    const EncTile et = pick_enc_tile(r);
-    const int rt = et.rt;
-    if (use_ring(rt, k, cfg, true)) {
-      for (int r0 = 0; r0 < (int)r; r0 += rt * et.waves) {
-        FEC_BS2_DISPATCH(launch_encode_bs2, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                         (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
-      }
-    } else {
-      for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
-        FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
-                        (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
-      }
+    for (int r0 = 0; r0 < (int)r; r0 += et.rt * et.waves) {
+      FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
+                      (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
     }
   }
   HIPCHK(hipGetLastError());
@@ -2696,12 +2416,18 @@ int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   hipStream_t s = (hipStream_t)stream;
   const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0;
   const int Lv = (int)(v4 ? symbol_size / 16 : symbol_size / 4);
-  const uint64_t total = nblocks * (uint64_t)Lv;
-  const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
-  if (v4)
-    xor_dispatch<u32x4, XorEnc>(k, total, grid, s, (const u32x4 *)src, (u32x4 *)rep, nblocks, (int)k, Lv);
-  else
-    xor_dispatch<uint32_t, XorEnc>(k, total, grid, s, (const uint32_t *)src, (uint32_t *)rep, nblocks, (int)k, Lv);
+  const uint32_t gmax = 1u << 20;
+  for (uint64_t b0 = 0, n; b0 < nblocks; b0 += n) {
+    n = xor_sub_batch(nblocks - b0, Lv, gmax);
+    const uint64_t total = n * (uint64_t)Lv;
+    const uint32_t grid = (uint32_t)((total + 255) / 256 < gmax ? (total + 255) / 256 : gmax);
+    const uint64_t so = b0 * k * (uint64_t)Lv, ro = b0 * (uint64_t)Lv;  // in vectors
+    if (v4)
+      xor_dispatch_k<u32x4, XorEnc, uint32_t>(k, grid, s, (const u32x4 *)src + so, (u32x4 *)rep + ro, n, (int)k, Lv);
+    else
+      xor_dispatch_k<uint32_t, XorEnc, uint32_t>(k, grid, s, (const uint32_t *)src + so, (uint32_t *)rep + ro, n,
+                                                 (int)k, Lv);
+  }
   HIPCHK(hipGetLastError());
   g_stats[0]++;
   g_stats[1] += nblocks;
@@ -2858,16 +2584,6 @@ static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64
   // decode passes: the smallest tile covering e_max (one pass, finalize fused) up to 16 unknowns
   const int rt = L.em <= 1 ? 1 : L.em <= 2 ? 2 : L.em <= 4 ? 4 : L.em <= 8 ? 8 : 16;
   if (r == 0) return launch_finalize(nblocks, k, r, status, recovered, ws, s);
-  if (use_perm_path()) {
-    const int Ldw = (int)(symbol_size / 4);
-    const DataCfg cfg = pick_data_cfg(Ldw);
-    for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
-      FEC_DISPATCH_RT(launch_recover, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k, (int)r, Ldw,
-                      cfg, ws, r0, s, (uint32_t *)dst)
-    }
-    HIPCHK(hipGetLastError());
-    return launch_finalize(nblocks, k, r, status, recovered, ws, s);
-  }
   if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const bool fused = (int)L.em <= rt;  // one pass covers every unknown of every block
@@ -2911,15 +2627,7 @@ static void launch_decode_small(uint8_t *src, const uint8_t *rep, uint64_t nb, i
   const uint32_t rec_off = pad16((uint32_t)(pl > rl ? pl : rl));  // the plan record, past both phases' scratch
   (void)ws;  // the record never leaves the workgroup
   const size_t lds = rec_off + pad16(ws_layout((uint32_t)k, (uint32_t)r).stride);
-  if constexpr (RT <= 8) {
-    if (k <= 32 && knob(K_SMALL_PLAN) == 1) {  // the lane-register plan: its system fits one lane
-      hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, true>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k,
-                         r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered,
-                         dst, 0);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC, false>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k, r,
+  hipLaunchKernelGGL((k_rlc_decode_small<RT, VEC>), dim3((uint32_t)nb), dim3(64), lds, s, src, rep, nb, k, r,
                      L, c.nchunks, c.chunk_bytes, fbn_base, fbn, seeds, sp, rp, rec_off, status, recovered, dst,
                      knob(K_PLAN) != PLAN_WAVE);
 }
@@ -2943,7 +2651,7 @@ static int decode_impl(const void *src, const void *rep, void *dst, uint64_t nbl
   const WsLayout WL = ws_layout(k, r);
   // the one-launch path: a few blocks, one data pass (e <= 16), the default kernels (no knob forces a
   // plan kernel or another data path)
-  if (nblocks <= kDecodeSmallMaxBlocks && r > 0 && WL.em <= 16 && knob(K_PLAN) == 0 && !use_perm_path() &&
+  if (nblocks <= kDecodeSmallMaxBlocks && r > 0 && WL.em <= 16 && knob(K_PLAN) == 0 &&
       plan_lds_bytes(k, r) <= 65536) {
     const BsCfg cfg = pick_bs_cfg((int)L);
     const int rt = WL.em <= 1 ? 1 : WL.em <= 2 ? 2 : WL.em <= 4 ? 4 : WL.em <= 8 ? 8 : 16;
@@ -2998,14 +2706,21 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
   hipStream_t s = (hipStream_t)stream;
   const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0;
   const int Lv = (int)(v4 ? symbol_size / 16 : symbol_size / 4);
-  const uint64_t total = nblocks * (uint64_t)Lv;
-  const uint32_t grid = (uint32_t)((total + 255) / 256 < (1u << 20) ? (total + 255) / 256 : (1u << 20));
-  if (v4)
-    xor_dispatch<u32x4, XorDec>(k, total, grid, s, (u32x4 *)src, (const u32x4 *)rep, nblocks, (int)k, Lv,
-                                src_present, rep_present, status, recovered);
-  else
-    xor_dispatch<uint32_t, XorDec>(k, total, grid, s, (uint32_t *)src, (const uint32_t *)rep, nblocks, (int)k,
-                                   Lv, src_present, rep_present, status, recovered);
+  const uint32_t gmax = 1u << 20;
+  for (uint64_t b0 = 0, n; b0 < nblocks; b0 += n) {
+    n = xor_sub_batch(nblocks - b0, Lv, gmax);
+    const uint64_t total = n * (uint64_t)Lv;
+    const uint32_t grid = (uint32_t)((total + 255) / 256 < gmax ? (total + 255) / 256 : gmax);
+    const uint64_t so = b0 * k * (uint64_t)Lv, ro = b0 * (uint64_t)Lv;  // in vectors
+    if (v4)
+      xor_dispatch_k<u32x4, XorDec, uint32_t>(k, grid, s, (u32x4 *)src + so, (const u32x4 *)rep + ro, n, (int)k, Lv,
+                                              src_present + 2 * b0, rep_present + 2 * b0, status + b0,
+                                              recovered + 2 * b0);
+    else
+      xor_dispatch_k<uint32_t, XorDec, uint32_t>(k, grid, s, (uint32_t *)src + so, (const uint32_t *)rep + ro, n,
+                                                 (int)k, Lv, src_present + 2 * b0, rep_present + 2 * b0, status + b0,
+                                                 recovered + 2 * b0);
+  }
   HIPCHK(hipGetLastError());
   g_stats[2]++;
   g_stats[3] += nblocks;

@@ -1269,8 +1269,11 @@ def main():
     parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
     parts.append(f"#define FEC_BS2_RT16_WAVES {4 if os.environ.get('FEC_GEN2_PROBE_ALIAS') else 3}  // 16-repair ring encode waves/SIMD")
     parts.append(f"#define FEC_BS2_SLOT {S2_SLOT}  // ring slot bytes (the bodies address slots by immediates)")
+    # the ring bodies ship for 16-repair / 16-unknown tiles only (round 2's A/Bs retired them for
+    # smaller tiles: k32 r8 +2 %, decode +10-20 %); FEC_GEN2_TILES=1,2,4,8,16 emits the rest for A/B builds
+    tiles2 = [int(x) for x in os.environ.get("FEC_GEN2_TILES", "16").split(",") if x]
     for mode in ("enc", "dec"):
-        for RT in (1, 2, 4, 8, 16):
+        for RT in tiles2:
             D = ring_depth(mode, RT)
             parts.append(f"#define FEC_BS2_D_{mode.upper()}_RT{RT} {D}")
             for NDMA in (1, 2):
@@ -1280,7 +1283,7 @@ def main():
                 parts.append("")
     with open(OUT, "w") as f:
         f.write("\n".join(parts))
-    print(f"wrote {OUT}: {len(CONFIGS) * 2} + 20 bodies, max VGPR {max(tops.values())}")
+    print(f"wrote {OUT}: {len(CONFIGS) * 2} + 4 + {4 * len(tiles2)} bodies, max VGPR {max(tops.values())}")
 
 
 if __name__ == "__main__":

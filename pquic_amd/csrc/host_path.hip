@@ -9,7 +9,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
+#include <shared_mutex>
+#include <vector>
 
 #include "../../include/fecgpu.h"
 
@@ -79,32 +83,75 @@ void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *c) {
   delete c;
 }
 
-// Page-locked allocations made through fecgpu_host_alloc, with their device addresses, so the
-// per-call lookups of the library's own staging buffers (the synchronous hooks pass seven pointers
-// per recover) skip hipPointerGetAttributes.  fecgpu_host_free removes an entry before freeing,
-// so a stale entry can never describe memory that is no longer page-locked.
+// Page-locked ranges the library made itself (fecgpu_host_alloc) or registered for a caller
+// (fecgpu_host_register: e.g. a plugin's memory arena), with their device addresses, so the per-call
+// lookups (the synchronous hooks pass seven pointers per recover, the batcher one table per job) skip
+// hipPointerGetAttributes.  Sorted by base, read under a shared lock; an entry is removed before its
+// memory stops being page-locked, so a stale entry can never describe unpinned memory.
 namespace {
-struct PinnedRange { uintptr_t base; size_t size; uint8_t *dev; };
-constexpr int kPinnedMax = 64;
-PinnedRange g_pinned[kPinnedMax];
-int g_npinned = 0;
-std::mutex g_pinned_mu;
+struct PinnedRange { uintptr_t base; size_t size; uint8_t *dev; bool registered; };
+std::vector<PinnedRange> g_pinned;  // sorted by base, disjoint
+std::shared_mutex g_pinned_mu;
+std::atomic<uint64_t> g_pin_hits{0}, g_pin_misses{0};
+
+void pinned_add(uintptr_t base, size_t size, uint8_t *dev, bool registered) {
+  std::unique_lock<std::shared_mutex> g(g_pinned_mu);
+  auto it = std::lower_bound(g_pinned.begin(), g_pinned.end(), base,
+                             [](const PinnedRange &r, uintptr_t b) { return r.base < b; });
+  g_pinned.insert(it, PinnedRange{base, size, dev, registered});
+}
+
+// removes the range starting at base; returns whether it was there (and whether it was registered)
+bool pinned_remove(uintptr_t base, bool *registered) {
+  std::unique_lock<std::shared_mutex> g(g_pinned_mu);
+  auto it = std::lower_bound(g_pinned.begin(), g_pinned.end(), base,
+                             [](const PinnedRange &r, uintptr_t b) { return r.base < b; });
+  if (it == g_pinned.end() || it->base != base) return false;
+  if (registered) *registered = it->registered;
+  g_pinned.erase(it);
+  return true;
+}
 }  // namespace
 
-// Device address of page-locked host memory (hipHostMalloc'd or registered), else nullptr.
-static uint8_t *mapped_host(const void *p) {
+extern "C" __attribute__((visibility("hidden"))) void fecgpu_host_registry_stats(uint64_t *hits, uint64_t *misses) {
+  *hits = g_pin_hits.load();
+  *misses = g_pin_misses.load();
+}
+
+// Device address of [p, p + len) when ALL of it is page-locked host memory (hipHostMalloc'd or
+// registered), else nullptr: the kernels then read and write the caller's memory directly, so an
+// array that starts inside a pinned buffer but runs past its end must take the staged copies.
+static uint8_t *mapped_host(const void *p, size_t len) {
   if (!p) return nullptr;
+  const uintptr_t a = (uintptr_t)p;
   {
-    const uintptr_t a = (uintptr_t)p;
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    for (int i = 0; i < g_npinned; i++)
-      if (a - g_pinned[i].base < g_pinned[i].size) return g_pinned[i].dev + (a - g_pinned[i].base);
+    std::shared_lock<std::shared_mutex> g(g_pinned_mu);
+    auto it = std::upper_bound(g_pinned.begin(), g_pinned.end(), a,
+                               [](uintptr_t x, const PinnedRange &r) { return x < r.base; });
+    if (it != g_pinned.begin()) {
+      --it;
+      if (a - it->base < it->size) {
+        g_pin_hits++;
+        return len <= it->size - (a - it->base) ? it->dev + (a - it->base) : nullptr;
+      }
+    }
   }
+  g_pin_misses++;
   hipPointerAttribute_t pa;
-  if (p && hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer)
-    return (uint8_t *)pa.devicePointer;
-  (void)hipGetLastError();  // pageable memory: clear the query error
-  return nullptr;
+  if (hipPointerGetAttributes(&pa, p) != hipSuccess || pa.type != hipMemoryTypeHost || !pa.devicePointer) {
+    (void)hipGetLastError();  // pageable memory: clear the query error
+    return nullptr;
+  }
+  uint8_t *d = (uint8_t *)pa.devicePointer;
+  if (len > 1) {  // the last byte must map into the same allocation, at the same offset
+    hipPointerAttribute_t pe;
+    if (hipPointerGetAttributes(&pe, (const uint8_t *)p + len - 1) != hipSuccess || pe.type != hipMemoryTypeHost ||
+        (uint8_t *)pe.devicePointer != d + len - 1) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  }
+  return d;
 }
 
 // Page-locked host buffers are read (and written) by the kernels directly over PCIe instead of
@@ -150,7 +197,7 @@ int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   HCHK(hipSetDevice(c->device));
   const size_t sb = (size_t)k * L, rb = (size_t)r * L;
   const uint64_t n = sub_batch(c, nblocks, sb);
-  uint8_t *zs = zc_read() ? mapped_host(src) : nullptr, *zr = zs ? mapped_host(rep) : nullptr;
+  uint8_t *zs = zc_read() ? mapped_host(src, nblocks * sb) : nullptr, *zr = zs ? mapped_host(rep, nblocks * rb) : nullptr;
   int si = 0, rc = FECGPU_OK;
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
@@ -213,8 +260,8 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
   const uint64_t n = sub_batch(c, nblocks, sb + rb);
   // page-locked src (hipHostMalloc / registered): the apply kernel writes the recovered rows
   // straight into it over PCIe, so nothing but status comes back by copy
-  uint8_t *zdst = xr ? nullptr : mapped_host(src);
-  const uint8_t *zrep = zdst && zc_read() ? mapped_host(rep) : nullptr;
+  uint8_t *zdst = xr ? nullptr : mapped_host(src, nblocks * sb);
+  const uint8_t *zrep = zdst && zc_read() ? mapped_host(rep, nblocks * rb) : nullptr;
   // page-locked masks / seeds / outputs as well (the synchronous protoops keep theirs so): the
   // kernels read and write them in place, and a call is two launches and one synchronisation with
   // no copies at all -- the latency of one-block calls is launch + PCIe round trips
@@ -223,12 +270,12 @@ static int decode_host(fecgpu_host_ctx_t *c, bool xr, void *src, const void *rep
   uint8_t *zst = nullptr;
   uint64_t *zrec = nullptr;
   if (zrep) {
-    zsp = (const uint64_t *)mapped_host(sp);
-    zrp = zsp ? (const uint64_t *)mapped_host(rp) : nullptr;
-    zst = zrp ? mapped_host(status) : nullptr;
-    zrec = zst ? (uint64_t *)mapped_host(recovered) : nullptr;
+    zsp = (const uint64_t *)mapped_host(sp, nblocks * 16);
+    zrp = zsp ? (const uint64_t *)mapped_host(rp, nblocks * 16) : nullptr;
+    zst = zrp ? mapped_host(status, nblocks) : nullptr;
+    zrec = zst ? (uint64_t *)mapped_host(recovered, nblocks * 16) : nullptr;
     const uint32_t *sf = seeds ? seeds : fbn;
-    zseed = zrec && sf ? (const uint32_t *)mapped_host(sf) : nullptr;
+    zseed = zrec && sf ? (const uint32_t *)mapped_host(sf, nblocks * 4 * (seeds ? (r ? r : 1) : 1)) : nullptr;
     if (!zrec || (sf && !zseed)) zsp = nullptr;  // all or nothing
   }
   int si = 0, rc = FECGPU_OK;
@@ -315,25 +362,45 @@ void *fecgpu_host_alloc(size_t bytes) {
   void *p = nullptr;
   if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
   hipPointerAttribute_t pa;
-  if (hipPointerGetAttributes(&pa, p) == hipSuccess && pa.devicePointer) {
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    if (g_npinned < kPinnedMax) g_pinned[g_npinned++] = {(uintptr_t)p, bytes ? bytes : 1, (uint8_t *)pa.devicePointer};
-  } else {
+  if (hipPointerGetAttributes(&pa, p) == hipSuccess && pa.devicePointer)
+    pinned_add((uintptr_t)p, bytes ? bytes : 1, (uint8_t *)pa.devicePointer, false);
+  else
     (void)hipGetLastError();
-  }
   return p;
 }
 
 void fecgpu_host_free(void *p) {
   if (!p) return;
-  {
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    for (int i = 0; i < g_npinned; i++)
-      if (g_pinned[i].base == (uintptr_t)p) {
-        g_pinned[i] = g_pinned[--g_npinned];
-        break;
-      }
-  }
+  pinned_remove((uintptr_t)p, nullptr);
   (void)hipHostFree(p);
+}
+
+int fecgpu_host_register(void *p, size_t bytes) {
+  if (!p || !bytes) return FECGPU_ERR_INVALID;
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return FECGPU_ERR_HIP;
+  }
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(p);
+    return FECGPU_ERR_HIP;
+  }
+  pinned_add((uintptr_t)p, bytes, (uint8_t *)d, true);
+  return FECGPU_OK;
+}
+
+int fecgpu_host_unregister(void *p) {
+  bool reg = false;
+  if (!p || !pinned_remove((uintptr_t)p, &reg) || !reg) return FECGPU_ERR_INVALID;
+  return hipHostUnregister(p) == hipSuccess ? FECGPU_OK : FECGPU_ERR_HIP;
+}
+
+int fecgpu_host_device_address(const void *p, size_t bytes, uint64_t *dev) {
+  if (!dev) return FECGPU_ERR_INVALID;
+  uint8_t *d = mapped_host(p, bytes);
+  *dev = (uint64_t)(uintptr_t)d;
+  return d ? FECGPU_OK : FECGPU_ERR_INVALID;
 }
 }  // extern "C"

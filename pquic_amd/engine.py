@@ -25,7 +25,8 @@ class FecGpuError(RuntimeError):
 
 class FecGpuStats(C.Structure):
     _fields_ = [("encode_calls", C.c_uint64), ("encode_blocks", C.c_uint64),
-                ("decode_calls", C.c_uint64), ("decode_blocks", C.c_uint64)]
+                ("decode_calls", C.c_uint64), ("decode_blocks", C.c_uint64),
+                ("pinned_registry_hits", C.c_uint64), ("pinned_registry_misses", C.c_uint64)]
 
 
 def load_library(path: str = LIB_PATH, private: bool = False):
@@ -66,6 +67,9 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_rlc_decode_host_seeded.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, v, v]
     L.fecgpu_xor_encode_host.argtypes = [v, v, v, u64, u32, u32]
     L.fecgpu_xor_decode_host.argtypes = [v, v, v, u64, u32, u32, v, v, v, v]
+    L.fecgpu_host_register.argtypes = [v, sz]
+    L.fecgpu_host_unregister.argtypes = [v]
+    L.fecgpu_host_device_address.argtypes = [v, sz, C.POINTER(u64)]
     if not private:
         _lib = L
     return L

@@ -232,17 +232,13 @@ def test_small_batch_decode_one_launch(eng, oracle, k, r, L, nb):
     work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     with eng.knob("plan", 1):  # the wave plan as its own launch, then the data pass
         _, got2, st2, rec2 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
-    with eng.knob("small_plan", 1):  # one launch with the lane-register plan (k <= 32, e <= 8; else the wave plan)
-        _, got3, st3, rec3 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     ref = work.copy()
     st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
     assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)
     assert np.array_equal(st2, st_ref) and np.array_equal(rec2, rec_ref)
-    assert np.array_equal(st3, st_ref) and np.array_equal(rec3, rec_ref)
     for b in range(nb):
         for j in bits(rec[b], k):
             assert np.array_equal(got[b, j], src_h[b, j]) and np.array_equal(got2[b, j], src_h[b, j])
-            assert np.array_equal(got3[b, j], src_h[b, j])
 
 
 def test_decode_zero_symbol_propagation(eng, oracle):
@@ -273,13 +269,10 @@ def test_decode_zero_symbol_propagation(eng, oracle):
             assert np.array_equal(got[b, j], src_h[b, j])
 
 
-@pytest.mark.parametrize("knob", [None, "xor_generic", "xor_idx64"])
-def test_xor_vs_oracle(eng, oracle, knob):
-    """XOR encode/recover vs the oracle: the k-specialised kernels (k = 2..8, 16; 16-B and 4-B
-    pieces), the runtime-k kernel, and the 64-bit-index instantiations."""
-    import contextlib
-    with eng.knob(knob, 1) if knob else contextlib.nullcontext():
-        _xor_vs_oracle(eng, oracle)
+def test_xor_vs_oracle(eng, oracle):
+    """XOR encode/recover vs the oracle: the k-specialised kernels (k = 2..6, 8, 16; 16-B and 4-B
+    pieces) and the runtime-k kernel (k = 1, 7, 100, 128)."""
+    _xor_vs_oracle(eng, oracle)
 
 
 def _xor_vs_oracle(eng, oracle):
@@ -489,7 +482,11 @@ def test_window_decode_vs_oracle(eng, oracle):
 
 @pytest.mark.parametrize("k,r,L,nb,plan", [(16, 4, 1200, 300, 0), (30, 5, 1200, 200, 0), (32, 8, 1204, 120, 0),
                                             (64, 16, 9000, 6, 0), (40, 20, 100, 60, 0), (100, 30, 64, 12, 0),
-                                            (16, 8, 256, 100, 1), (16, 8, 256, 100, 2)])
+                                            (16, 8, 256, 100, 1), (16, 8, 256, 100, 2),
+                                            # <= 64 blocks, e <= 8, k + e <= 64: the one-launch decode with
+                                            # the register wave plan (the synchronous hook's path)
+                                            (16, 4, 1200, 1, 0), (32, 8, 1200, 7, 0), (20, 6, 64, 64, 0),
+                                            (56, 8, 200, 33, 0)])
 def test_decode_seeded_vs_oracle(eng, oracle, k, r, L, nb, plan):
     """fecgpu_rlc_decode_seeded: each repair's coefficients come from its own FPID
     (rlc_fec_scheme_gf256.c:200) -- window style (0 << 8) | i, mixed block numbers per repair, and
@@ -752,6 +749,49 @@ def test_host_encode_zero_copy_pinned(oracle):
     hp.close()
 
 
+def test_host_register_zero_copy(oracle):
+    """fecgpu_host_register on an existing (malloc'd, page-aligned) host range -- as the batching
+    adapter registers a plugin arena -- makes it zero-copy for the host path: device addresses for
+    ranges inside it, none for a range that runs past its end, encode straight from / into it, and
+    unregistering twice is refused."""
+    import ctypes as C
+    from pquic_amd import HostPath, load_library
+    lib = load_library()
+    nb, k, r, L = 300, 16, 4, 1200
+    page = 4096
+    size = ((nb * (k + r) * L + page - 1) // page) * page
+    raw = np.zeros(size + page, np.uint8)
+    off = (-raw.ctypes.data) % page
+    arena = raw[off:off + size]
+    base = arena.ctypes.data
+    assert lib.fecgpu_host_register(base, size) == 0
+    try:
+        dev = C.c_uint64()
+        assert lib.fecgpu_host_device_address(base + 100, size - 100, C.byref(dev)) == 0 and dev.value
+        assert lib.fecgpu_host_device_address(base + 100, size - 99, C.byref(dev)) != 0  # one byte past the end
+        st0 = _stats(lib)
+        src = arena[:nb * k * L].reshape(nb, k, L)
+        rep = arena[nb * k * L:nb * (k + r) * L].reshape(nb, r, L)
+        src[:] = synth_bytes(nb * k * L, 77).reshape(nb, k, L)
+        hp = HostPath(0, 2, 1 << 20)
+        hp.rlc_encode(src, rep, nb, k, r, L, 5)
+        hp.close()
+        assert np.array_equal(rep, oracle.rlc_encode_batch(np.ascontiguousarray(src), r, 5))
+        st1 = _stats(lib)
+        assert st1.pinned_registry_hits >= st0.pinned_registry_hits + 2  # both arrays found in the registry
+    finally:
+        assert lib.fecgpu_host_unregister(base) == 0
+    assert lib.fecgpu_host_unregister(base) != 0
+
+
+def _stats(lib):
+    from pquic_amd.engine import FecGpuStats
+    import ctypes as C
+    s = FecGpuStats()
+    lib.fecgpu_get_stats(C.byref(s))
+    return s
+
+
 def test_window_encode_past_grid_cap(eng, oracle):
     """More than 2^22 windows: one window per group, so the launch's grid is capped and the
     kernel's group loop takes over; windows past the cap (and the very last) match the oracle."""
@@ -813,21 +853,21 @@ def test_roundtrip_k32_e8(eng, oracle):
     torch.cuda.empty_cache()
 
 
-ALT_PATH_CASES = [(16, 4, 1200, 300), (32, 8, 1200, 100), (7, 5, 2052, 60), (64, 16, 9000, 6)]
-RING_CASES = ALT_PATH_CASES + [(8, 1, 1200, 90), (10, 2, 16, 70), (9, 16, 1040, 50), (40, 16, 4100, 7),
-                               (33, 9, 2048, 40), (4, 3, 20, 65)]
+RING_CASES = [(64, 16, 9000, 6), (9, 16, 1040, 50), (40, 16, 4100, 7), (20, 17, 2048, 40), (16, 16, 1200, 60),
+              (5, 16, 16, 70), (4, 16, 20, 65)]
 
 
-@pytest.mark.parametrize("knob,k,r,L,nb", [("datapath_perm",) + c for c in ALT_PATH_CASES] +
-                         [("ring",) + c for c in RING_CASES])
-def test_alt_datapath_vs_oracle(eng, oracle, knob, k, r, L, nb):
-    """The v_perm data path (knob datapath_perm) and the LDS-DMA ring data path (knob ring), kept
-    for A/B against the default bitsliced one, give the same encode and decode bytes as the
-    oracle (the ring path over tiles of 1..16 repairs, one and two DMAs per row, several chunks,
-    short blocks that fall back to the default path)."""
+@pytest.mark.parametrize("ring", [2, 0])
+@pytest.mark.parametrize("k,r,L,nb", RING_CASES)
+def test_ring_datapath_vs_oracle(eng, oracle, ring, k, r, L, nb):
+    """16-repair / 16-unknown tiles run on the LDS-DMA ring body by default (knob ring = 2) and on the
+    register-prefetch body with ring = 0; both give the oracle's encode and decode bytes (one and
+    two DMAs per row, several chunks, ragged symbol lengths, blocks shorter than the ring depth
+    that fall back to the register body)."""
+    knob = "ring"
     rng = np.random.default_rng(k + 7 * r)
     src_h = synth_bytes(nb * k * L, 3 + k).reshape(nb, k, L)
-    with eng.knob(knob, 1):
+    with eng.knob(knob, ring):
         src = to_dev(src_h)
         rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
         eng.rlc_encode(src, rep, k, r, L, fbn_base=41)

@@ -42,8 +42,6 @@ def to_knobs(env):
         if kk == "FECGPU_ENC_TILE":
             a, b = vv.split(",")
             out["enc_tile_rt"], out["enc_tile_waves"] = int(a), int(b)
-        elif kk == "FECGPU_DATAPATH":
-            out["datapath_perm"] = int(vv == "perm")
         elif kk == "FECGPU_PLAN":
             out["plan"] = PLAN.get(vv, 0)
         elif kk.startswith("FECGPU_"):
