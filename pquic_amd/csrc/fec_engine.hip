@@ -48,9 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
-                                           "zc_read", "ring", "window_sc", "min_groups"};
+                                           "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
+                                           "small_lds"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -79,6 +80,12 @@ static void knobs_from_env() {
   // batches too small to fill the chip stream fewer blocks per wave: groups of blocks shrink until
   // there are at least this many groups (0: the per-shape group sizes at every batch size)
   g_knob[K_MIN_GROUPS] = num(getenv("FECGPU_MIN_GROUPS"), 1024);
+  // ring tiles of symbols wider than one column chunk: one wave per chunk of a block at once (1) or
+  // one wave coding the chunks in turn (0)
+  g_knob[K_CHUNK_WAVES] = num(getenv("FECGPU_CHUNK_WAVES"), 1) != 0;
+  // batches of <= kSmallLdsMaxBlocks blocks: rows staged in LDS by a workgroup per block (1) or the
+  // bitsliced one-wave-per-block kernels (0)
+  g_knob[K_SMALL_LDS] = num(getenv("FECGPU_SMALL_LDS"), 1) != 0;
 }
 
 static inline int knob(KnobId id) {
@@ -137,6 +144,19 @@ __device__ __forceinline__ uint32_t block_fbn(uint64_t b, uint32_t fbn_base, con
 __device__ __forceinline__ uint32_t repair_seed(const uint32_t *seeds, uint64_t b, int r, uint32_t f, uint32_t i) {
   return seeds ? seeds[b * (uint64_t)r + i] : rlc_seed(f, i);
 }
+
+// Phase stamps (diagnostic builds only, -DFEC_STAMP; tools/phase_probe.py): workgroup 0's thread 0
+// records s_memrealtime (100 MHz) at the marked points of a kernel, in issue order, so a one-block
+// launch can be split into its phases.  The shipped library compiles them out.
+#ifdef FEC_STAMP
+__device__ uint64_t g_fec_stamps[16];
+#define FEC_STAMP_AT(i)                                                          \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_fec_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FEC_STAMP_AT(i) do { } while (0)
+#endif
 
 static uint32_t grid_for(uint64_t units);
 
@@ -208,6 +228,15 @@ __device__ __forceinline__ void clip128(uint64_t &m0, uint64_t &m1, int n) {
   else if (n < 128) m1 &= (1ull << (n - 64)) - 1;
 }
 
+// Barrier of the wave plans: the workgroup's (one-wave plan kernels, k_rlc_decode_small) or, when one
+// wave of a larger workgroup plans while the others stage rows (WG = false), the wave's own: its LDS
+// operations complete in order, so waiting for them orders every lane's later reads after the writes.
+template <bool WG>
+__device__ __forceinline__ void plan_sync() {
+  if constexpr (WG) __syncthreads();
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // One block's plan by one wave (row-parallel elimination).  `lds` holds the log/exp tables at 0
 // (plan_load_tables) and room for plan_lds_bytes(k, r).  Every lane of the wave must call it.
 // (48 lanes, one 16-B load each: one memory round trip, which a one-block decode waits for)
@@ -220,6 +249,7 @@ __device__ __forceinline__ void plan_load_tables(uint8_t *lds) {
 // Common start of the wave plans: the block's unknowns (unk[u] = u-th missing source), its equations
 // (sel[e] = e-th present repair, :194-212) and their TinyMT32 coefficient rows X[e][0..k) in LDS.
 // Returns n, the number of unknowns, or 0 after writing the "nothing to do" record (:140-144).
+template <bool WG>
 __device__ __forceinline__ int plan_wave_setup(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
                                                const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp,
                                                uint8_t *h, const PlanLds &P, int kpad, uint64_t &m0,
@@ -230,7 +260,9 @@ __device__ __forceinline__ int plan_wave_setup(uint64_t b, int k, int r, uint32_
   clip128(q0, q1, r);
   const int cur_ss = __popcll(s0) + __popcll(s1);
   const int cur_rs = __popcll(q0) + __popcll(q1);
-  __syncthreads();
+  if (cur_ss + cur_rs == 255) FEC_STAMP_AT(15);  // (never true: orders stamp 1 after the mask loads)
+  FEC_STAMP_AT(1);
+  plan_sync<WG>();
   // rlc_fec_scheme_gf256.c:140-144
   if (r == 0 || cur_ss == k || cur_ss + cur_rs < k) {
     if (lane == 0) { h[0] = FECGPU_BLOCK_NOTHING; h[1] = 0; }
@@ -247,14 +279,15 @@ __device__ __forceinline__ int plan_wave_setup(uint64_t b, int k, int r, uint32_
       const int e = rank128(q0, q1, i);
       if (e < n) P.sel[e] = i;
     }
-  __syncthreads();
+  plan_sync<WG>();
   const uint32_t f = block_fbn(b, fbn_base, fbn);
   for (int e = lane; e < n; e += 64) {  // TinyMT32 row of repair sel[e] (get_coefs :117-125)
     Tmt t;
     tmt_init(t, repair_seed(seeds, b, r, f, (uint32_t)P.sel[e]));
     for (int j = 0; j < k; j++) P.X[e * kpad + j] = tmt_coef(t);
   }
-  __syncthreads();
+  plan_sync<WG>();
+  FEC_STAMP_AT(2);
   return n;
 }
 
@@ -273,6 +306,7 @@ __device__ __forceinline__ void plan_wave_finish(uint8_t *h, const WsLayout &L, 
   if (lane == 0) { h[0] = FECGPU_BLOCK_RECOVERED; h[1] = (uint8_t)n; }
 }
 
+template <bool WG = true>
 __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
                                 const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *ws,
                                 uint8_t *lds) {
@@ -289,7 +323,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
   {
     uint8_t *h = ws + b * (uint64_t)L.stride;
     uint64_t m0 = 0, m1 = 0;
-    const int n = plan_wave_setup(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
+    const int n = plan_wave_setup<WG>(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
     if (!n) return;
     // A[e][u] = row_e[unk[u]];  V[e][j] = present j ? row_e[j] : (j == unk[e])
     for (int x = lane; x < n * n; x += 64) {
@@ -300,12 +334,12 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       const int e = x / k, j = x - e * k;
       V[e * kpad + j] = bit128(m0, m1, j) ? (uint8_t)(unk[e] == j) : X[e * kpad + j];
     }
-    __syncthreads();
+    plan_sync<WG>();
     // sort_system (:28-40): position i takes the first row with the largest A[.][i].  The scan
     // over rows j >= i is a wave max-reduction of (value << 16 | 0xffff - j), so the largest value
     // wins and, among equal values, the smallest j -- the reference's strict '<' scan.
     for (int i = lane; i < n; i += 64) perm[i] = i;
-    __syncthreads();
+    plan_sync<WG>();
     for (int i = 0; i < n; i++) {
       uint32_t key = 0;
       for (int j = i + lane; j < n; j += 64) {
@@ -318,9 +352,9 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
         key = o > key ? o : key;
       }
       const int mx = (int)(0xffffu - (key & 0xffffu));
-      __syncthreads();  // every lane has read perm[] before it changes
+      plan_sync<WG>();  // every lane has read perm[] before it changes
       if (lane == 0) { const int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t; }
-      __syncthreads();
+      plan_sync<WG>();
     }
     // forward elimination without re-pivoting (:54-70): row_pk -= (A[pk][i] / A[pi][i]) row_pi for all
     // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below).  A lane owns a
@@ -337,7 +371,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
         const int d = (int)LOG[a] - (int)lpiv;
         terms[x] = (piv && a) ? (uint8_t)(d < 0 ? d + 255 : d) : (uint8_t)255;
       }
-      __syncthreads();
+      plan_sync<WG>();
       const int wa = n - i, w = wa + k;  // columns i..n-1 of A, then all of V
       for (int c = lane; c < w; c += 64) {
         const bool ina = c < wa;
@@ -352,7 +386,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
           col[perm[i + 1 + rr] * rs] ^= EXP[lp + t];
         }
       }
-      __syncthreads();
+      plan_sync<WG>();
     }
     // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
     const bool zd = lane < n && A[perm[lane] * empad + lane] == 0;
@@ -379,7 +413,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
         }
       }
     }
-    __syncthreads();
+    plan_sync<WG>();
     for (int x = lane; x < n * n; x += 64) {
       const int i = x / n, u = x - i * n;
       h[L.off_dep + i * em + u] = (u > i) && A[perm[i] * empad + u] != 0;
@@ -399,7 +433,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
 // constant of the unrolled loops and the per-row scalars (pivot terms, A[m][i]) come from the
 // owning lane through readlane, so the only LDS traffic is the log/exp lookups, which are
 // independent across rows.  Same record bytes (test_plan_kernels_agree).
-template <int EM, int C>
+template <int EM, int C, bool WG = true>
 __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, const uint32_t *fbn,
                                 const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *ws,
                                 uint8_t *lds) {
@@ -410,7 +444,7 @@ __device__ void plan_wreg_block(uint64_t b, int k, int r, uint32_t fbn_base, con
   const uint8_t *EXP = P.exp, *LOG = P.log, *X = P.X;
   uint8_t *h = ws + b * (uint64_t)L.stride;
   uint64_t m0 = 0, m1 = 0;
-  const int n = plan_wave_setup(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
+  const int n = plan_wave_setup<WG>(b, k, r, fbn_base, fbn, seeds, sp, rp, h, P, kpad, m0, m1);
   if (!n) return;
   uint32_t col[C][EM];
   bool isv[C], live[C];
@@ -539,16 +573,17 @@ __device__ __forceinline__ bool plan_wreg_fits(int k, int r) {
   const int em = k < r ? k : r;
   return em <= 8 && k + em <= 64;
 }
+template <bool WG = true>
 __device__ __forceinline__ void plan_wave_any(int wreg, uint64_t b, int k, int r, uint32_t fbn_base,
                                               const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
                                               const uint64_t *rp, uint8_t *ws, uint8_t *lds) {
   const int em = k < r ? k : r;
   if (wreg && plan_wreg_fits(k, r)) {
-    if (em <= 4) plan_wreg_block<4, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
-    else plan_wreg_block<8, 1>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    if (em <= 4) plan_wreg_block<4, 1, WG>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+    else plan_wreg_block<8, 1, WG>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
     return;
   }
-  plan_wave_block(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
+  plan_wave_block<WG>(b, k, r, fbn_base, fbn, seeds, sp, rp, ws, lds);
 }
 
 // The register wave plan as its own kernel (k_rlc_plan keeps the LDS plan's smaller register
@@ -1318,6 +1353,7 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
+    FEC_STAMP_AT(5);
     if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
@@ -1338,6 +1374,7 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
       }
     }
     __syncthreads();
+    FEC_STAMP_AT(6);
     if (rt <= 0) continue;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
@@ -1351,6 +1388,10 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
         bs_enc_call<RT, VEC>(sp, rpp, (uint32_t)L, rstep, sdelta, (uint32_t)(ng * k), (uint32_t)k, (uint32_t)rt,
                              lds_addr(lds), ln);
     }
+#ifdef FEC_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    FEC_STAMP_AT(7);
   }
 }
 
@@ -1537,11 +1578,224 @@ __global__ __launch_bounds__(64) void k_rlc_decode_small(uint8_t *__restrict__ s
   for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
     uint8_t *wsx = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(lds + rec_off) - b * stride);
     __syncthreads();
+    FEC_STAMP_AT(0);
     plan_load_tables(lds);
     plan_wave_any(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, wsx, lds);
     __syncthreads();
+    FEC_STAMP_AT(3);
     recover_bs_group<RT, VEC>(b, nblocks, 1, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, wsx, 0, 1, status,
                               recovered, 0, dst, lds);
+#ifdef FEC_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    FEC_STAMP_AT(4);
+  }
+}
+
+// =============================================================================================
+// A few blocks with their rows staged in LDS (the synchronous hooks run one block per call).
+// One workgroup of 8 waves per block.  A one-block launch is latency-bound: the bitsliced bodies
+// stream a block's rows through ONE wave, a dependent chain of k steps, and from page-locked host
+// memory every prefetch window is a PCIe round trip.  Here waves 1-7 fetch all of the block's rows
+// into LDS at once (one round trip) while wave 0 computes the coefficients -- TinyMT32 rows (encode)
+// or the whole wave plan (decode) -- and then every thread multiply-accumulates one 4-byte word of the
+// outputs with the packed v_perm GF multiply (fec_device.h gf_mac), its coefficient tables built once
+// per (output, input) pair in LDS.
+// =============================================================================================
+constexpr int kLdsThreads = 512;
+constexpr uint64_t kSmallLdsMaxBlocks = 64;  // batches up to this many blocks (knob small_lds)
+
+// rows [row0, row0 + nrows) of `base` (row stride L bytes) into LDS rows of Lp bytes, by threads
+// [t0, kLdsThreads); 16-B pieces when L and the base are 16-B aligned, else dwords
+__device__ __forceinline__ void stage_rows_lds(uint8_t *lrows, const uint8_t *base, int nrows, int L, int Lp, int t0) {
+  const int tid = (int)threadIdx.x - t0, nt = kLdsThreads - t0;
+  if (tid < 0) return;
+  if ((L & 15) == 0 && ((uintptr_t)base & 15) == 0) {
+    const int pr = L >> 4, tot = nrows * pr;
+    for (int x = tid; x < tot; x += nt) {
+      const int row = x / pr, c = x - row * pr;
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<v4u *>(lrows + row * Lp + 16 * c) =
+          __builtin_nontemporal_load(reinterpret_cast<const v4u *>(base + (size_t)row * L + 16 * c));
+    }
+  } else {
+    const int pr = L >> 2, tot = nrows * pr;
+    for (int x = tid; x < tot; x += nt) {
+      const int row = x / pr, c = x - row * pr;
+      *reinterpret_cast<uint32_t *>(lrows + row * Lp + 4 * c) =
+          __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base + (size_t)row * L + 4 * c));
+    }
+  }
+}
+
+// packed-multiply tables of a tile of OT outputs x k inputs, input-major ([j][o]: the OT tables an
+// input step needs are contiguous, so they load as a few back-to-back broadcast LDS reads); outputs
+// past the tile's live ones get the zero coefficient's (all-zero) tables, so the loops need no guards
+struct LdsTabs {
+  uint4 *t01;
+  uint32_t *t2;
+};
+
+template <int OT>
+__device__ __forceinline__ void build_tabs(LdsTabs T, const uint8_t *coef, int cstride, int o0, int no, int k) {
+  for (int x = threadIdx.x; x < OT * k; x += kLdsThreads) {
+    const int j = x / OT, o = x - j * OT;
+    const PermTab t = perm_table(o < no ? coef[(o0 + o) * cstride + j] : 0u);
+    T.t01[x] = t.t01;
+    T.t2[x] = t.t2;
+  }
+}
+
+// out[o][w] = sum_j coef(o, j) * row_j[w] for the tile's outputs o < no, words w of this thread (row j
+// at rows + j * rstride dwords); store(o, w, value)
+template <int OT, typename Store>
+__device__ __forceinline__ void lds_mac_words(const LdsTabs &T, int no, int k, int Lw, const uint32_t *rows,
+                                              int rstride, Store store) {
+  for (int w = threadIdx.x; w < Lw; w += kLdsThreads) {
+    uint32_t acc[OT];
+#pragma unroll
+    for (int o = 0; o < OT; o++) acc[o] = 0;
+#pragma unroll 2
+    for (int j = 0; j < k; j++) {
+      const Sel sl = perm_selectors(rows[j * rstride + w]);
+      const uint4 *t01 = T.t01 + j * OT;
+      const uint32_t *t2 = T.t2 + j * OT;
+#pragma unroll
+      for (int o = 0; o < OT; o++) acc[o] = gf_mac(acc[o], sl, t01[o], t2[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < OT; o++)
+      if (o < no) store(o, w, acc[o]);
+  }
+}
+
+struct EncLdsLayout {
+  uint32_t coef, t01, t2, rows, bytes;
+  __host__ __device__ EncLdsLayout(int k, int r, int L, int OT) {
+    coef = 0;
+    t01 = pad16((uint32_t)(r * pad16((uint32_t)k)));
+    t2 = t01 + 16u * OT * k;
+    rows = pad16(t2 + 4u * OT * k);
+    bytes = rows + (uint32_t)k * pad16((uint32_t)L);
+  }
+};
+
+template <int RT>
+__global__ __launch_bounds__(kLdsThreads) void k_rlc_encode_lds(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                                uint64_t nblocks, int k, int r, int L, uint32_t fbn_base,
+                                                                const uint32_t *fbn) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const EncLdsLayout Y(k, r, L, RT);
+  const int kpad = (int)pad16((uint32_t)k), Lp = (int)pad16((uint32_t)L), Lw = L >> 2;
+  uint8_t *C = lds + Y.coef;
+  const LdsTabs T{reinterpret_cast<uint4 *>(lds + Y.t01), reinterpret_cast<uint32_t *>(lds + Y.t2)};
+  const uint32_t *rows = reinterpret_cast<const uint32_t *>(lds + Y.rows);
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    __syncthreads();
+    FEC_STAMP_AT(5);
+    if (threadIdx.x < 64) {  // wave 0: the TinyMT32 rows of repairs i (get_coefs, rlc_fec_scheme_generate_gf256.c:9-17)
+      const uint32_t f = block_fbn(b, fbn_base, fbn);
+      for (int i = (int)threadIdx.x; i < r; i += 64) {
+        Tmt t;
+        tmt_init(t, rlc_seed(f, (uint32_t)i));
+        for (int j = 0; j < k; j++) C[i * kpad + j] = tmt_coef(t);
+      }
+    } else {
+      stage_rows_lds(lds + Y.rows, src + b * (uint64_t)k * L, k, L, Lp, 64);
+    }
+    uint32_t *rb = reinterpret_cast<uint32_t *>(rep + b * (uint64_t)r * L);
+    for (int i0 = 0; i0 < r; i0 += RT) {  // tiles of RT repairs
+      const int no = r - i0 < RT ? r - i0 : RT;
+      __syncthreads();
+      if (i0 == 0) FEC_STAMP_AT(6);
+      build_tabs<RT>(T, C, kpad, i0, no, k);
+      __syncthreads();
+      lds_mac_words<RT>(T, no, k, Lw, rows, Lp >> 2, [&](int i, int w, uint32_t v) {
+        __builtin_nontemporal_store(v, rb + (size_t)(i0 + i) * Lw + w);
+      });
+    }
+#ifdef FEC_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#endif
+    FEC_STAMP_AT(7);
+  }
+}
+
+struct DecLdsLayout {
+  uint32_t rec, nz, t01, t2, rows, bytes;
+  __host__ __device__ DecLdsLayout(int k, int r, int L, int OT) {
+    const WsLayout W = ws_layout((uint32_t)k, (uint32_t)r);
+    rec = pad16((uint32_t)plan_lds_bytes((uint32_t)k, (uint32_t)r));
+    nz = rec + W.stride;
+    t01 = nz + 16;
+    t2 = t01 + 16u * OT * k;
+    rows = pad16(t2 + 4u * OT * k);
+    bytes = rows + (uint32_t)(k + r) * pad16((uint32_t)L);
+  }
+};
+
+// e <= EM unknowns per block (one pass); the zero/undetermined rule runs at the end (thread 0).
+template <int EM>
+__global__ __launch_bounds__(kLdsThreads) void k_rlc_decode_lds(const uint8_t *__restrict__ src,
+                                                                const uint8_t *__restrict__ rep, uint64_t nblocks, int k,
+                                                                int r, int L, uint32_t fbn_base, const uint32_t *fbn,
+                                                                const uint32_t *seeds, const uint64_t *sp,
+                                                                const uint64_t *rp, uint8_t *status, uint64_t *recovered,
+                                                                uint8_t *dst, int wreg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const DecLdsLayout Y(k, r, L, EM);
+  const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
+  const int Lp = (int)pad16((uint32_t)L), Lw = L >> 2;
+  uint8_t *h = lds + Y.rec;
+  uint32_t *nzword = reinterpret_cast<uint32_t *>(lds + Y.nz);
+  const LdsTabs T{reinterpret_cast<uint4 *>(lds + Y.t01), reinterpret_cast<uint32_t *>(lds + Y.t2)};
+  uint32_t *rows = reinterpret_cast<uint32_t *>(lds + Y.rows);
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    __syncthreads();
+    if (threadIdx.x < 64) {  // wave 0: the plan (its record lands in LDS: a base that puts block b's there)
+      FEC_STAMP_AT(0);
+      plan_load_tables(lds);
+      plan_wave_any<false>(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, h - b * (uint64_t)WL.stride, lds);
+      if (threadIdx.x == 0) *nzword = 0;
+    } else {  // waves 1-7: all k source and r repair rows of the block (absent ones are never read)
+      stage_rows_lds(lds + Y.rows, src + b * (uint64_t)k * L, k, L, Lp, 64);
+      stage_rows_lds(lds + Y.rows + k * Lp, rep + b * (uint64_t)r * L, r, L, Lp, 64);
+    }
+    __syncthreads();
+    FEC_STAMP_AT(3);
+    const int st = h[0], n = h[1];
+    if (st == FECGPU_BLOCK_RECOVERED) {
+      // input j is source j, or for a missing source the repair its slot names: copy those repair rows
+      // over the missing sources' rows, so input j is LDS row j
+      const int Lq = Lp >> 2;
+      for (int x = threadIdx.x; x < n * Lq; x += kLdsThreads) {
+        const int u = x / Lq, c = x - u * Lq, j = h[WL.off_unk + u];
+        rows[j * Lq + c] = rows[(k + (h[WL.off_slot + j] & 0x7f)) * Lq + c];
+      }
+      build_tabs<EM>(T, h + WL.off_D, k, 0, n, k);
+      __syncthreads();
+      uint32_t *db = reinterpret_cast<uint32_t *>(dst + b * (uint64_t)k * L);
+      uint32_t nzm = 0;
+      lds_mac_words<EM>(T, n, k, Lw, rows, Lq, [&](int u, int w, uint32_t v) {
+        __builtin_nontemporal_store(v, db + (size_t)h[WL.off_unk + u] * Lw + w);
+        nzm |= (uint32_t)(v != 0) << u;
+      });
+      if (nzm) atomicOr(nzword, nzm);
+    }
+    __syncthreads();
+    FEC_STAMP_AT(4);
+    if (threadIdx.x == 0) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (rlc_finalize_block)
+      uint64_t m0 = 0, m1 = 0;
+      if (st == FECGPU_BLOCK_RECOVERED) {
+        uint8_t nzf[16];
+        for (int u = 0; u < 16; u++) nzf[u] = (uint8_t)((*nzword >> u) & 1u);
+        rlc_finalize_block(h, WL, nzf, m0, m1);
+      }
+      status[b] = (uint8_t)st;
+      recovered[2 * b] = m0;
+      recovered[2 * b + 1] = m1;
+    }
   }
 }
 
@@ -1747,11 +2001,23 @@ __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa,
 // W waves per workgroup split a group's repairs (wave w: repairs r0 + w RT ..), each with its own
 // coefficient rows and ring; they read the same source rows close together in time (L2 serves the
 // repeats).  W = 1 unless a tile knob asks for more.
-template <int RT>
+// CW (chunk waves): symbols wider than one column chunk (L > 2 KiB, e.g. configs[4]'s 9000 B).  A
+// workgroup of kCwWaves waves codes a group of G blocks as the list of its (block, chunk) items --
+// wave w takes items w, w + kCwWaves, ... -- so each round codes kCwWaves consecutive chunks at once,
+// sharing the group's coefficient rows (one TinyMT32 pass) and each wave streaming its own ring.
+// Neighbouring chunks of a row advance together, so the 128-B lines they share (chunk and row
+// boundaries are not line-aligned) are fetched once and hit in L2 for the other wave, instead of
+// being re-fetched by the next chunk pass of one wave tens of microseconds later.  Four waves per
+// workgroup: the waves of a workgroup are spread evenly over the CU's four SIMDs, so a 5-wave
+// workgroup holds two slots on every SIMD and halved the resident waves (+68 % time at k64 r16
+// L9000, profiles/r03_ab_chunk_waves_5wave_wg.log).
+constexpr int kCwWaves = 4;
+
+template <int RT, bool CW>
 #ifndef FEC_BS2_RT16_WAVES
 #define FEC_BS2_RT16_WAVES 3
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? FEC_BS2_RT16_WAVES : 1)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? FEC_BS2_RT16_WAVES : 1)))
 void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
@@ -1762,10 +2028,11 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
   constexpr int D = Bs2Depth16::enc;
-  const uint32_t per_wave = pad16((uint32_t)(G * k * CSB)) + D * slotb;
-  uint8_t *lds = lds_all + (size_t)wave * per_wave;
-  const uint32_t ring = lds_addr(lds) + pad16((uint32_t)(G * k * CSB));
-  r0 += wave * RT;
+  const uint32_t coef_bytes = pad16((uint32_t)(G * k * CSB));
+  // CW: one set of coefficient rows for the group, then a ring per wave; otherwise rows + ring per wave
+  uint8_t *lds = CW ? lds_all : lds_all + (size_t)wave * (coef_bytes + D * slotb);
+  const uint32_t ring = CW ? lds_addr(lds_all) + coef_bytes + (uint32_t)wave * D * slotb : lds_addr(lds) + coef_bytes;
+  if constexpr (!CW) r0 += wave * RT;
   const int rt = r - r0 < RT ? r - r0 : RT;  // <= 0: this wave has no repairs (waits at barriers)
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
@@ -1774,7 +2041,8 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
-    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0 + lane % RT)
+    if ((CW ? (int)threadIdx.x : lane) < G * RT) {  // TinyMT32 rows: lane -> (block g, repair r0 + lane % RT)
+      // (CW: wave 0's lanes only, G * RT <= 64)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
       uint16_t *row0 = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB);
@@ -1795,24 +2063,40 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
     }
     __syncthreads();
     if (rt <= 0) continue;
-    for (int ch = 0; ch < nchunks; ch++) {
-      const int c0 = ch * chunk_bytes;
-      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-      const Bs2Lanes ln(lane, cb, 0u, ring);
-      const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);
-      const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L + c0);
-      const uint64_t rstep = bstep * (uint64_t)r * L;
-      const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;
-      const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
-      const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
-      bs2_enc_call(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
-                       ln);
+    if constexpr (CW) {  // items (block g, chunk ch), one block's k rows per body call
+      for (int it = wave; it < ng * nchunks; it += kCwWaves) {
+        const int g = it / nchunks, ch = it - g * nchunks;
+        const int c0 = ch * chunk_bytes;
+        const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+        const Bs2Lanes ln(lane, cb, 0u, ring);
+        const uint64_t b = b0 + g * bstep;
+        const uint64_t sp = (uint64_t)(uintptr_t)(src + b * sbs + c0);
+        const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b * (uint64_t)r + r0) * (uint64_t)L + c0);
+        bs2_enc_call(ln.npieces > 64, sp, rpp, L, 0u, 0u, (uint64_t)L, (uint64_t)L, rt, (uint32_t)k, k,
+                     lds_addr(lds + (size_t)g * k * CSB), ring, ln);
+      }
+    } else {
+      for (int ch = 0; ch < nchunks; ch++) {
+        const int c0 = ch * chunk_bytes;
+        const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+        const Bs2Lanes ln(lane, cb, 0u, ring);
+        const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);
+        const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L + c0);
+        const uint64_t rstep = bstep * (uint64_t)r * L;
+        const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;
+        const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
+        const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
+        bs2_enc_call(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
+                     ln);
+      }
     }
   }
 }
 
-template <int RT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT == 16 ? 3 : RT == 8 ? 4 : 1)))
+// CW: as in k_rlc_encode_bs2, kCwWaves waves code the group's (block, chunk) items; the setup is
+// spread over every thread of the workgroup and wave 0 writes the statuses once all items are done.
+template <int RT, bool CW>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 ? 3 : RT == 8 ? 4 : 1)))
 void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint8_t *ws, int r0, int G,
@@ -1820,9 +2104,12 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
                                                         uint8_t *dst, uint32_t slotb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = CW ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  const int tid = CW ? (int)threadIdx.x : lane, nthr = CW ? (int)blockDim.x : 64;
   RecoverLds<RT> S(lds, G, k);
-  const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k));
+  const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) +
+                        (uint32_t)wave * Bs2Depth16::dec * slotb;
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
@@ -1831,7 +2118,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
     const int ng = left < (uint64_t)G ? (int)left : G;
     bool act = false;
     int st = FECGPU_BLOCK_NOTHING, e = 0;
-    if (lane < ng) {
+    if (lane < ng) {  // every wave reads the group's headers (the same values)
       const uint8_t *h = ws + (b0 + lane * bstep) * (uint64_t)WL.stride;
       st = h[0];
       e = h[1];
@@ -1840,13 +2127,13 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
     const uint64_t am = __ballot(act);
     const int nact = __popcll(am);
     __syncthreads();
-    if (act) {
+    if (act && wave == 0) {
       const int t = __popcll(am & ((1ull << lane) - 1));
       S.gid[t] = (uint8_t)lane;
       S.ecnt[t] = (uint8_t)(e - r0 < RT ? e - r0 : RT);
     }
     __syncthreads();
-    for (int x = lane; x < nact * k; x += 64) {
+    for (int x = tid; x < nact * k; x += nthr) {
       const int t = x / k, j = x - t * k;
       const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
@@ -1861,7 +2148,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
                                      : src + (b * (uint64_t)k + sl) * (uint64_t)L;
       S.intab[x] = (uint64_t)(uintptr_t)p;
     }
-    for (int x = lane; x < nact * 16; x += 64) {
+    for (int x = tid; x < nact * 16; x += nthr) {
       const int t = x >> 4, u = x & 15;
       const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
@@ -1884,7 +2171,16 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       }
     }
     __syncthreads();
-    if (nact) {
+    if constexpr (CW) {  // items (active block t, chunk ch); the chunks' non-zero flags OR together
+      for (int it = wave; it < nact * nchunks; it += kCwWaves) {
+        const int t = it / nchunks, ch = it - t * nchunks;
+        const int c0 = ch * chunk_bytes;
+        const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+        const Bs2Lanes ln(lane, cb, (uint32_t)c0, ring);
+        bs2_dec_call(ln.npieces > 64, lds_addr(S.intab + (size_t)t * k), lds_addr(S.rec + (size_t)t * kDecRec),
+                     (uint32_t)k, k, lds_addr(S.coef + (size_t)t * k * RecoverLds<RT>::CSB), ring, ln);
+      }
+    } else if (nact) {
       for (int ch = 0; ch < nchunks; ch++) {
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
@@ -1894,6 +2190,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       }
     }
     __syncthreads();
+    if (wave != 0) continue;
     if (status) {
       if (lane < ng) {
         const uint64_t b = b0 + lane * bstep;
@@ -1942,20 +2239,39 @@ static inline int bs2_waves_per_cu(int RT) {
   return RT <= 4 ? 20 : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 4 * FEC_BS2_RT16_WAVES : 8;
 }
 
+// Chunk waves (knob chunk_waves, default on): symbols wider than one column chunk are coded by
+// workgroups of kCwWaves waves over groups of up to 64 / RT blocks (k_rlc_encode_bs2 /
+// k_rlc_recover_bs2 CW), the group halved until the workgroup's LDS fits 64 KiB.
+static int cw_group(int RT, int k, int per_j, int per_block, size_t ring_bytes, uint64_t nb) {
+  if (!knob(K_CHUNK_WAVES)) return 0;
+  int g = 64 / RT;
+  while (g > 1 && (uint64_t)g > nb) g >>= 1;
+  while (g >= 1 && (size_t)g * (k * per_j + per_block) + 256 + kCwWaves * ring_bytes > 65536) g >>= 1;
+  return g;
+}
+
 template <int RT>
 static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                               uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                               hipStream_t s) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth16::enc * slotb;
+  const int CSB = FEC_BS_COEF_ROW_BYTES(RT);
+  if (int G = (W == 1 && c.nchunks > 1) ? cw_group(RT, k, CSB, 0, ring_bytes, nb) : 0) {
+    if (sbs != (uint64_t)k * L) G = 1;  // overlapping blocks (windows): one per group
+    const size_t lds = pad16((uint32_t)(G * k * CSB)) + kCwWaves * ring_bytes;
+    hipLaunchKernelGGL((k_rlc_encode_bs2<RT, true>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * kCwWaves), lds, s,
+                       src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step,
+                       interleave_groups(), slotb);
+    return;
+  }
   const int G = sbs == (uint64_t)k * L
-                    ? bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT),
-                                nb)
+                    ? bs2_group(RT, k, CSB, 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT), nb)
                     : 1;
-  const size_t lds = (size_t)W * (pad16((uint32_t)(G * k * FEC_BS_COEF_ROW_BYTES(RT))) + ring_bytes);
-  const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_encode_bs2<RT>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k, r, L,
-                     c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups(), slotb);
+  const size_t coef = pad16((uint32_t)(G * k * CSB));
+  hipLaunchKernelGGL((k_rlc_encode_bs2<RT, false>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * W),
+                     (size_t)W * (coef + ring_bytes), s, src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn,
+                     r0, G, sbs, fbn_step, interleave_groups(), slotb);
 }
 
 template <int RT>
@@ -1964,12 +2280,19 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
                                uint8_t *dst) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth16::dec * slotb;
-  const int G = bs2_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, ring_bytes,
-                          bs2_waves_per_cu(RT), nb);
-  const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + ring_bytes;
-  const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_recover_bs2<RT>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r, L,
-                     c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, slotb);
+  const int per_j = FEC_BS_COEF_ROW_BYTES(RT) + 8, per_block = kDecRec + 80;
+  if (const int G = c.nchunks > 1 ? cw_group(RT, k, per_j, per_block, ring_bytes, nb) : 0) {
+    const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + kCwWaves * ring_bytes;
+    hipLaunchKernelGGL((k_rlc_recover_bs2<RT, true>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * kCwWaves), lds, s,
+                       src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered,
+                       interleave_groups(), dst, slotb);
+    return;
+  }
+  const int G = bs2_group(RT, k, per_j, per_block, false, c.nchunks, ring_bytes, bs2_waves_per_cu(RT), nb);
+  const size_t stage = pad16((uint32_t)RecoverLds<RT>::bytes(G, k));
+  hipLaunchKernelGGL((k_rlc_recover_bs2<RT, false>), dim3(grid_for((nb + G - 1) / G)), dim3(64), stage + ring_bytes, s,
+                     src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(),
+                     dst, slotb);
 }
 
 // The ring path applies to 16-repair / 16-unknown tiles of 16-B pieces (symbol_size >= 16) and blocks
@@ -2060,7 +2383,7 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
   for (I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x; t < total; t += (I)gridDim.x * (I)blockDim.x) {
     const I b = t / Lv, c = t - b * Lv;
     uint64_t s0 = sp[2 * (uint64_t)b], s1 = sp[2 * (uint64_t)b + 1];
-    if (k < 64) { s0 &= (1ull << k) - 1; s1 = 0; } else if (k < 128) s1 &= (1ull << (k - 64)) - 1;
+    if (k < 64) { s0 &= (1ull << k) - 1; s1 = 0; } else if (k < 128) s1 &= (1ull << ((k - 64) & 63)) - 1;
     const int cur_ss = __popcll(s0) + __popcll(s1);
     const int cur_rs = (int)(rp[2 * (uint64_t)b] & 1);
     int st = FECGPU_BLOCK_NOTHING, miss = -1;
@@ -2069,7 +2392,7 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
       else {
         st = FECGPU_BLOCK_RECOVERED;
         uint64_t m0 = ~s0, m1 = ~s1;
-        if (k < 64) { m0 &= (1ull << k) - 1; m1 = 0; } else if (k < 128) m1 &= (1ull << (k - 64)) - 1;
+        if (k < 64) { m0 &= (1ull << k) - 1; m1 = 0; } else if (k < 128) m1 &= (1ull << ((k - 64) & 63)) - 1;
         miss = m1 ? 127 - __clzll(m1) : 63 - __clzll(m0);  // LAST missing index (:54-58)
       }
     }
@@ -2337,6 +2660,14 @@ int fecgpu_get_knob(const char *name, int *value) {
   return set_err(FECGPU_ERR_INVALID, "unknown knob %s", name ? name : "(null)");
 }
 
+#ifdef FEC_STAMP
+int fecgpu_debug_stamps(uint64_t out[16]) {  // diagnostic builds: the phase stamps of the last launch
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fec_stamps), 16 * sizeof(uint64_t)));
+  return FECGPU_OK;
+}
+#endif
+
 void fecgpu_host_registry_stats(uint64_t *hits, uint64_t *misses);  // host_path.hip (library-internal)
 
 void fecgpu_get_stats(fecgpu_stats_t *out) {
@@ -2366,6 +2697,25 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   int rc = check_common(src, rep, nblocks, k, r, symbol_size);
   if (rc || nblocks == 0 || r == 0) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (nblocks <= kSmallLdsMaxBlocks && knob(K_SMALL_LDS) && !knob(K_ENC_RT)) {
+    const EncLdsLayout Y((int)k, (int)r, (int)symbol_size, r <= 4 ? 4 : r <= 8 ? 8 : 16);
+    if (Y.bytes <= 65536) {
+      const uint32_t grid = (uint32_t)nblocks;
+      if (r <= 4)
+        hipLaunchKernelGGL(k_rlc_encode_lds<4>, dim3(grid), dim3(kLdsThreads), Y.bytes, s, (const uint8_t *)src,
+                           (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn);
+      else if (r <= 8)
+        hipLaunchKernelGGL(k_rlc_encode_lds<8>, dim3(grid), dim3(kLdsThreads), Y.bytes, s, (const uint8_t *)src,
+                           (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn);
+      else
+        hipLaunchKernelGGL(k_rlc_encode_lds<16>, dim3(grid), dim3(kLdsThreads), Y.bytes, s, (const uint8_t *)src,
+                           (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn);
+      HIPCHK(hipGetLastError());
+      g_stats[0]++;
+      g_stats[1] += nblocks;
+      return FECGPU_OK;
+    }
+  }
   if (int rc2 = bs_table_check()) return rc2;
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const EncTile et = pick_enc_tile(r);
@@ -2649,6 +2999,25 @@ static int decode_impl(const void *src, const void *rep, void *dst, uint64_t nbl
   if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL output buffer");
   if ((uintptr_t)dst % 4) return set_err(FECGPU_ERR_INVALID, "%s", "output buffer must be 4-byte aligned");
   const WsLayout WL = ws_layout(k, r);
+  // a few blocks with their rows in LDS: one launch, the plan beside the row fetch
+  if (nblocks <= kSmallLdsMaxBlocks && r > 0 && WL.em <= 16 && knob(K_PLAN) == 0 && knob(K_SMALL_LDS)) {
+    const DecLdsLayout Y((int)k, (int)r, (int)L, WL.em <= 4 ? 4 : WL.em <= 8 ? 8 : 16);
+    if (Y.bytes <= 65536) {
+      g_stats[2]++;
+      g_stats[3] += nblocks;
+      const int wreg = knob(K_PLAN) != PLAN_WAVE;
+#define FEC_DEC_LDS(EM)                                                                                          \
+  hipLaunchKernelGGL(k_rlc_decode_lds<EM>, dim3((uint32_t)nblocks), dim3(kLdsThreads), Y.bytes, s, (const uint8_t *)src, \
+                     (const uint8_t *)rep, nblocks, (int)k, (int)r, (int)L, fbn_base, fbn, seeds, sp, rp, status,      \
+                     recovered, (uint8_t *)dst, wreg)
+      if (WL.em <= 4) FEC_DEC_LDS(4);
+      else if (WL.em <= 8) FEC_DEC_LDS(8);
+      else FEC_DEC_LDS(16);
+#undef FEC_DEC_LDS
+      HIPCHK(hipGetLastError());
+      return FECGPU_OK;
+    }
+  }
   // the one-launch path: a few blocks, one data pass (e <= 16), the default kernels (no knob forces a
   // plan kernel or another data path)
   if (nblocks <= kDecodeSmallMaxBlocks && r > 0 && WL.em <= 16 && knob(K_PLAN) == 0 &&

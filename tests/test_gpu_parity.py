@@ -232,13 +232,35 @@ def test_small_batch_decode_one_launch(eng, oracle, k, r, L, nb):
     work, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     with eng.knob("plan", 1):  # the wave plan as its own launch, then the data pass
         _, got2, st2, rec2 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+    with eng.knob("small_lds", 0):  # the bitsliced one-launch kernel instead of the LDS-staged one
+        _, got3, st3, rec3 = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
     ref = work.copy()
     st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
     assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref)
     assert np.array_equal(st2, st_ref) and np.array_equal(rec2, rec_ref)
+    assert np.array_equal(st3, st_ref) and np.array_equal(rec3, rec_ref)
     for b in range(nb):
         for j in bits(rec[b], k):
             assert np.array_equal(got[b, j], src_h[b, j]) and np.array_equal(got2[b, j], src_h[b, j])
+            assert np.array_equal(got3[b, j], src_h[b, j])
+
+
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 1), (32, 8, 1200, 7), (1, 1, 4, 3), (5, 3, 20, 64),
+                                      (16, 20, 1204, 5), (40, 17, 600, 2), (100, 4, 100, 9), (3, 33, 52, 4),
+                                      (64, 16, 32, 12)])
+def test_small_batch_encode_lds_vs_oracle(eng, oracle, k, r, L, nb):
+    """Batches of <= 64 blocks encode with their source rows staged in LDS (a workgroup per block,
+    packed v_perm multiply); same repairs as the oracle and as the bitsliced kernels (small_lds = 0):
+    dword and 16-B row staging, repair tiles past 16, k = 1."""
+    src_h = synth_bytes(nb * k * L, 900 + k + r).reshape(nb, k, L)
+    src = to_dev(src_h)
+    want = oracle.rlc_encode_batch(src_h, r, 123)
+    for v in (1, 0):
+        with eng.knob("small_lds", v):
+            rep = torch.full((nb, r, L), 0x77, dtype=torch.uint8, device=DEV)
+            eng.rlc_encode(src, rep, k, r, L, fbn_base=123)
+            torch.cuda.synchronize()
+            assert np.array_equal(rep.cpu().numpy(), want), v
 
 
 def test_decode_zero_symbol_propagation(eng, oracle):
