@@ -165,6 +165,29 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
                            uint32_t k, uint32_t symbol_size, const uint64_t *src_present,
                            const uint64_t *rep_present, uint8_t *status, uint64_t *recovered);
 
+/* ---- Resident single-block service (the synchronous hooks) ------------------------------------
+ * One block per call, as the block framework calls fec_generate_repair_symbols / fec_recover
+ * (block_framework_sender.h:187, fec_protoops.h:246): a worker workgroup stays resident on the device
+ * and polls a page-locked mailbox, so a call costs a mailbox round trip over PCIe instead of a
+ * kernel launch.  The worker ends by itself after 20 ms without a request (and after 2 s in all);
+ * the next call relaunches it.  Every buffer must be page-locked (fecgpu_host_alloc, registered
+ * ranges); the rows are zero-copy.  Returns FECGPU_ERR_INVALID when the block does not fit the
+ * worker (e > 16 unknowns, rows beyond its LDS), a buffer is not page-locked, or knob block_svc is 0
+ * -- the caller then takes the host path.  Thread-safe (one request at a time per service). */
+typedef struct fecgpu_block_svc fecgpu_block_svc_t;
+fecgpu_block_svc_t *fecgpu_block_svc_create(int device);
+void fecgpu_block_svc_destroy(fecgpu_block_svc_t *svc);
+/* rep[i] = sum_j coef((fbn << 8) | i)[j] * src[j] for one block (k rows of symbol_size bytes) */
+int fecgpu_block_svc_rlc_encode(fecgpu_block_svc_t *svc, const void *src, void *rep, uint32_t k, uint32_t r,
+                                uint32_t symbol_size, uint32_t fbn);
+/* fecgpu_rlc_decode_seeded for one block; recovered rows go to dst (src's layout), src is only read */
+int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *svc, const void *src, const void *rep, void *dst,
+                                       uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed,
+                                       const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                                       uint64_t *recovered);
+/* worker generations launched so far (diagnostics: one per idle gap) */
+uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *svc);
+
 /* FEC frames for a batch of repair symbols, ready for packet buffers (the block framework's
  * get_repair_payload_from_queue + write_fec_frame, block_framework_sender.h:100-133,
  * protoops/write_fec_frame.c; wire format in pquic_fec_frames.h).  Frame b*r + i, at
@@ -202,7 +225,10 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
  * data path of 16-repair / 16-unknown tiles: 2 = default, 0 off), "window_sc" (window encode on the
  * shared-coefficient kernel: 0 never, 1 = default for overlapping windows, 2 wherever it applies),
  * "min_groups" (batches with fewer block groups than this stream fewer blocks per wave; default
- * 1024, 0 = the per-shape group sizes at any batch size).  Returns FECGPU_OK, or FECGPU_ERR_INVALID
+ * 1024, 0 = the per-shape group sizes at any batch size), "chunk_waves" (symbols wider than one column
+ * chunk coded by 4-wave workgroups over (block, chunk) items: 1 = default, 0 one wave per group),
+ * "small_lds" (batches of <= 64 blocks with their rows staged in LDS: 1 = default, 0 the bitsliced
+ * kernels), "block_svc" (the resident single-block service: 1 = default, 0 refused).  Returns FECGPU_OK, or FECGPU_ERR_INVALID
  * for an unknown name or a value outside its range. */
 int fecgpu_set_knob(const char *name, int value);
 int fecgpu_get_knob(const char *name, int *value);

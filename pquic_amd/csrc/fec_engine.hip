@@ -48,10 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_CHUNK_WAVES, K_SMALL_LDS, K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
-                                           "small_lds"};
+                                           "small_lds", "block_svc"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -86,6 +86,9 @@ static void knobs_from_env() {
   // batches of <= kSmallLdsMaxBlocks blocks: rows staged in LDS by a workgroup per block (1) or the
   // bitsliced one-wave-per-block kernels (0)
   g_knob[K_SMALL_LDS] = num(getenv("FECGPU_SMALL_LDS"), 1) != 0;
+  // fecgpu_block_svc_*: the resident worker serves requests (1) or every call returns
+  // FECGPU_ERR_INVALID so the caller takes the launch path (0)
+  g_knob[K_BLOCK_SVC] = num(getenv("FECGPU_BLOCK_SVC"), 1) != 0;
 }
 
 static inline int knob(KnobId id) {
@@ -1680,46 +1683,53 @@ struct EncLdsLayout {
   }
 };
 
+// One block's encode with its rows staged in LDS, by all kLdsThreads threads (src_b / rep_b: the
+// block's k source rows and r repair rows, L bytes each).
 template <int RT>
-__global__ __launch_bounds__(kLdsThreads) void k_rlc_encode_lds(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
-                                                                uint64_t nblocks, int k, int r, int L, uint32_t fbn_base,
-                                                                const uint32_t *fbn) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+__device__ __forceinline__ void encode_block_lds(uint8_t *lds, const uint8_t *src_b, uint8_t *rep_b, int k, int r,
+                                                 int L, uint32_t f) {
   const EncLdsLayout Y(k, r, L, RT);
   const int kpad = (int)pad16((uint32_t)k), Lp = (int)pad16((uint32_t)L), Lw = L >> 2;
   uint8_t *C = lds + Y.coef;
   const LdsTabs T{reinterpret_cast<uint4 *>(lds + Y.t01), reinterpret_cast<uint32_t *>(lds + Y.t2)};
   const uint32_t *rows = reinterpret_cast<const uint32_t *>(lds + Y.rows);
-  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    __syncthreads();
-    FEC_STAMP_AT(5);
-    if (threadIdx.x < 64) {  // wave 0: the TinyMT32 rows of repairs i (get_coefs, rlc_fec_scheme_generate_gf256.c:9-17)
-      const uint32_t f = block_fbn(b, fbn_base, fbn);
-      for (int i = (int)threadIdx.x; i < r; i += 64) {
-        Tmt t;
-        tmt_init(t, rlc_seed(f, (uint32_t)i));
-        for (int j = 0; j < k; j++) C[i * kpad + j] = tmt_coef(t);
-      }
-    } else {
-      stage_rows_lds(lds + Y.rows, src + b * (uint64_t)k * L, k, L, Lp, 64);
+  __syncthreads();
+  FEC_STAMP_AT(5);
+  if (threadIdx.x < 64) {  // wave 0: the TinyMT32 rows of repairs i (get_coefs, rlc_fec_scheme_generate_gf256.c:9-17)
+    for (int i = (int)threadIdx.x; i < r; i += 64) {
+      Tmt t;
+      tmt_init(t, rlc_seed(f, (uint32_t)i));
+      for (int j = 0; j < k; j++) C[i * kpad + j] = tmt_coef(t);
     }
-    uint32_t *rb = reinterpret_cast<uint32_t *>(rep + b * (uint64_t)r * L);
-    for (int i0 = 0; i0 < r; i0 += RT) {  // tiles of RT repairs
-      const int no = r - i0 < RT ? r - i0 : RT;
-      __syncthreads();
-      if (i0 == 0) FEC_STAMP_AT(6);
-      build_tabs<RT>(T, C, kpad, i0, no, k);
-      __syncthreads();
-      lds_mac_words<RT>(T, no, k, Lw, rows, Lp >> 2, [&](int i, int w, uint32_t v) {
-        __builtin_nontemporal_store(v, rb + (size_t)(i0 + i) * Lw + w);
-      });
-    }
-#ifdef FEC_STAMP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    FEC_STAMP_AT(7);
+  } else {
+    stage_rows_lds(lds + Y.rows, src_b, k, L, Lp, 64);
   }
+  uint32_t *rb = reinterpret_cast<uint32_t *>(rep_b);
+  for (int i0 = 0; i0 < r; i0 += RT) {  // tiles of RT repairs
+    const int no = r - i0 < RT ? r - i0 : RT;
+    __syncthreads();
+    if (i0 == 0) FEC_STAMP_AT(6);
+    build_tabs<RT>(T, C, kpad, i0, no, k);
+    __syncthreads();
+    lds_mac_words<RT>(T, no, k, Lw, rows, Lp >> 2, [&](int i, int w, uint32_t v) {
+      __builtin_nontemporal_store(v, rb + (size_t)(i0 + i) * Lw + w);
+    });
+  }
+#ifdef FEC_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  FEC_STAMP_AT(7);
+}
+
+template <int RT>
+__global__ __launch_bounds__(kLdsThreads) void k_rlc_encode_lds(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
+                                                                uint64_t nblocks, int k, int r, int L, uint32_t fbn_base,
+                                                                const uint32_t *fbn) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    encode_block_lds<RT>(lds, src + b * (uint64_t)k * L, rep + b * (uint64_t)r * L, k, r, L,
+                         block_fbn(b, fbn_base, fbn));
 }
 
 struct DecLdsLayout {
@@ -1735,7 +1745,67 @@ struct DecLdsLayout {
   }
 };
 
-// e <= EM unknowns per block (one pass); the zero/undetermined rule runs at the end (thread 0).
+// One block's decode (block b of the mask / seed / status arrays; src_b, rep_b, dst_b: its rows) with
+// its rows staged in LDS, by all kLdsThreads threads; e <= EM unknowns (one pass), the zero /
+// undetermined rule at the end (thread 0).
+template <int EM>
+__device__ __forceinline__ void decode_block_lds(uint8_t *lds, uint64_t b, const uint8_t *src_b, const uint8_t *rep_b,
+                                                 uint8_t *dst_b, int k, int r, int L, uint32_t fbn_base,
+                                                 const uint32_t *fbn, const uint32_t *seeds, const uint64_t *sp,
+                                                 const uint64_t *rp, uint8_t *status, uint64_t *recovered, int wreg) {
+  const DecLdsLayout Y(k, r, L, EM);
+  const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
+  const int Lp = (int)pad16((uint32_t)L), Lw = L >> 2;
+  uint8_t *h = lds + Y.rec;
+  uint32_t *nzword = reinterpret_cast<uint32_t *>(lds + Y.nz);
+  const LdsTabs T{reinterpret_cast<uint4 *>(lds + Y.t01), reinterpret_cast<uint32_t *>(lds + Y.t2)};
+  uint32_t *rows = reinterpret_cast<uint32_t *>(lds + Y.rows);
+  __syncthreads();
+  if (threadIdx.x < 64) {  // wave 0: the plan (its record lands in LDS: a base that puts block b's there)
+    FEC_STAMP_AT(0);
+    plan_load_tables(lds);
+    plan_wave_any<false>(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, h - b * (uint64_t)WL.stride, lds);
+    if (threadIdx.x == 0) *nzword = 0;
+  } else {  // waves 1-7: all k source and r repair rows of the block (absent ones are never read)
+    stage_rows_lds(lds + Y.rows, src_b, k, L, Lp, 64);
+    stage_rows_lds(lds + Y.rows + k * Lp, rep_b, r, L, Lp, 64);
+  }
+  __syncthreads();
+  FEC_STAMP_AT(3);
+  const int st = h[0], n = h[1];
+  if (st == FECGPU_BLOCK_RECOVERED) {
+    // input j is source j, or for a missing source the repair its slot names: copy those repair rows
+    // over the missing sources' rows, so input j is LDS row j
+    const int Lq = Lp >> 2;
+    for (int x = threadIdx.x; x < n * Lq; x += kLdsThreads) {
+      const int u = x / Lq, c = x - u * Lq, j = h[WL.off_unk + u];
+      rows[j * Lq + c] = rows[(k + (h[WL.off_slot + j] & 0x7f)) * Lq + c];
+    }
+    build_tabs<EM>(T, h + WL.off_D, k, 0, n, k);
+    __syncthreads();
+    uint32_t *db = reinterpret_cast<uint32_t *>(dst_b);
+    uint32_t nzm = 0;
+    lds_mac_words<EM>(T, n, k, Lw, rows, Lq, [&](int u, int w, uint32_t v) {
+      __builtin_nontemporal_store(v, db + (size_t)h[WL.off_unk + u] * Lw + w);
+      nzm |= (uint32_t)(v != 0) << u;
+    });
+    if (nzm) atomicOr(nzword, nzm);
+  }
+  __syncthreads();
+  FEC_STAMP_AT(4);
+  if (threadIdx.x == 0) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (rlc_finalize_block)
+    uint64_t m0 = 0, m1 = 0;
+    if (st == FECGPU_BLOCK_RECOVERED) {
+      uint8_t nzf[16];
+      for (int u = 0; u < 16; u++) nzf[u] = (uint8_t)((*nzword >> u) & 1u);
+      rlc_finalize_block(h, WL, nzf, m0, m1);
+    }
+    status[b] = (uint8_t)st;
+    recovered[2 * b] = m0;
+    recovered[2 * b + 1] = m1;
+  }
+}
+
 template <int EM>
 __global__ __launch_bounds__(kLdsThreads) void k_rlc_decode_lds(const uint8_t *__restrict__ src,
                                                                 const uint8_t *__restrict__ rep, uint64_t nblocks, int k,
@@ -1744,57 +1814,103 @@ __global__ __launch_bounds__(kLdsThreads) void k_rlc_decode_lds(const uint8_t *_
                                                                 const uint64_t *rp, uint8_t *status, uint64_t *recovered,
                                                                 uint8_t *dst, int wreg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const DecLdsLayout Y(k, r, L, EM);
-  const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
-  const int Lp = (int)pad16((uint32_t)L), Lw = L >> 2;
-  uint8_t *h = lds + Y.rec;
-  uint32_t *nzword = reinterpret_cast<uint32_t *>(lds + Y.nz);
-  const LdsTabs T{reinterpret_cast<uint4 *>(lds + Y.t01), reinterpret_cast<uint32_t *>(lds + Y.t2)};
-  uint32_t *rows = reinterpret_cast<uint32_t *>(lds + Y.rows);
-  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    __syncthreads();
-    if (threadIdx.x < 64) {  // wave 0: the plan (its record lands in LDS: a base that puts block b's there)
-      FEC_STAMP_AT(0);
-      plan_load_tables(lds);
-      plan_wave_any<false>(wreg, b, k, r, fbn_base, fbn, seeds, sp, rp, h - b * (uint64_t)WL.stride, lds);
-      if (threadIdx.x == 0) *nzword = 0;
-    } else {  // waves 1-7: all k source and r repair rows of the block (absent ones are never read)
-      stage_rows_lds(lds + Y.rows, src + b * (uint64_t)k * L, k, L, Lp, 64);
-      stage_rows_lds(lds + Y.rows + k * Lp, rep + b * (uint64_t)r * L, r, L, Lp, 64);
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    decode_block_lds<EM>(lds, b, src + b * (uint64_t)k * L, rep + b * (uint64_t)r * L, dst + b * (uint64_t)k * L, k, r,
+                         L, fbn_base, fbn, seeds, sp, rp, status, recovered, wreg);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Resident block service (fecgpu_block_svc_*, the synchronous hooks): one workgroup of kLdsThreads
+// threads stays resident and polls a page-locked mailbox, so a one-block call costs a mailbox
+// round trip over PCIe instead of a kernel launch and its completion signal.  Requests are the
+// LDS-staged single-block encode / decode above on page-locked buffers.  The kernel always ends:
+// on the quit flag, after `idle_ticks` without a request, or after `life_ticks` in all
+// (s_memrealtime, 100 MHz); the host relaunches it for the next request.
+// ---------------------------------------------------------------------------------------------
+// The mailbox: the request (everything a block needs beside its rows, so the worker fetches it with
+// one parallel load: wave 0's lanes read 16 B each) then the device-written words.
+constexpr int kSvcMaxR = 128;
+struct alignas(64) BlockSvcReq {
+  uint64_t seq;                     // request number, written last by the host (release)
+  uint32_t op, k, r, L, fbn, wreg;  // op 1 = RLC encode, 2 = RLC decode with per-repair seeds
+  uint64_t src, rep, dst;           // device addresses of the block's rows (page-locked host memory)
+  uint64_t sp[2], rp[2];            // presence masks (decode)
+  uint32_t seeds[kSvcMaxR];         // the repairs' FPID seeds (decode)
+};
+static_assert(sizeof(BlockSvcReq) % 16 == 0 && sizeof(BlockSvcReq) / 16 <= 64, "one 16-B load per lane of a wave");
+struct alignas(64) BlockSvcMailbox {
+  BlockSvcReq req;
+  uint64_t done;                    // device: last request number finished (release)
+  uint64_t recovered[2];            // device: decode outputs
+  uint32_t status, pad0;
+  uint64_t quit;                    // host: 1 = end the worker
+  uint64_t launches;                // device: worker generations started (diagnostics)
+};
+
+__device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, uint64_t idle_ticks,
+                                                           uint64_t life_ticks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ BlockSvcReq R;
+  __shared__ int go;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_last = t_start, done = 0;
+  if (threadIdx.x == 0) {
+    done = sys_load(&mb->done);
+    __hip_atomic_fetch_add(&mb->launches, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int g = 0;
+      for (;;) {
+        if (sys_load(&mb->req.seq) != done) {
+          g = 1;
+          break;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (sys_load(&mb->quit) || now - t_last > idle_ticks || now - t_start > life_ticks) {
+          g = -1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      go = g;
     }
     __syncthreads();
-    FEC_STAMP_AT(3);
-    const int st = h[0], n = h[1];
-    if (st == FECGPU_BLOCK_RECOVERED) {
-      // input j is source j, or for a missing source the repair its slot names: copy those repair rows
-      // over the missing sources' rows, so input j is LDS row j
-      const int Lq = Lp >> 2;
-      for (int x = threadIdx.x; x < n * Lq; x += kLdsThreads) {
-        const int u = x / Lq, c = x - u * Lq, j = h[WL.off_unk + u];
-        rows[j * Lq + c] = rows[(k + (h[WL.off_slot + j] & 0x7f)) * Lq + c];
-      }
-      build_tabs<EM>(T, h + WL.off_D, k, 0, n, k);
-      __syncthreads();
-      uint32_t *db = reinterpret_cast<uint32_t *>(dst + b * (uint64_t)k * L);
-      uint32_t nzm = 0;
-      lds_mac_words<EM>(T, n, k, Lw, rows, Lq, [&](int u, int w, uint32_t v) {
-        __builtin_nontemporal_store(v, db + (size_t)h[WL.off_unk + u] * Lw + w);
-        nzm |= (uint32_t)(v != 0) << u;
-      });
-      if (nzm) atomicOr(nzword, nzm);
+    if (go < 0) break;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // no stale cached copy of the last request or its rows
+    if (threadIdx.x < sizeof(BlockSvcReq) / 16) {  // the whole request in one round trip (after the acquire)
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      reinterpret_cast<v4u *>(&R)[threadIdx.x] =
+          __builtin_nontemporal_load(reinterpret_cast<const v4u *>(&mb->req) + threadIdx.x);
     }
     __syncthreads();
-    FEC_STAMP_AT(4);
-    if (threadIdx.x == 0) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (rlc_finalize_block)
-      uint64_t m0 = 0, m1 = 0;
-      if (st == FECGPU_BLOCK_RECOVERED) {
-        uint8_t nzf[16];
-        for (int u = 0; u < 16; u++) nzf[u] = (uint8_t)((*nzword >> u) & 1u);
-        rlc_finalize_block(h, WL, nzf, m0, m1);
-      }
-      status[b] = (uint8_t)st;
-      recovered[2 * b] = m0;
-      recovered[2 * b + 1] = m1;
+    const int k = (int)R.k, r = (int)R.r, L = (int)R.L;
+    const uint32_t em = (uint32_t)(k < r ? k : r);
+    if (R.op == 1) {
+      uint8_t *src = (uint8_t *)R.src, *rep = (uint8_t *)R.rep;
+      if (r <= 4) encode_block_lds<4>(lds, src, rep, k, r, L, R.fbn);
+      else if (r <= 8) encode_block_lds<8>(lds, src, rep, k, r, L, R.fbn);
+      else encode_block_lds<16>(lds, src, rep, k, r, L, R.fbn);
+    } else {
+      const uint8_t *src = (const uint8_t *)R.src, *rep = (const uint8_t *)R.rep;
+      uint8_t *dst = (uint8_t *)R.dst;
+      uint8_t *st = reinterpret_cast<uint8_t *>(&mb->status);
+      uint64_t *rec = mb->recovered;
+      // masks and seeds from the LDS copy of the request
+      if (em <= 4) decode_block_lds<4>(lds, 0, src, rep, dst, k, r, L, 0, nullptr, R.seeds, R.sp, R.rp, st, rec, R.wreg);
+      else if (em <= 8) decode_block_lds<8>(lds, 0, src, rep, dst, k, r, L, 0, nullptr, R.seeds, R.sp, R.rp, st, rec, R.wreg);
+      else decode_block_lds<16>(lds, 0, src, rep, dst, k, r, L, 0, nullptr, R.seeds, R.sp, R.rp, st, rec, R.wreg);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave's outputs reach host memory first
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      done = R.seq;
+      __hip_atomic_store(&mb->done, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      t_last = __builtin_amdgcn_s_memrealtime();
     }
   }
 }
@@ -3124,6 +3240,165 @@ int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, ui
   }
   HIPCHK(hipGetLastError());
   return FECGPU_OK;
+}
+
+// ---- resident block service (k_block_svc) ----
+struct fecgpu_block_svc {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;          // recorded after each worker launch: complete once it has ended
+  BlockSvcMailbox *mb = nullptr;    // page-locked, coherent
+  BlockSvcMailbox *mb_dev = nullptr;
+  uint64_t seq = 0;
+  bool launched = false;
+  std::mutex mu;
+};
+
+// worker lifetime: ends after 20 ms without a request (the next call relaunches it) and after 2 s
+// in all, so no launch outlives its caller by more than that (s_memrealtime: 100 MHz)
+constexpr uint64_t kSvcIdleTicks = 2000000, kSvcLifeTicks = 200000000;
+constexpr uint32_t kSvcLds = 60 * 1024;  // dynamic LDS of the worker (the mailbox copy is static)
+
+fecgpu_block_svc_t *fecgpu_block_svc_create(int device) {
+  if (fecgpu_init(device) != FECGPU_OK) return nullptr;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
+  auto *v = new fecgpu_block_svc;
+  v->device = device;
+  bool ok = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&v->ev, hipEventDisableTiming) == hipSuccess &&
+            hipHostMalloc((void **)&v->mb, sizeof(BlockSvcMailbox), hipHostMallocDefault) == hipSuccess;
+  if (ok) {
+    memset(v->mb, 0, sizeof(BlockSvcMailbox));
+    ok = hipHostGetDevicePointer((void **)&v->mb_dev, v->mb, 0) == hipSuccess &&
+         hipFuncSetAttribute((const void *)k_block_svc, hipFuncAttributeMaxDynamicSharedMemorySize, kSvcLds) ==
+             hipSuccess;
+  }
+  (void)hipSetDevice(cur);
+  if (!ok) {
+    (void)hipGetLastError();
+    fecgpu_block_svc_destroy(v);
+    return nullptr;
+  }
+  return v;
+}
+
+void fecgpu_block_svc_destroy(fecgpu_block_svc_t *v) {
+  if (!v) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(v->device);
+  if (v->mb) __atomic_store_n(&v->mb->quit, 1ull, __ATOMIC_RELEASE);
+  if (v->launched) (void)hipEventSynchronize(v->ev);  // the worker sees quit within a poll
+  if (v->ev) (void)hipEventDestroy(v->ev);
+  if (v->stream) (void)hipStreamDestroy(v->stream);
+  if (v->mb) (void)hipHostFree(v->mb);
+  (void)hipSetDevice(cur);
+  delete v;
+}
+
+// (re)launch the worker unless one is running
+static int svc_ensure(fecgpu_block_svc_t *v) {
+  if (v->launched && hipEventQuery(v->ev) == hipErrorNotReady) return FECGPU_OK;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(k_block_svc, dim3(1), dim3(kLdsThreads), kSvcLds, v->stream, v->mb_dev, kSvcIdleTicks,
+                     kSvcLifeTicks);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(v->ev, v->stream));
+  v->launched = true;
+  return FECGPU_OK;
+}
+
+// Posts the request already written into the mailbox and waits for its completion.
+static int svc_run(fecgpu_block_svc_t *v) {
+  const uint64_t seq = ++v->seq;
+  __atomic_store_n(&v->mb->req.seq, seq, __ATOMIC_RELEASE);
+  if (int rc = svc_ensure(v)) return rc;
+  for (uint64_t spin = 1;; spin++) {
+    if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+    __builtin_ia32_pause();
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipEventQuery(v->ev);
+      if (q == hipErrorNotReady) continue;
+      if (q != hipSuccess) return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(q));
+      // the worker ended (idle limit reached as the request was posted): the next one serves it
+      if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+      if (int rc = svc_ensure(v)) return rc;
+    }
+  }
+}
+
+int fecgpu_host_device_address(const void *p, size_t bytes, uint64_t *dev);  // host_path.hip
+
+static bool svc_addr(const void *p, size_t n, uint64_t *d) { return fecgpu_host_device_address(p, n, d) == FECGPU_OK; }
+
+int fecgpu_block_svc_rlc_encode(fecgpu_block_svc_t *v, const void *src, void *rep, uint32_t k, uint32_t r,
+                                uint32_t symbol_size, uint32_t fbn) {
+  if (!v || !knob(K_BLOCK_SVC)) return FECGPU_ERR_INVALID;
+  if (int rc = check_common(src, rep, 1, k, r, symbol_size)) return rc;
+  if (!r) return FECGPU_OK;
+  const int OT = r <= 4 ? 4 : r <= 8 ? 8 : 16;
+  if (EncLdsLayout((int)k, (int)r, (int)symbol_size, OT).bytes > kSvcLds)
+    return set_err(FECGPU_ERR_INVALID, "%s", "block service: block too large for its LDS");
+  uint64_t ds, dr;
+  if (!svc_addr(src, (size_t)k * symbol_size, &ds) || !svc_addr(rep, (size_t)r * symbol_size, &dr))
+    return set_err(FECGPU_ERR_INVALID, "%s", "block service: buffers must be page-locked");
+  std::lock_guard<std::mutex> g(v->mu);
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  if (cur != v->device) HIPCHK(hipSetDevice(v->device));
+  BlockSvcReq *m = &v->mb->req;
+  m->op = 1; m->k = k; m->r = r; m->L = symbol_size; m->fbn = fbn & 0xffffffu;
+  m->src = ds; m->rep = dr;
+  const int rc = svc_run(v);
+  if (cur != v->device) (void)hipSetDevice(cur);
+  if (!rc) {
+    g_stats[0]++;
+    g_stats[1]++;
+  }
+  return rc;
+}
+
+int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *v, const void *src, const void *rep, void *dst, uint32_t k,
+                                       uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed,
+                                       const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                                       uint64_t *recovered) {
+  if (!v || !knob(K_BLOCK_SVC)) return FECGPU_ERR_INVALID;
+  if (int rc = check_common(src, rep, 1, k, r, symbol_size)) return rc;
+  if (!dst || !rep_seed || !src_present || !rep_present || !status || !recovered || r == 0)
+    return set_err(FECGPU_ERR_INVALID, "%s", "block service: NULL argument or r == 0");
+  const uint32_t em = k < r ? k : r;
+  if (em > 16 || r > (uint32_t)kSvcMaxR || knob(K_PLAN) != 0 ||
+      DecLdsLayout((int)k, (int)r, (int)symbol_size, em <= 4 ? 4 : em <= 8 ? 8 : 16).bytes > kSvcLds)
+    return set_err(FECGPU_ERR_INVALID, "%s", "block service: block too large for its LDS");
+  uint64_t a[3];
+  if (!svc_addr(src, (size_t)k * symbol_size, &a[0]) || !svc_addr(rep, (size_t)r * symbol_size, &a[1]) ||
+      !svc_addr(dst, (size_t)k * symbol_size, &a[2]))
+    return set_err(FECGPU_ERR_INVALID, "%s", "block service: symbol rows must be page-locked");
+  std::lock_guard<std::mutex> g(v->mu);
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  if (cur != v->device) HIPCHK(hipSetDevice(v->device));
+  BlockSvcReq *m = &v->mb->req;
+  m->op = 2; m->k = k; m->r = r; m->L = symbol_size; m->fbn = 0; m->wreg = knob(K_PLAN) != PLAN_WAVE;
+  m->src = a[0]; m->rep = a[1]; m->dst = a[2];
+  m->sp[0] = src_present[0]; m->sp[1] = src_present[1];
+  m->rp[0] = rep_present[0]; m->rp[1] = rep_present[1];
+  memcpy(m->seeds, rep_seed, (size_t)r * 4);
+  const int rc = svc_run(v);
+  if (cur != v->device) (void)hipSetDevice(cur);
+  if (!rc) {
+    *status = (uint8_t)v->mb->status;
+    recovered[0] = v->mb->recovered[0];
+    recovered[1] = v->mb->recovered[1];
+    g_stats[2]++;
+    g_stats[3]++;
+  }
+  return rc;
+}
+
+uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *v) {
+  return v && v->mb ? __atomic_load_n(&v->mb->launches, __ATOMIC_ACQUIRE) : 0;
 }
 
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream) {

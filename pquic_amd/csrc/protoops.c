@@ -37,6 +37,10 @@ int g_fec_bound;
 pquic_fec_protoop_stats_t g_fec_stats;
 static int g_device;
 static fecgpu_host_ctx_t *g_ctx;
+/* the resident single-block service (fecgpu_block_svc_*): one block per call without a kernel launch;
+ * calls it refuses (block too large for it, knob off) take the host path */
+static fecgpu_block_svc_t *g_svc;
+static int g_svc_failed;
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 
 /* Per-call staging, page-locked (fecgpu_host_alloc) and grown on demand: the engine's host path
@@ -64,6 +68,11 @@ int pquic_fec_bind_host(const pquic_fec_host_api_t *api, int device) {
         fecgpu_host_ctx_destroy(g_ctx);
         g_ctx = NULL;
     }
+    if (g_svc && g_device != device) {
+        fecgpu_block_svc_destroy(g_svc);
+        g_svc = NULL;
+    }
+    g_svc_failed = 0;
     g_device = device;
     pthread_mutex_unlock(&g_mu);
     return g_fec_bound ? 0 : -1;
@@ -92,6 +101,21 @@ int pquic_fec_layout(uint64_t out[8]) {
 static fecgpu_host_ctx_t *ctx(void) {
     if (!g_ctx) g_ctx = fecgpu_host_ctx_create(g_device, 1, 1u << 20);
     return g_ctx;
+}
+
+/* the worker ends within a poll of the quit flag; at exit it must not outlive the process's HIP state */
+static void svc_atexit(void) {
+    pthread_mutex_lock(&g_mu);
+    fecgpu_block_svc_destroy(g_svc);
+    g_svc = NULL;
+    pthread_mutex_unlock(&g_mu);
+}
+
+static fecgpu_block_svc_t *svc(void) {
+    static int at_exit;
+    if (!g_svc && !g_svc_failed && !(g_svc = fecgpu_block_svc_create(g_device))) g_svc_failed = 1;
+    if (g_svc && !at_exit) at_exit = !atexit(svc_atexit);
+    return g_svc;
 }
 
 static int grow_pinned(uint8_t **p, size_t *cap, size_t need) {
@@ -159,8 +183,11 @@ static protoop_arg_t generate(picoquic_cnx_t *cnx, int xor_scheme) {
     fecgpu_host_ctx_t *c = rc ? NULL : ctx();
     if (c) {
         fec_generate_stage(fb, g_src, L);
-        rc = xor_scheme ? fecgpu_xor_encode_host(c, g_src, g_rep, 1, (uint32_t)k, L)
-                        : fecgpu_rlc_encode_host(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, fbn, NULL);
+        fecgpu_block_svc_t *v = xor_scheme ? NULL : svc();
+        rc = v ? fecgpu_block_svc_rlc_encode(v, g_src, g_rep, (uint32_t)k, (uint32_t)r, L, fbn) : FECGPU_ERR_INVALID;
+        if (rc == FECGPU_ERR_INVALID)
+            rc = xor_scheme ? fecgpu_xor_encode_host(c, g_src, g_rep, 1, (uint32_t)k, L)
+                            : fecgpu_rlc_encode_host(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, fbn, NULL);
     } else {
         rc = -1;
     }
@@ -205,9 +232,14 @@ static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
         a->st = FECGPU_BLOCK_NOTHING;
         a->rec[0] = a->rec[1] = 0;
         fec_recover_stage(fb, xor_scheme, maxl, g_src, g_rep, L, a->sp, a->rp, a->seeds);
-        rc = xor_scheme ? fecgpu_xor_decode_host(c, g_src, g_rep, 1, (uint32_t)k, L, a->sp, a->rp, &a->st, a->rec)
-                        : fecgpu_rlc_decode_host_seeded(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, a->seeds,
-                                                        a->sp, a->rp, &a->st, a->rec);
+        fecgpu_block_svc_t *v = xor_scheme ? NULL : svc();
+        rc = v ? fecgpu_block_svc_rlc_decode_seeded(v, g_src, g_rep, g_src, (uint32_t)k, (uint32_t)r, L, a->seeds,
+                                                    a->sp, a->rp, &a->st, a->rec)
+               : FECGPU_ERR_INVALID;
+        if (rc == FECGPU_ERR_INVALID)
+            rc = xor_scheme ? fecgpu_xor_decode_host(c, g_src, g_rep, 1, (uint32_t)k, L, a->sp, a->rp, &a->st, a->rec)
+                            : fecgpu_rlc_decode_host_seeded(c, g_src, g_rep, 1, (uint32_t)k, (uint32_t)r, L, a->seeds,
+                                                            a->sp, a->rp, &a->st, a->rec);
     } else {
         rc = -1;
     }

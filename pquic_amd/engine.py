@@ -70,6 +70,13 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_host_register.argtypes = [v, sz]
     L.fecgpu_host_unregister.argtypes = [v]
     L.fecgpu_host_device_address.argtypes = [v, sz, C.POINTER(u64)]
+    L.fecgpu_block_svc_create.argtypes = [C.c_int]
+    L.fecgpu_block_svc_create.restype = v
+    L.fecgpu_block_svc_destroy.argtypes = [v]
+    L.fecgpu_block_svc_rlc_encode.argtypes = [v, v, v, u32, u32, u32, u32]
+    L.fecgpu_block_svc_rlc_decode_seeded.argtypes = [v, v, v, v, u32, u32, u32, v, v, v, v, v]
+    L.fecgpu_block_svc_launches.argtypes = [v]
+    L.fecgpu_block_svc_launches.restype = u64
     if not private:
         _lib = L
     return L

@@ -1,0 +1,132 @@
+"""The resident single-block service (fecgpu_block_svc_*, include/fecgpu.h), which serves the
+synchronous hooks one block per call (block_framework_sender.h:187, fec_protoops.h:246) without a
+kernel launch: bytes against the oracle, the worker's idle exit and relaunch, and its refusals."""
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle_py import Oracle, synth_bytes  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    from pquic_amd import load_library
+    return load_library()
+
+
+@pytest.fixture(scope="module")
+def svc(lib):
+    v = lib.fecgpu_block_svc_create(0)
+    assert v
+    yield v
+    lib.fecgpu_block_svc_destroy(v)
+
+
+def pinned(a):
+    t = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+    return t, t.numpy()
+
+
+def _decode_case(oracle, k, r, L, seed, rng):
+    src = synth_bytes(k * L, seed).reshape(1, k, L)
+    seeds = np.array([(int(rng.integers(0, 1 << 24)) << 8) | i for i in range(r)], np.uint32)
+    mul, _ = oracle.gf_tables()
+    rep = np.zeros((1, r, L), np.uint8)
+    for i in range(r):
+        c = oracle.coefs(int(seeds[i]), k)
+        for j in range(k):
+            rep[0, i] ^= mul[c[j]][src[0, j]]
+    e = int(rng.integers(0, min(k, r) + 1))
+    miss = rng.choice(k, e, replace=False)
+    sp = np.zeros((1, 2), np.uint64)
+    rp = np.zeros((1, 2), np.uint64)
+    for j in range(k):
+        if j not in miss:
+            sp[0, j >> 6] |= np.uint64(1 << (j & 63))
+    for i in rng.choice(r, int(rng.integers(max(0, e - 1), r + 1)), replace=False):
+        rp[0, int(i) >> 6] |= np.uint64(1 << (int(i) & 63))
+    work = src.copy()
+    work[0, miss] = 0
+    return src, rep, seeds, sp, rp, work
+
+
+@pytest.mark.parametrize("k,r,L", [(16, 4, 1200), (32, 8, 1200), (5, 3, 20), (64, 16, 100), (1, 1, 4), (20, 16, 36)])
+def test_svc_encode_decode_vs_oracle(lib, svc, k, r, L):
+    o = Oracle()
+    rng = np.random.default_rng(k * 31 + r)
+    for it in range(6):
+        fbn = int(rng.integers(0, 1 << 24))
+        src = synth_bytes(k * L, 1000 + it).reshape(1, k, L)
+        ts, hs = pinned(src)
+        tr, hr = pinned(np.zeros((1, r, L), np.uint8))
+        assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, fbn) == 0
+        assert np.array_equal(hr, o.rlc_encode_batch(src, r, fbn))
+        src, rep, seeds, sp, rp, work = _decode_case(o, k, r, L, 2000 + it, rng)
+        tw, hw = pinned(work)
+        trp, _ = pinned(rep)
+        tseed, _ = pinned(seeds)
+        tsp, _ = pinned(sp.view(np.int64))
+        trpm, _ = pinned(rp.view(np.int64))
+        tst, hst = pinned(np.full(1, 0xEE, np.uint8))
+        trec, hrec = pinned(np.zeros((1, 2), np.int64))
+        assert lib.fecgpu_block_svc_rlc_decode_seeded(svc, tw.data_ptr(), trp.data_ptr(), tw.data_ptr(), k, r, L,
+                                                      tseed.data_ptr(), tsp.data_ptr(), trpm.data_ptr(),
+                                                      tst.data_ptr(), trec.data_ptr()) == 0
+        blk = [work[0, j].copy() if (int(sp[0, j >> 6]) >> (j & 63)) & 1 else None for j in range(k)]
+        reps = [rep[0, i].copy() if (int(rp[0, i >> 6]) >> (i & 63)) & 1 else None for i in range(r)]
+        st, out = o.rlc_decode_block(0, blk, reps, rep_seeds=[int(x) for x in seeds])
+        assert hst[0] == st
+        got_rec = [j for j in range(k) if (int(hrec.view(np.uint64)[0, j >> 6]) >> (j & 63)) & 1]
+        assert sorted(got_rec) == sorted(out.keys())
+        for j, row in out.items():
+            assert np.array_equal(hw[0, j, :len(row)], row)
+
+
+def test_svc_idle_exit_and_relaunch(lib, svc):
+    """The worker ends after 20 ms without a request; the next call relaunches it and is served."""
+    o = Oracle()
+    k, r, L = 16, 4, 1200
+    src = synth_bytes(k * L, 7).reshape(1, k, L)
+    ts, _ = pinned(src)
+    tr, hr = pinned(np.zeros((1, r, L), np.uint8))
+    want = o.rlc_encode_batch(src, r, 99)
+    assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, 99) == 0
+    n0 = lib.fecgpu_block_svc_launches(svc)
+    for _ in range(50):  # back to back: one worker serves them all
+        hr[:] = 0
+        assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, 99) == 0
+        assert np.array_equal(hr, want)
+    assert lib.fecgpu_block_svc_launches(svc) == n0
+    time.sleep(0.1)
+    hr[:] = 0
+    assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, 99) == 0
+    assert np.array_equal(hr, want)
+    assert lib.fecgpu_block_svc_launches(svc) == n0 + 1
+
+
+def test_svc_refusals(lib, svc):
+    """Pageable buffers and blocks too large for the worker are refused (FECGPU_ERR_INVALID = -1),
+    so the caller takes the launch path."""
+    k, r, L = 16, 4, 1200
+    src = np.zeros((1, k, L), np.uint8)  # pageable
+    rep = np.zeros((1, r, L), np.uint8)
+    assert lib.fecgpu_block_svc_rlc_encode(svc, src.ctypes.data, rep.ctypes.data, k, r, L, 0) == -1
+    ts, _ = pinned(np.zeros((1, 20, 36), np.uint8))  # 20 unknowns possible: more than one pass
+    tr, _ = pinned(np.zeros((1, 20, 36), np.uint8))
+    tm, _ = pinned(np.zeros((1, 2), np.int64))
+    tsd, _ = pinned(np.zeros(20, np.uint32))
+    tst, _ = pinned(np.zeros(1, np.uint8))
+    assert lib.fecgpu_block_svc_rlc_decode_seeded(svc, ts.data_ptr(), tr.data_ptr(), ts.data_ptr(), 20, 20, 36,
+                                                  tsd.data_ptr(), tm.data_ptr(), tm.data_ptr(), tst.data_ptr(),
+                                                  tm.data_ptr()) == -1
+    big_k, big_L = 100, 2000  # 200 KB of rows
+    ts, _ = pinned(np.zeros((1, big_k, big_L), np.uint8))
+    tr, _ = pinned(np.zeros((1, 4, big_L), np.uint8))
+    assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), big_k, 4, big_L, 0) == -1
