@@ -418,27 +418,31 @@ def pcie_legs(torch, args, dev):
 
 def batching_legs(dev_index, args):
     """§8f row 1: the block framework's blocks through the batching adapter
-    (include/pquic_fec_batch.h), end to end from host packet buffers: host staging into pinned
-    queues, PCIe, kernels, completion on the caller thread.  tools/batch_load.c plays the
-    single-threaded sender over 64 connections."""
+    (include/pquic_fec_batch.h), end to end from host packet buffers: PCIe, kernels, completion on the
+    caller thread.  tools/batch_load.c plays the single-threaded sender over 64 connections, its
+    symbols in one plugin-style memory arena.  "saturated" / "paced": the arena is registered with the
+    batcher (pquic_fec_batch_register_heap), so the kernels read sources and write repairs in place;
+    "saturated_staged": unregistered, the stager threads copy every row through pinned staging."""
     import ctypes as C
     path = os.path.join(ROOT, "tools", "libbatchload.so")
     if not os.path.exists(path):
         return {}
     lib = C.CDLL(path)
     lib.bl_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint, C.c_uint, C.c_int,
-                           C.c_double, C.POINTER(C.c_double)]
+                           C.c_double, C.c_int, C.POINTER(C.c_double)]
     legs = {}
-    for name, nblocks, batch, delay, offered in (("saturated", 200000, 4096, 2000, 0.0),
-                                                 ("paced_2GiBps", 100000, 4096, 250, 2.0)):
+    for name, nblocks, batch, delay, offered, reg in (("saturated", 200000, 4096, 2000, 0.0, 1),
+                                                      ("saturated_staged", 200000, 4096, 2000, 0.0, 0),
+                                                      ("paced_2GiBps", 100000, 4096, 250, 2.0, 1)):
         out = (C.c_double * 8)()
-        rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, out)
+        rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, reg, out)
         if rc:
             legs["batch_" + name] = {"error": rc}
             continue
         legs["batch_" + name] = {
             "k": args.k, "r": args.r, "L": args.symbol, "blocks": nblocks, "connections": 64,
             "batch_blocks": batch, "max_delay_us": delay, "offered_GiB_s": offered or None,
+            "rows": "gathered in place (registered arena)" if reg else "staged by copies",
             "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
             "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1)}
     return legs

@@ -72,6 +72,13 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
 int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t step, uint32_t k, uint32_t r,
                              uint32_t symbol_size, void *rep, void *stream);
 
+/* RLC encode with every row given by its address: src_rows[b * k + j] / rep_rows[b * r + i] are the
+ * device addresses (4-byte aligned; device memory or mapped page-locked host memory, e.g. a registered
+ * plugin arena) of source row j / repair row i of block b, each symbol_size bytes.  The tables and
+ * fbn[] must themselves be device-accessible.  Same result as fecgpu_rlc_encode on packed rows. */
+int fecgpu_rlc_encode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn, void *stream);
+
 /* XOR encode (r == 1): rep[b][0] = XOR_j src[b][j]. */
 int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k,
                       uint32_t symbol_size, void *stream);
@@ -159,6 +166,10 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *ctx, void *src, const void 
                                   uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed,
                                   const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
                                   uint64_t *recovered);
+/* fecgpu_rlc_encode_rows from the host: the row tables and fbn[] are host arrays (page-locked arrays
+ * are read in place, others are copied), the rows themselves must be device-accessible. */
+int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
+                                uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *fbn);
 int fecgpu_xor_encode_host(fecgpu_host_ctx_t *ctx, const void *src, void *rep, uint64_t nblocks,
                            uint32_t k, uint32_t symbol_size);
 int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,

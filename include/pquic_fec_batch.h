@@ -58,6 +58,14 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg);
 /* Drains (completing every queued block) and frees. */
 void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b);
 
+/* Register a host memory range that holds symbols -- a FEC plugin instance's memory arena
+ * (picoquic_internal.h:576, char memory[PLUGIN_MEMORY], carved into 2100-B slots by
+ * picoquic/memory.c:181-191, registered once after init_memory_management, memory.c:254).  It is
+ * page-locked and mapped (fecgpu_host_register) until the batcher is destroyed, and RLC generate
+ * batches then read source symbols and write repair symbols in it directly instead of copying them
+ * through staging rows.  Call before submitting.  Returns 0 or -1. */
+int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t bytes);
+
 /* Queue fec_generate_repair_symbols (xor_scheme = 0: RLC-GF(256), 1: XOR) for `fb`, whose
  * totals are set as the block framework sets them before the call
  * (block_framework_sender.h:184-185).  `now_us` starts the block's latency clock.

@@ -13,6 +13,11 @@
  *     kernels on the page-locked rows);
  *   - for generate, the stager threads copy the repair rows into the symbols allocated at
  *     submission (the caller's thread was the bound when it copied them itself).
+ * Gather (pquic_fec_batch_register_heap): once the FEC plugin's memory arena is registered, a
+ * generate job's stagers copy nothing for rows that lie in it -- they write the rows' device
+ * addresses into page-locked tables and the kernel (fecgpu_rlc_encode_rows) reads the sources and
+ * writes the repairs where the symbols are.  Rows outside a registered arena, or shorter than the
+ * block's length (the reference zero-pads them), are staged as before.
  * Finished jobs are completed on the caller's thread in poll / drain with the same finish
  * halves the synchronous operations use (fec_core.c), so a batched block ends in exactly the
  * state the protocol operation would leave it in.  The caller keeps a block unmodified until
@@ -31,7 +36,13 @@
 #include "fecgpu.h"
 
 enum { OP_GENERATE = 0, OP_RECOVER = 1 };
-enum { MAX_OPEN = 32, MAX_STAGERS = 16, STAGE_CHUNK = 256 /* blocks per staging work item */ };
+enum { MAX_OPEN = 32, MAX_STAGERS = 16, STAGE_CHUNK = 256 /* blocks per staging work item */, MAX_HEAPS = 64 };
+
+typedef struct {
+    uintptr_t base;
+    size_t size;
+    uint64_t dev;  /* device address of base */
+} heap_t;
 
 typedef struct {
     picoquic_cnx_t *cnx;
@@ -59,6 +70,12 @@ typedef struct job {
     int rc;
     int post;                      /* 1 once the engine ran: work items copy repairs out */
     uint32_t next_chunk, chunks_done;  /* staging work items claimed / finished (under the batcher lock) */
+    int gather;                    /* generate with row tables (fecgpu_rlc_encode_rows) */
+    uint64_t *srow, *rrow;         /* pinned: [cap][k] source / [cap][r] repair row device addresses */
+    size_t srow_cap, rrow_cap;
+    uint64_t src_dev, rep_dev;     /* device addresses of the staging rows */
+    uint8_t *copy;                 /* gather: block needs its repairs copied out of the staging rows */
+    uint32_t ncopy;                /* blocks flagged in copy[] (atomic while staging) */
 } job_t;
 
 struct pquic_fec_batcher {
@@ -75,10 +92,40 @@ struct pquic_fec_batcher {
     job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *post_head, *post_tail, *done_head, *done_tail;
     int inflight, stop, stagers_done;
     pquic_fec_batch_stats_t stats;
+    heap_t heaps[MAX_HEAPS];
+    int nheaps;
 };
+
+/* device address of [p, p + n) when it lies in a registered heap, else 0 */
+static uint64_t heap_dev(const pquic_fec_batcher_t *b, const void *p, size_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    for (int i = 0; i < b->nheaps; i++) {
+        const heap_t *h = &b->heaps[i];
+        if (a - h->base < h->size && n <= h->size - (a - h->base) && (a & 3) == 0) return h->dev + (a - h->base);
+    }
+    return 0;
+}
+
+int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t bytes) {
+    if (!b || !base || !bytes || b->nheaps >= MAX_HEAPS) return -1;
+    if (fecgpu_host_register(base, bytes) != FECGPU_OK) return -1;
+    uint64_t dev = 0;
+    if (fecgpu_host_device_address(base, bytes, &dev) != FECGPU_OK) {
+        fecgpu_host_unregister(base);
+        return -1;
+    }
+    pthread_mutex_lock(&b->mu);  /* stagers read the list while holding no lock: register before traffic */
+    b->heaps[b->nheaps] = (heap_t){(uintptr_t)base, bytes, dev};
+    b->nheaps++;
+    pthread_mutex_unlock(&b->mu);
+    return 0;
+}
 
 static void job_free(job_t *j) {
     if (!j) return;
+    fecgpu_host_free(j->srow);
+    fecgpu_host_free(j->rrow);
+    free(j->copy);
     fecgpu_host_free(j->src);
     fecgpu_host_free(j->rep);
     fecgpu_host_free(j->st);
@@ -128,6 +175,24 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         }
         j->seed_bytes = eb;
     }
+    /* gather tables (RLC generate with a registered heap): grown on reuse like the repair table */
+    j->gather = op == OP_GENERATE && !xor_scheme && b->nheaps > 0;
+    if (j->gather && (j->srow_cap < (size_t)cap * k || j->rrow_cap < (size_t)cap * r || !j->copy)) {
+        if (j->srow_cap < (size_t)cap * k) {
+            fecgpu_host_free(j->srow);
+            j->srow_cap = (j->srow = fecgpu_host_alloc((size_t)cap * k * 8)) ? (size_t)cap * k : 0;
+        }
+        if (j->rrow_cap < (size_t)cap * r) {
+            fecgpu_host_free(j->rrow);
+            j->rrow_cap = (j->rrow = fecgpu_host_alloc((size_t)cap * r * 8)) ? (size_t)cap * r : 0;
+        }
+        if (!j->copy) j->copy = malloc(cap);
+        if (!j->srow || !j->rrow || !j->copy) j->gather = 0;  /* staged instead */
+    }
+    if (j->gather && (fecgpu_host_device_address(j->src, sb, &j->src_dev) != FECGPU_OK ||
+                      fecgpu_host_device_address(j->rep, rb ? rb : 4, &j->rep_dev) != FECGPU_OK))
+        j->gather = 0;
+    j->ncopy = 0;
     if (op == OP_GENERATE && j->reps_cap < (size_t)cap * r) {
         pquic_repair_symbol_t **nr = realloc(j->reps, sizeof *nr * (size_t)cap * r);
         if (!nr) {
@@ -157,7 +222,9 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
 static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
     fecgpu_host_ctx_t *c = b->ctx;
     const uint32_t S = j->stride;
-    if (j->op == OP_GENERATE)
+    if (j->gather)
+        j->rc = fecgpu_rlc_encode_rows_host(c, j->srow, j->rrow, j->n, j->k, j->r, S, j->fbn);
+    else if (j->op == OP_GENERATE)
         j->rc = j->xor_scheme ? fecgpu_xor_encode_host(c, j->src, j->rep, j->n, j->k, S)
                               : fecgpu_rlc_encode_host(c, j->src, j->rep, j->n, j->k, j->r, S, 0, j->fbn);
     else
@@ -165,6 +232,44 @@ static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
                     ? fecgpu_xor_decode_host(c, j->src, j->rep, j->n, j->k, S, j->sp, j->rp, j->st, j->rec)
                     : fecgpu_rlc_decode_host_seeded(c, j->src, j->rep, j->n, j->k, j->r, S, j->seeds, j->sp, j->rp,
                                                     j->st, j->rec);
+}
+
+/* Gather: the row tables of blocks [i0, i1).  A source row is read in place when it lies in a
+ * registered heap and is as long as the block (shorter ones are zero-padded, :41-55, so they are
+ * staged); a repair row is written in place when its symbol is in a heap and as long as the stride
+ * (the kernel writes `stride` bytes), else into the staging rows and copied out after the engine. */
+static void gather_blocks(const pquic_fec_batcher_t *b, job_t *j, uint32_t i0, uint32_t i1) {
+    const uint32_t S = j->stride, k = j->k, r = j->r;
+    uint32_t ncopy = 0;
+    for (uint32_t i = i0; i < i1; i++) {
+        const entry_t *e = &j->ent[i];
+        const pquic_fec_block_t *fb = e->fb;
+        for (uint32_t x = 0; x < k; x++) {
+            const pquic_source_symbol_t *ss = fb->source_symbols[x];
+            const size_t o = ((size_t)i * k + x) * S;
+            uint64_t d = ss && ss->data_length == e->maxl ? heap_dev(b, ss->data, S) : 0;
+            if (!d) {  /* staged, zero-padded to the stride */
+                const uint16_t n = ss ? ss->data_length : 0;
+                if (n) memcpy(j->src + o, ss->data, n);
+                memset(j->src + o + n, 0, S - n);
+                d = j->src_dev + o;
+            }
+            j->srow[(size_t)i * k + x] = d;
+        }
+        uint8_t cp = 0;
+        for (uint32_t x = 0; x < r; x++) {
+            pquic_repair_symbol_t *rs = (int)x < e->nalloc ? j->reps[(size_t)i * r + x] : NULL;
+            uint64_t d = rs && e->maxl == S ? heap_dev(b, rs->data, S) : 0;
+            if (!d) {
+                d = j->rep_dev + ((size_t)i * r + x) * S;
+                cp |= rs != NULL;
+            }
+            j->rrow[(size_t)i * r + x] = d;
+        }
+        j->copy[i] = cp;
+        ncopy += cp;
+    }
+    if (ncopy) __atomic_fetch_add(&j->ncopy, ncopy, __ATOMIC_RELAXED);
 }
 
 /* Copies blocks [i0, i1) of a job into its page-locked rows (the stage halves of fec_core.c). */
@@ -187,6 +292,7 @@ static void copy_out_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     const uint32_t S = j->stride, r = j->r;
     for (uint32_t i = i0; i < i1; i++) {
         const entry_t *e = &j->ent[i];
+        if (j->gather && !j->copy[i]) continue;  /* written in place by the kernel */
         for (int x = 0; x < e->nalloc; x++)
             memcpy(j->reps[(size_t)i * r + x]->data, j->rep + ((size_t)i * r + x) * S, e->maxl);
     }
@@ -219,7 +325,9 @@ static void *stager_main(void *arg) {
         }
         pthread_mutex_unlock(&b->mu);
         const uint32_t i0 = c * STAGE_CHUNK, i1 = i0 + STAGE_CHUNK < j->n ? i0 + STAGE_CHUNK : j->n;
-        if (j->post) copy_out_blocks(j, i0, i1); else stage_blocks(j, i0, i1);
+        if (j->post) copy_out_blocks(j, i0, i1);
+        else if (j->gather) gather_blocks(b, j, i0, i1);
+        else stage_blocks(j, i0, i1);
         pthread_mutex_lock(&b->mu);
         if (++j->chunks_done == nchunks) {
             if (j->post) {
@@ -268,7 +376,7 @@ static void *worker_main(void *arg) {
         pthread_mutex_unlock(&b->mu);
         run_engine(b, j);
         pthread_mutex_lock(&b->mu);
-        if (j->op == OP_GENERATE && !j->rc) {  /* the repair rows go to their symbols on the stagers */
+        if (j->op == OP_GENERATE && !j->rc && (!j->gather || j->ncopy)) {  /* repair rows to their symbols */
             j->post = 1;
             j->next_chunk = j->chunks_done = 0;
             push(&b->post_head, &b->post_tail, j);
@@ -506,6 +614,7 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
         b->free_jobs = j->next;
         job_free(j);
     }
+    for (int i = 0; i < b->nheaps; i++) fecgpu_host_unregister((void *)b->heaps[i].base);
     fecgpu_host_ctx_destroy(b->ctx);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->cv_todo);

@@ -1564,6 +1564,65 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
                               recovered, ilv, dst, lds);
 }
 
+// Encode with the rows given by address (fecgpu_rlc_encode_rows): the batching adapter hands the
+// kernel the symbols where they lie -- the FEC plugin's registered memory arena -- instead of copying
+// them into a packed batch.  src_rows[b * k + j] / rep_rows[b * r + i]: device addresses of source row
+// j / repair row i of block b.  Same data body as the recover pass (input addresses and output records
+// staged in LDS per group), with the coefficients from TinyMT32 as in k_rlc_encode_bs.
+template <int RT, int VEC>
+__global__ __launch_bounds__(64) void k_rlc_encode_rows(const uint64_t *__restrict__ src_rows,
+                                                        const uint64_t *__restrict__ rep_rows, uint64_t nblocks, int k,
+                                                        int r, int L, int nchunks, int chunk_bytes, uint32_t fbn_base,
+                                                        const uint32_t *fbn, int r0, int G) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  RecoverLds<RT> S(lds, G, k);
+  constexpr int CSB = RecoverLds<RT>::CSB;
+  const int lane = threadIdx.x;
+  const int rt = r - r0 < RT ? r - r0 : RT;
+  const uint64_t NG = (nblocks + G - 1) / G;
+  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+    const uint64_t b0 = q * G;
+    const int ng = nblocks - b0 < (uint64_t)G ? (int)(nblocks - b0) : G;
+    __syncthreads();
+    if (lane < ng * RT) {  // TinyMT32 rows (get_coefs, rlc_fec_scheme_generate_gf256.c:9-17): lane -> (block g, repair)
+      const int g = lane / RT, i = lane % RT;
+      uint16_t *row0 = reinterpret_cast<uint16_t *>(S.coef + (size_t)g * k * CSB);
+      uint16_t *row = row0 + FEC_BS_FIELD_SLOT(RT, i);
+      if (i < rt) {
+        Tmt t;
+        tmt_init(t, rlc_seed(block_fbn(b0 + g, fbn_base, fbn), (uint32_t)(r0 + i)));
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD(tmt_coef(t), i);
+      } else {
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;  // ends the chain: repair i is not live
+      }
+      if constexpr (RT < 4) {
+        if (i == 0)
+          for (int j = 0; j < k; j++)
+            for (int x = RT; x < 4; x++) row0[j * (CSB / 2) + FEC_BS_FIELD_SLOT(RT, x)] = 0;
+      }
+    }
+    for (int x = lane; x < ng * k; x += 64) S.intab[x] = src_rows[b0 * k + x];
+    for (int x = lane; x < ng * 16; x += 64) {
+      const int t = x >> 4, u = x & 15;
+      uint8_t *rc = S.rec + (size_t)t * kDecRec;
+      rc[kDecRecNz + u] = 0;
+      if (u < rt) reinterpret_cast<uint64_t *>(rc)[u] = rep_rows[(b0 + t) * r + r0 + u];
+      if (u == 0) reinterpret_cast<uint32_t *>(rc)[kDecRecRt] = (uint32_t)rt;
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ch++) {
+      const int c0 = ch * chunk_bytes;
+      const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
+      BsLanes<VEC> ln(lane, cb);
+#pragma unroll
+      for (int x = 0; x < BsLanes<VEC>::NP; x++) ln.off[x] += (uint32_t)c0;
+      if (lane < ln.active)
+        bs_dec_call<RT, VEC>(lds_addr(S.intab), lds_addr(S.rec), (uint32_t)__builtin_amdgcn_readfirstlane(ng * k),
+                             (uint32_t)__builtin_amdgcn_readfirstlane(k), lds_addr(S.coef), ln);
+    }
+  }
+}
+
 // Decode of a few blocks in ONE launch (the synchronous hooks decode one block per call): each
 // workgroup plans its block with the wave plan, then runs the single-pass data pass on it.  The
 // plan's record stays in LDS (past both phases' scratch, at rec_off): both phases address a record
@@ -1955,6 +2014,14 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
                      L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst);
+}
+
+template <int RT, int VEC>
+static void launch_encode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nb, int k, int r, int L,
+                               const BsCfg &c, uint32_t fbn_base, const uint32_t *fbn, int r0, hipStream_t s) {
+  const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, nb);
+  hipLaunchKernelGGL((k_rlc_encode_rows<RT, VEC>), dim3(grid_for((nb + G - 1) / G)), dim3(64), RecoverLds<RT>::bytes(G, k),
+                     s, src_rows, rep_rows, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2846,6 +2913,24 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
       FEC_BS_DISPATCH(launch_encode_bs, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,
                       (int)symbol_size, cfg, fbn_base, fbn, r0, et.waves, (uint64_t)k * symbol_size, 1u, s)
     }
+  }
+  HIPCHK(hipGetLastError());
+  g_stats[0]++;
+  g_stats[1] += nblocks;
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_encode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn, void *stream) {
+  int rc = check_common(src_rows, rep_rows, nblocks, k, r, symbol_size);
+  if (rc || nblocks == 0 || r == 0) return rc;
+  if (int rc2 = bs_table_check()) return rc2;
+  hipStream_t s = (hipStream_t)stream;
+  const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+  const int rt = pick_rt(r);
+  for (int r0 = 0; r0 < (int)r; r0 += rt) {
+    FEC_BS_DISPATCH(launch_encode_rows, src_rows, rep_rows, nblocks, (int)k, (int)r, (int)symbol_size, cfg, fbn_base,
+                    fbn, r0, s)
   }
   HIPCHK(hipGetLastError());
   g_stats[0]++;

@@ -222,6 +222,34 @@ int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   return finish(c, rc);
 }
 
+int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, const uint64_t *rep_rows,
+                                uint64_t nblocks, uint32_t k, uint32_t r, uint32_t L, const uint32_t *fbn) {
+  if (!c || !src_rows || !rep_rows) return FECGPU_ERR_INVALID;
+  if (!nblocks || !r) return FECGPU_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  Slot &s = c->slot[0];
+  const uint64_t *ds = (const uint64_t *)mapped_host(src_rows, nblocks * k * 8);
+  const uint64_t *dr = (const uint64_t *)mapped_host(rep_rows, nblocks * r * 8);
+  const uint32_t *df = fbn ? (const uint32_t *)mapped_host(fbn, nblocks * 4) : nullptr;
+  int rc = FECGPU_OK;
+  do {
+    if (!ds || !dr || (fbn && !df)) {  // pageable tables: one device copy
+      const size_t need = nblocks * (k + r) * 8 + (fbn ? nblocks * 4 : 0);
+      LCHK(grow(&s.d_aux, &s.cap_aux, need));
+      uint8_t *a = (uint8_t *)s.d_aux;
+      LCHK(hipMemcpyAsync(a, src_rows, nblocks * k * 8, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync(a + nblocks * k * 8, rep_rows, nblocks * r * 8, hipMemcpyHostToDevice, s.st));
+      if (fbn) LCHK(hipMemcpyAsync(a + nblocks * (k + r) * 8, fbn, nblocks * 4, hipMemcpyHostToDevice, s.st));
+      ds = (const uint64_t *)a;
+      dr = (const uint64_t *)(a + nblocks * k * 8);
+      df = fbn ? (const uint32_t *)(a + nblocks * (k + r) * 8) : nullptr;
+    }
+    rc = fecgpu_rlc_encode_rows(ds, dr, nblocks, k, r, L, 0, df, s.st);
+  } while (0);
+  return finish(c, rc);
+}
+
 int fecgpu_xor_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uint64_t nblocks, uint32_t k,
                            uint32_t L) {
   if (!c || !src || !rep) return FECGPU_ERR_INVALID;

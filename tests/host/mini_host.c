@@ -13,8 +13,10 @@
  * Blocks are assembled as the block framework does (block_framework_sender.h:175-203,
  * block_framework_receiver.h:29-80, fec.h:292-308).
  */
+#define _GNU_SOURCE  /* MAP_ANONYMOUS */
 #include <stdint.h>
 #include <stdlib.h>
+#include <sys/mman.h>
 #include <string.h>
 
 #include "pquic_fec_protoops.h"
@@ -44,6 +46,29 @@ static long g_fail_after = -1;  /* allocation-failure injection: the n-th alloca
 
 void mh_fail_alloc_after(long n) { g_fail_after = n; }
 
+/* Optional plugin-style memory arena (picoquic_internal.h:576 memory[PLUGIN_MEMORY], carved into
+ * 2100-B slots, picoquic/memory.c:181-191): allocations up to 2092 B come from it, so the batching
+ * adapter can be given the arena (mh_batch_register_arena) and gather rows in place. */
+enum { MH_SLOT = 2112 };
+static uint8_t *g_arena;
+static size_t g_arena_size, g_arena_used;
+static void *g_arena_free;
+
+int mh_arena_enable(size_t bytes) {
+    if (g_arena) return 0;
+    g_arena_size = (bytes + 4095) & ~(size_t)4095;
+    void *p = mmap(NULL, g_arena_size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return -1;
+    g_arena = p;
+    g_arena_used = 0;
+    g_arena_free = NULL;
+    return 0;
+}
+
+static int in_arena(const void *p) {
+    return g_arena && (uintptr_t)p - (uintptr_t)g_arena < g_arena_size;
+}
+
 static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
     (void)cnx;
     if (g_fail_after == 0) {
@@ -51,14 +76,31 @@ static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
         return NULL;
     }
     if (g_fail_after > 0) g_fail_after--;
-    void *p = malloc(size <= 2092 ? 2100 : size);
+    void *p = NULL;
+    if (g_arena && size <= 2092) {
+        if (g_arena_free) {
+            p = g_arena_free;
+            g_arena_free = *(void **)p;
+        } else if (g_arena_used + MH_SLOT <= g_arena_size) {
+            p = g_arena + g_arena_used;
+            g_arena_used += MH_SLOT;
+        }
+    }
+    if (!p) p = malloc(size <= 2092 ? 2100 : size);
     if (p) g_live++;
     return p;
 }
 
 static void mh_free(picoquic_cnx_t *cnx, void *p) {
     (void)cnx;
-    if (p) { g_live--; free(p); }
+    if (!p) return;
+    g_live--;
+    if (in_arena(p)) {
+        *(void **)p = g_arena_free;
+        g_arena_free = p;
+    } else {
+        free(p);
+    }
 }
 
 typedef protoop_arg_t (*op_t)(picoquic_cnx_t *);
@@ -298,6 +340,11 @@ int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsi
     pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, max_symbol, nstreams};
     g_batcher = pquic_fec_batcher_create(&cfg);
     return g_batcher ? 0 : -1;
+}
+
+/* registers the arena (mh_arena_enable) with the open batcher */
+int mh_batch_register_arena(void) {
+    return g_arena ? pquic_fec_batch_register_heap(g_batcher, g_arena, g_arena_size) : -1;
 }
 
 static long new_ticket(pquic_fec_block_t *fb, int k, int r) {

@@ -24,8 +24,9 @@ def _p(a, t=C.c_uint8):
 
 
 class Batch:
-    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2):
+    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2, arena=False):
         L = C.CDLL(MINIHOST)
+        L.mh_arena_enable.argtypes = [C.c_size_t]
         for f in ("mh_batch_generate", "mh_batch_recover", "mh_batch_status", "mh_live_allocations"):
             getattr(L, f).restype = C.c_long
         L.mh_batch_generate.argtypes = [C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -40,7 +41,11 @@ class Batch:
         self.L = L
         assert L.mh_bind(0) == 0
         self.base = L.mh_live_allocations()
+        if arena:  # symbols in a plugin-style arena the batcher gathers rows from (registered heap)
+            assert L.mh_arena_enable(256 << 20) == 0
         assert L.mh_batch_open(0, batch_blocks, max_delay_us, max_symbol, nstreams) == 0
+        if arena:
+            assert L.mh_batch_register_arena() == 0
         self.meta = {}
 
     def generate(self, xor, fbn, srcs, r, now=0):
@@ -167,6 +172,33 @@ def test_batch_generate_matches_reference(batch_blocks):
         _check_generate(bt, t, j)
     st = bt.stats()
     assert st["completed"] + st["immediate"] == len(jobs) == st["submitted"] + st["immediate"]
+    assert st["engine_errors"] == 0
+    bt.close()
+
+
+@pytest.mark.parametrize("batch_blocks,max_symbol", [(5, 9000), (64, 1200), (64, 9000)])
+def test_batch_generate_gathers_from_registered_arena(batch_blocks, max_symbol):
+    """With the symbols' arena registered (pquic_fec_batch_register_heap), RLC generate batches read
+    the sources and write the repairs in place (fecgpu_rlc_encode_rows); rows outside the arena
+    (symbols > 2092 B), shorter than the block (zero-padded) or repairs shorter than the stride are
+    staged.  Same repairs, FPIDs and return values as the reference fixtures; no leaks."""
+    bt = Batch(batch_blocks, max_symbol=max_symbol, arena=True)
+    jobs = [j for j in _encode_jobs() if max(len(s) for s in j[2]) <= max_symbol]
+    # blocks whose rows are all exactly max_symbol long: sources and repairs both in place
+    rng = np.random.default_rng(max_symbol + batch_blocks)
+    o = Oracle()
+    for b in range(40):
+        k, r = int(rng.integers(1, 33)), int(rng.integers(1, 9))
+        srcs = [rng.integers(0, 256, max_symbol, dtype=np.uint8) for _ in range(k)]
+        fbn = int(rng.integers(0, 1 << 24))
+        rep = o.rlc_encode_batch(np.stack(srcs)[None], r, fbn)[0]
+        jobs.append((False, fbn, srcs, r, ("hex", [x.tobytes().hex() for x in rep]),
+                     [(fbn << 8) | i for i in range(r)], 0))
+    tickets = [bt.generate(*j[:4], now=i) for i, j in enumerate(jobs)]
+    bt.L.mh_batch_drain()
+    for t, j in zip(tickets, jobs):
+        _check_generate(bt, t, j)
+    st = bt.stats()
     assert st["engine_errors"] == 0
     bt.close()
 

@@ -7,10 +7,12 @@
  * does after sending them (block_framework_sender.h:125-133).  Reports end-to-end throughput
  * (host staging + PCIe + kernels) and the submit -> completion latency distribution.
  */
+#define _GNU_SOURCE  /* MAP_ANONYMOUS */
 #define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "pquic_fec_batch.h"
@@ -23,12 +25,16 @@ static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) {
 static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t v) {
     if (ak == PQUIC_AK_CNX_OUTPUT) c->out[p & 15] = v;
 }
-/* The plugin allocator hands out fixed 2100-byte slots from a free list (picoquic/memory.c:72-95,
- * 181-191); this load generator does the same, so completions cost what they cost in PQUIC
- * rather than glibc malloc's price.  Larger requests fall back to the heap, tagged. */
+/* The plugin allocator hands out fixed 2100-byte slots from a free list carved out of the plugin's
+ * memory arena (picoquic/memory.c:72-95, 181-191; picoquic_internal.h:576); this load generator does
+ * the same -- one contiguous arena, so the batcher can register it (pquic_fec_batch_register_heap) --
+ * and completions cost what they cost in PQUIC rather than glibc malloc's price.  Larger requests
+ * (and an exhausted arena) fall back to the heap, tagged. */
 enum { SLOT = 2112 };  /* 2100 B rounded to 64, plus room for the tag */
 typedef union slot_u { union slot_u *next; uint8_t bytes[SLOT]; } slot_u;
 static slot_u *g_free_slots;
+static uint8_t *g_arena;
+static size_t g_arena_bytes, g_arena_used;
 static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
     (void)c;
     if (n > SLOT - 16) {
@@ -38,7 +44,14 @@ static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
         return p + 16;
     }
     slot_u *s = g_free_slots;
-    if (s) g_free_slots = s->next; else if (!(s = malloc(sizeof *s))) return NULL;
+    if (s) {
+        g_free_slots = s->next;
+    } else if (g_arena && g_arena_used + SLOT <= g_arena_bytes) {
+        s = (slot_u *)(g_arena + g_arena_used);
+        g_arena_used += SLOT;
+    } else if (!(s = malloc(sizeof *s))) {
+        return NULL;
+    }
     s->bytes[0] = 0;
     return s->bytes + 16;
 }
@@ -84,9 +97,11 @@ static int cmp_u64(const void *a, const void *b) {
 }
 
 /* out: [0] payload GiB/s, [1] p50 us, [2] p99 us, [3] max us, [4] batches, [5] wall s,
- *      [6] blocks completed, [7] mean blocks per batch.  Returns 0 or -1. */
+ *      [6] blocks completed, [7] mean blocks per batch.  register_heap: the symbols' arena (slot
+ * allocator and payload) is registered with the batcher, which then gathers rows in place.
+ * Returns 0 or -1. */
 int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks, unsigned max_delay_us,
-           int nstreams, double offered_gib_s, double out[8]) {
+           int nstreams, double offered_gib_s, int register_heap, double out[8]) {
     pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device)) return -1;
     pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
@@ -96,7 +111,16 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     const long nslots = (long)batch_blocks * 4 + nconn + 64;
     slot_t *slots = calloc(nslots, sizeof *slots);
     const size_t pool_bytes = (size_t)64 * k * L;  /* 64 blocks of distinct payload, reused */
-    uint8_t *pool = malloc(pool_bytes);
+    /* the arena: 2 slots per repair symbol of every block in flight (struct + data), plus the payload */
+    g_free_slots = NULL;
+    g_arena_bytes = ((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes;
+    g_arena_bytes = (g_arena_bytes + 4095) & ~(size_t)4095;
+    g_arena_used = 0;
+    g_arena = mmap(NULL, g_arena_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (g_arena == MAP_FAILED) return -1;
+    uint8_t *pool = g_arena;  /* the payload (source symbols) lives in the arena as well */
+    g_arena_used = (pool_bytes + 63) & ~(size_t)63;
+    if (register_heap && pquic_fec_batch_register_heap(b, g_arena, g_arena_bytes)) return -1;
     pquic_source_symbol_t *ss = calloc((size_t)nslots * k, sizeof *ss);
     g_lat = malloc(sizeof *g_lat * (size_t)(nblocks + nblocks / 5 + 1));
     g_nlat = 0;
@@ -153,7 +177,7 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     const double wall = (now_us() - t0) * 1e-6;
     pquic_fec_batch_stats_t st;
     pquic_fec_batch_get_stats(b, &st);
-    pquic_fec_batcher_destroy(b);
+    pquic_fec_batcher_destroy(b);  /* unregisters the arena */
     qsort(g_lat, g_nlat, sizeof *g_lat, cmp_u64);
     out[0] = nblocks * bytes_per_block / wall / 1073741824.0;
     out[1] = g_nlat ? (double)g_lat[g_nlat / 2] : 0;
@@ -163,8 +187,11 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     out[5] = wall;
     out[6] = (double)(st.completed - st0.completed);
     out[7] = out[4] > 0 ? out[6] / out[4] : 0;
-    free(slots); free(pool); free(ss); free(g_lat); free(cnx);
+    free(slots); free(ss); free(g_lat); free(cnx);
     g_lat = NULL;
+    g_free_slots = NULL;  /* every slot lives in the arena or was malloc'd and leaks here (tool only) */
+    munmap(g_arena, g_arena_bytes);
+    g_arena = NULL;
     return 0;
 }
 
