@@ -72,6 +72,14 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
 int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t step, uint32_t k, uint32_t r,
                              uint32_t symbol_size, void *rep, void *stream);
 
+/* Window encode over de-duplicated symbol streams (the batching adapter's window jobs): symbols[] holds
+ * nrows rows of symbol_size bytes -- each connection's symbols once, in order -- and window w protects
+ * the k rows starting at row wrow[w] (a device array), with block number 0 like every window:
+ *   rep[w][i] = sum_j coef(0, i)[j] * symbols[wrow[w] + j].
+ * symbol_size % 16 == 0, 16-B aligned buffers, nrows * symbol_size < 2 GiB; knob window_sc != 0. */
+int fecgpu_rlc_window_encode_table(const void *symbols, uint64_t nrows, const uint32_t *wrow, uint64_t nwindows,
+                                   uint32_t k, uint32_t r, uint32_t symbol_size, void *rep, void *stream);
+
 /* RLC encode with every row given by its address: src_rows[b * k + j] / rep_rows[b * r + i] are the
  * device addresses (4-byte aligned; device memory or mapped page-locked host memory, e.g. a registered
  * plugin arena) of source row j / repair row i of block b, each symbol_size bytes.  The tables and
@@ -170,6 +178,12 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *ctx, void *src, const void 
  * are read in place, others are copied), the rows themselves must be device-accessible. */
 int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
                                 uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *fbn);
+/* fecgpu_rlc_window_encode_table from the host: the stream (host rows) crosses PCIe once, by one copy,
+ * before the windows are coded from device memory -- a symbol serves up to k windows, so reading it in
+ * place would cross the bus that many times; wrow[] is a host array; repairs go to page-locked `rep` in
+ * place, others by a copy.  With knob window_sc 0 the windows run through the row-table kernel. */
+int fecgpu_rlc_window_encode_host(fecgpu_host_ctx_t *ctx, const void *symbols, uint64_t nrows, const uint32_t *wrow,
+                                  uint64_t nwindows, uint32_t k, uint32_t r, uint32_t symbol_size, void *rep);
 int fecgpu_xor_encode_host(fecgpu_host_ctx_t *ctx, const void *src, void *rep, uint64_t nblocks,
                            uint32_t k, uint32_t symbol_size);
 int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, uint64_t nblocks,
@@ -214,6 +228,10 @@ int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, ui
  * C need no HIP headers.  NULL on failure. */
 void *fecgpu_host_alloc(size_t bytes);
 void fecgpu_host_free(void *p);
+/* The host CPUs nearest the device ("local_cpulist" of its PCI function, e.g. "0-63,128-191"), for
+ * placing the threads that feed it: page-locked rows read over PCIe from the device's own socket
+ * avoid the cross-socket hop.  FECGPU_OK or an error. */
+int fecgpu_device_local_cpus(int device, char *buf, size_t len);
 /* Page-lock and map an existing host range (hipHostRegister, mapped) so the kernels read and write
  * it in place -- e.g. a FEC plugin instance's memory arena (picoquic_internal.h:576, char
  * memory[PLUGIN_MEMORY], carved into 2100-B slots by picoquic/memory.c:181-191), which holds every

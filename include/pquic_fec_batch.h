@@ -51,6 +51,7 @@ typedef struct {
     uint64_t flushed_full, flushed_deadline, flushed_drain;
     uint64_t immediate;             /* blocks completed at submit (preconditions failed) */
     uint64_t engine_errors;
+    uint64_t windows, window_rows;  /* window blocks coded from shared streams; stream rows staged for them */
 } pquic_fec_batch_stats_t;
 
 /* NULL on failure (bad configuration, no device, out of pinned memory). */
@@ -74,6 +75,15 @@ int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t byt
  * max_symbol, allocation failure), in which case `done` is never called. */
 int pquic_fec_batch_generate(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
                              uint64_t now_us, pquic_fec_block_done_fn done, void *user);
+/* Queue fec_generate_repair_symbols (RLC-GF(256)) for a window block of the sliding-window sender
+ * (window_framework_sender.h:209-260: malloc_fec_block(cnx, 0) at :215, the symbols in flight chosen by
+ * window_select_symbols_to_protect, the generate call at :235).  Same contract and result as
+ * pquic_fec_batch_generate; in addition the batch stages each connection's symbols once for all the
+ * windows that share them and codes the windows together (every window is block number 0, so they share
+ * their coefficients).  Windows from one connection should arrive in sending order, as the sender
+ * produces them; a block with a non-zero block number is queued as an ordinary block. */
+int pquic_fec_batch_generate_window(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
+                                    uint64_t now_us, pquic_fec_block_done_fn done, void *user);
 /* Queue fec_recover for `fb` (the receiver's block copy, fec_protoops.h:220-222). */
 int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
                             uint64_t now_us, pquic_fec_block_done_fn done, void *user);

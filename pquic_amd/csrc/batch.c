@@ -18,6 +18,13 @@
  * addresses into page-locked tables and the kernel (fecgpu_rlc_encode_rows) reads the sources and
  * writes the repairs where the symbols are.  Rows outside a registered arena, or shorter than the
  * block's length (the reference zero-pads them), are staged as before.
+ * Windows (pquic_fec_batch_generate_window): the sliding-window sender protects the symbols in flight
+ * once per window, so consecutive windows of a connection share most of their symbols, and every window
+ * is block number 0, so all windows share their coefficients.  A window job therefore stages each
+ * connection's symbols once, as one run of rows (a stager lays the runs out at flush: windows grouped
+ * by connection, each window matched against the run's tail by symbol identity), records where each
+ * window starts, and the engine codes all windows from that stream with the shared-coefficient kernel
+ * (fecgpu_rlc_window_encode_host) after one copy of the stream to the device.
  * Finished jobs are completed on the caller's thread in poll / drain with the same finish
  * halves the synchronous operations use (fec_core.c), so a batched block ends in exactly the
  * state the protocol operation would leave it in.  The caller keeps a block unmodified until
@@ -35,7 +42,8 @@
 #include "fec_core.h"
 #include "fecgpu.h"
 
-enum { OP_GENERATE = 0, OP_RECOVER = 1 };
+enum { OP_GENERATE = 0, OP_RECOVER = 1, OP_WINDOW = 2 /* generate, window blocks */ };
+#define GENERATES(op) ((op) != OP_RECOVER)
 enum { MAX_OPEN = 32, MAX_STAGERS = 16, STAGE_CHUNK = 256 /* blocks per staging work item */, MAX_HEAPS = 64 };
 
 typedef struct {
@@ -76,6 +84,11 @@ typedef struct job {
     uint64_t src_dev, rep_dev;     /* device addresses of the staging rows */
     uint8_t *copy;                 /* gather: block needs its repairs copied out of the staging rows */
     uint32_t ncopy;                /* blocks flagged in copy[] (atomic while staging) */
+    uint32_t *wrow;                /* window: pinned [cap] start row of each window in the stream */
+    const pquic_source_symbol_t **rowsym;  /* window: [cap * k] the symbol of each stream row */
+    uint32_t *order;               /* window: [cap] entries grouped by connection */
+    size_t rowsym_cap;
+    uint64_t nrows;                /* window: stream rows */
 } job_t;
 
 struct pquic_fec_batcher {
@@ -123,6 +136,9 @@ int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t byt
 
 static void job_free(job_t *j) {
     if (!j) return;
+    fecgpu_host_free(j->wrow);
+    free(j->rowsym);
+    free(j->order);
     fecgpu_host_free(j->srow);
     fecgpu_host_free(j->rrow);
     free(j->copy);
@@ -138,8 +154,10 @@ static void job_free(job_t *j) {
 }
 
 /* A job for (op, scheme, k, r), from the free list when one is big enough. */
+static uint32_t window_stride(const pquic_fec_batcher_t *b) { return (b->stride + 15u) & ~15u; }
+
 static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
-    const uint32_t cap = b->cfg.batch_blocks, S = b->stride;
+    const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
     const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
     job_t **pp = &b->free_jobs;
     for (; *pp; pp = &(*pp)->next)
@@ -193,7 +211,24 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
                       fecgpu_host_device_address(j->rep, rb ? rb : 4, &j->rep_dev) != FECGPU_OK))
         j->gather = 0;
     j->ncopy = 0;
-    if (op == OP_GENERATE && j->reps_cap < (size_t)cap * r) {
+    if (op == OP_WINDOW) {  /* window tables: start rows (page-locked), the stream's symbols, the grouping */
+        if (!j->wrow) j->wrow = fecgpu_host_alloc((size_t)cap * 4);
+        if (!j->order) j->order = malloc((size_t)cap * 4);
+        if (j->rowsym_cap < (size_t)cap * k) {
+            const pquic_source_symbol_t **rs = realloc((void *)j->rowsym, sizeof *rs * (size_t)cap * k);
+            if (rs) {
+                j->rowsym = rs;
+                j->rowsym_cap = (size_t)cap * k;
+            }
+        }
+        if (!j->wrow || !j->order || j->rowsym_cap < (size_t)cap * k) {
+            j->next = b->free_jobs;
+            b->free_jobs = j;
+            return NULL;
+        }
+    }
+    j->nrows = 0;
+    if (GENERATES(op) && j->reps_cap < (size_t)cap * r) {
         pquic_repair_symbol_t **nr = realloc(j->reps, sizeof *nr * (size_t)cap * r);
         if (!nr) {
             j->next = b->free_jobs;
@@ -222,7 +257,9 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
 static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
     fecgpu_host_ctx_t *c = b->ctx;
     const uint32_t S = j->stride;
-    if (j->gather)
+    if (j->op == OP_WINDOW)
+        j->rc = fecgpu_rlc_window_encode_host(c, j->src, j->nrows, j->wrow, j->n, j->k, j->r, S, j->rep);
+    else if (j->gather)
         j->rc = fecgpu_rlc_encode_rows_host(c, j->srow, j->rrow, j->n, j->k, j->r, S, j->fbn);
     else if (j->op == OP_GENERATE)
         j->rc = j->xor_scheme ? fecgpu_xor_encode_host(c, j->src, j->rep, j->n, j->k, S)
@@ -286,6 +323,52 @@ static void stage_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     }
 }
 
+/* Window job: the stream layout, then its rows.  Entries are grouped by connection (stable), and a
+ * connection's windows extend one run of rows: a window whose first symbol is among the run's last
+ * rows, and whose symbols continue the run as far as it goes, starts there and appends only its new
+ * symbols; any other window starts a fresh run of its k symbols.  Rows are zero-padded to the stride
+ * (the reference pads each window's symbols to its max_length, which the copy-out then keeps). */
+static int cmp_cnx(const void *a, const void *b, void *arg) {
+    const job_t *j = arg;
+    const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    const uintptr_t cx = (uintptr_t)j->ent[x].cnx, cy = (uintptr_t)j->ent[y].cnx;
+    return cx != cy ? (cx < cy ? -1 : 1) : (x > y) - (x < y);
+}
+
+static void stage_windows(job_t *j) {
+    const uint32_t S = j->stride, k = j->k;
+    for (uint32_t i = 0; i < j->n; i++) j->order[i] = i;
+    qsort_r(j->order, j->n, sizeof *j->order, cmp_cnx, j);
+    uint64_t nrows = 0, run = 0;  /* run: first row of the current connection's run */
+    const picoquic_cnx_t *cur = NULL;
+    for (uint32_t o = 0; o < j->n; o++) {
+        const uint32_t i = j->order[o];
+        pquic_source_symbol_t *const *ss = j->ent[i].fb->source_symbols;
+        if (o == 0 || j->ent[i].cnx != cur) {
+            cur = j->ent[i].cnx;
+            run = nrows;
+        }
+        uint64_t start = nrows;
+        const uint64_t lo = nrows - run > k ? nrows - k : run;
+        for (uint64_t q = nrows; q-- > lo;) {  /* the newest row holding the window's first symbol */
+            if (!ss[0] || j->rowsym[q] != ss[0]) continue;
+            uint32_t x = 0;
+            while (x < k && q + x < nrows && ss[x] && j->rowsym[q + x] == ss[x]) x++;
+            if (q + x == nrows || x == k) start = q;  /* continues the run to its end, or lies within it */
+            break;
+        }
+        j->wrow[i] = (uint32_t)start;
+        for (uint64_t x = nrows - start; x < k; x++) j->rowsym[nrows++] = ss[x];
+    }
+    j->nrows = nrows;
+    for (uint64_t q = 0; q < nrows; q++) {
+        const pquic_source_symbol_t *sym = j->rowsym[q];
+        const uint16_t n = sym ? sym->data_length : 0;
+        if (n) memcpy(j->src + q * S, sym->data, n);
+        memset(j->src + q * S + n, 0, S - n);
+    }
+}
+
 /* Generate, after the engine: repair rows of blocks [i0, i1) into the symbols allocated at
  * submission (the copy half of fec_generate_finish). */
 static void copy_out_blocks(job_t *j, uint32_t i0, uint32_t i1) {
@@ -317,7 +400,8 @@ static void *stager_main(void *arg) {
         job_t **tail = b->post_head ? &b->post_tail : &b->todo_tail;
         if (!*head) break;  /* stop requested and nothing left */
         job_t *j = *head;
-        const uint32_t nchunks = (j->n + STAGE_CHUNK - 1) / STAGE_CHUNK;
+        /* a window job's layout is one item (it is sequential); its copy-out splits like any other */
+        const uint32_t nchunks = j->op == OP_WINDOW && !j->post ? 1 : (j->n + STAGE_CHUNK - 1) / STAGE_CHUNK;
         const uint32_t c = j->next_chunk++;
         if (j->next_chunk >= nchunks) {  /* every item of this job is claimed: the next job is up */
             *head = j->next;
@@ -326,6 +410,7 @@ static void *stager_main(void *arg) {
         pthread_mutex_unlock(&b->mu);
         const uint32_t i0 = c * STAGE_CHUNK, i1 = i0 + STAGE_CHUNK < j->n ? i0 + STAGE_CHUNK : j->n;
         if (j->post) copy_out_blocks(j, i0, i1);
+        else if (j->op == OP_WINDOW) stage_windows(j);
         else if (j->gather) gather_blocks(b, j, i0, i1);
         else stage_blocks(j, i0, i1);
         pthread_mutex_lock(&b->mu);
@@ -364,6 +449,28 @@ static int host_cpus(void) {
     return n < 1 ? 1 : n;
 }
 
+/* The CPUs nearest the device within this process's affinity mask: the engine and stager threads run
+ * there, so the page-locked rows they fill and the registered symbols the kernels read sit on the
+ * device's socket (a GPU box's second socket reaches the device over the inter-socket link).  Empty
+ * when unknown or disjoint from the mask. */
+static void local_cpus(int device, cpu_set_t *out) {
+    CPU_ZERO(out);
+    char list[512];
+    cpu_set_t aff;
+    if (fecgpu_device_local_cpus(device, list, sizeof list) != FECGPU_OK || sched_getaffinity(0, sizeof aff, &aff))
+        return;
+    for (char *p = list; *p;) {
+        char *end;
+        long a = strtol(p, &end, 10), b = a;
+        if (end == p) break;
+        if (*end == '-') b = strtol(end + 1, &end, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            if (c >= 0 && CPU_ISSET(c, &aff)) CPU_SET(c, out);
+        p = *end == ',' ? end + 1 : end;
+        if (*end != ',') break;
+    }
+}
+
 static void *worker_main(void *arg) {
     pquic_fec_batcher_t *b = arg;
     pthread_mutex_lock(&b->mu);
@@ -376,7 +483,7 @@ static void *worker_main(void *arg) {
         pthread_mutex_unlock(&b->mu);
         run_engine(b, j);
         pthread_mutex_lock(&b->mu);
-        if (j->op == OP_GENERATE && !j->rc && (!j->gather || j->ncopy)) {  /* repair rows to their symbols */
+        if (GENERATES(j->op) && !j->rc && (!j->gather || j->ncopy)) {  /* repair rows to their symbols */
             j->post = 1;
             j->next_chunk = j->chunks_done = 0;
             push(&b->post_head, &b->post_tail, j);
@@ -415,9 +522,16 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     b->nstagers = ns && atoi(ns) > 0 ? atoi(ns) : (half > 2 ? half : 2);
     if (b->nstagers > MAX_STAGERS) b->nstagers = MAX_STAGERS;
     int started = 0;
+    cpu_set_t near;
+    local_cpus(cfg->device, &near);
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    if (CPU_COUNT(&near)) pthread_attr_setaffinity_np(&attr, sizeof near, &near);
     for (; started < b->nstagers; started++)
-        if (pthread_create(&b->stager[started], NULL, stager_main, b)) break;
-    if (started < b->nstagers || pthread_create(&b->worker, NULL, worker_main, b)) {
+        if (pthread_create(&b->stager[started], &attr, stager_main, b)) break;
+    const int werr = started < b->nstagers || pthread_create(&b->worker, &attr, worker_main, b);
+    pthread_attr_destroy(&attr);
+    if (werr) {
         pthread_mutex_lock(&b->mu);
         b->stop = 1;
         b->nstagers = started;
@@ -492,7 +606,7 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     uint16_t maxl = 0;
     const uint32_t k = fb->total_source_symbols;
     uint32_t r = fb->total_repair_symbols;
-    if (op == OP_GENERATE) {
+    if (GENERATES(op)) {
         const int chk = fec_generate_check(fb, xor_scheme, &maxl);
         if (chk) {  /* the reference returns 1, nothing done; totals past 100 slots are an error */
             b->stats.immediate++;
@@ -517,7 +631,7 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     const uint32_t i = j->n;
     j->fbn[i] = fb->fec_block_number & 0xffffffu;  /* rows are copied later, by a stager */
     j->ent[i] = (entry_t){cnx, fb, done, user, maxl, -1};
-    if (op == OP_GENERATE)  /* the protocol operation's allocations, in its order, on this thread */
+    if (GENERATES(op))  /* the protocol operation's allocations, in its order, on this thread */
         j->ent[i].nalloc = (int16_t)fec_generate_alloc(cnx, fb, maxl, j->reps + (size_t)i * r);
     if (!i) j->t_first = now_us;
     j->n = i + 1;
@@ -529,6 +643,17 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
 int pquic_fec_batch_generate(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
                              uint64_t now_us, pquic_fec_block_done_fn done, void *user) {
     return submit(b, cnx, fb, OP_GENERATE, xor_scheme ? 1 : 0, now_us, done, user);
+}
+
+int pquic_fec_batch_generate_window(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
+                                    uint64_t now_us, pquic_fec_block_done_fn done, void *user) {
+    /* window jobs need block number 0 (shared coefficients) and a stream the kernel's 32-bit offsets
+     * reach; anything else is an ordinary block */
+    if (!b || !fb) return -1;
+    const size_t worst = ((size_t)b->cfg.batch_blocks + 1) * fb->total_source_symbols * window_stride(b);
+    if (fb->fec_block_number != 0 || worst >= ((size_t)1 << 31))
+        return submit(b, cnx, fb, OP_GENERATE, 0, now_us, done, user);
+    return submit(b, cnx, fb, OP_WINDOW, 0, now_us, done, user);
 }
 
 int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme,
@@ -550,7 +675,7 @@ static int collect(pquic_fec_batcher_t *b) {
         for (uint32_t i = 0; i < j->n; i++) {
             entry_t *e = &j->ent[i];
             protoop_arg_t ret;
-            pquic_repair_symbol_t **reps = j->op == OP_GENERATE ? j->reps + (size_t)i * j->r : NULL;
+            pquic_repair_symbol_t **reps = GENERATES(j->op) ? j->reps + (size_t)i * j->r : NULL;
             if (j->rc) {
                 FEC_STAT_ADD(errors, 1);
                 ret = PQUIC_FEC_ERR_UNBOUND;
@@ -558,17 +683,21 @@ static int collect(pquic_fec_batcher_t *b) {
                     g_fec_api.my_free(e->cnx, reps[x]->data);
                     g_fec_api.my_free(e->cnx, reps[x]);
                 }
-            } else if (j->op == OP_GENERATE) {
+            } else if (GENERATES(j->op)) {
                 ret = fec_generate_attach(e->fb, reps, e->nalloc);
             } else {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);
             }
-            if (j->op == OP_GENERATE) FEC_STAT_ADD(generate_calls, 1); else FEC_STAT_ADD(recover_calls, 1);
+            if (GENERATES(j->op)) FEC_STAT_ADD(generate_calls, 1); else FEC_STAT_ADD(recover_calls, 1);
             e->done(e->user, e->fb, ret);
             n++;
         }
         b->stats.completed += j->n;
+        if (j->op == OP_WINDOW && !j->rc) {
+            b->stats.windows += j->n;
+            b->stats.window_rows += j->nrows;
+        }
         j->n = 0;
         j->next = b->free_jobs;
         b->free_jobs = j;

@@ -98,6 +98,7 @@ static inline int knob(KnobId id) {
 
 // host_path.hip reads the zero-copy knob through this (library-internal)
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_window_sc(void) { return knob(K_WINDOW_SC); }
 
 static int set_err(int code, const char *fmt, const char *what) {
   snprintf(g_err, sizeof g_err, fmt, what);
@@ -2037,10 +2038,13 @@ static void launch_encode_rows(const uint64_t *src_rows, const uint64_t *rep_row
 #define BS_CALL_ENCSC(RT)                                                                          \
   bs_encsc_r##RT##_v16(sp, rpp, (uint32_t)L, 0u, 0u, (uint64_t)L, (uint64_t)L, (uint32_t)k, (uint32_t)k,  \
                        (uint32_t)rt, lds_addr(lds), off[0], off[1], so[0], so[1], vm[0], vm[1])
+// With a start table (wrow != nullptr) window w instead begins at row wrow[w] of `sym` -- the
+// batching adapter's de-duplicated symbol streams, several connections' runs in one buffer -- and
+// the pieces' load offsets are taken from `sym` itself (the host keeps the buffer below 2 GiB).
 template <int RT>
 __global__ __launch_bounds__(64) void k_rlc_encode_sc(const uint8_t *__restrict__ sym, uint8_t *__restrict__ rep,
                                                       uint64_t nwin, int k, int r, int L, uint64_t step_bytes,
-                                                      int r0) {
+                                                      int r0, const uint32_t *__restrict__ wrow) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
   const int lane = threadIdx.x;
@@ -2074,11 +2078,14 @@ __global__ __launch_bounds__(64) void k_rlc_encode_sc(const uint8_t *__restrict_
       const bool ok = p < F;
       const uint64_t w = p / (uint64_t)L;
       const uint32_t t = (uint32_t)(p - w * (uint64_t)L);
-      off[q] = ok ? (uint32_t)((w - w0) * step_bytes + t) : 0u;  // a piece past the end reads row 0
+      if (wrow)
+        off[q] = ok ? wrow[w] * (uint32_t)L + t : 0u;
+      else
+        off[q] = ok ? (uint32_t)((w - w0) * step_bytes + t) : 0u;  // a piece past the end reads row 0
       so[q] = ok ? (uint32_t)((w - w0) * (uint64_t)r * (uint64_t)L + t) : 0u;
       vm[q] = __ballot(ok);
     }
-    const uint64_t sp = (uint64_t)(uintptr_t)(sym + w0 * step_bytes);
+    const uint64_t sp = (uint64_t)(uintptr_t)(wrow ? sym : sym + w0 * step_bytes);
     const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (w0 * (uint64_t)r + (uint64_t)r0) * (uint64_t)L);
     if constexpr (RT == 1) BS_CALL_ENCSC(1);
     else if constexpr (RT == 2) BS_CALL_ENCSC(2);
@@ -2095,27 +2102,33 @@ __global__ __launch_bounds__(64) void k_rlc_encode_sc(const uint8_t *__restrict_
 // profiles/r02_ab_window_sc.log).  It takes 16-B pieces (L % 16 == 0, 16-B aligned rows) and
 // offsets that fit 32 bits; returns false (the block-at-a-time path then runs) otherwise.
 static bool launch_encode_sc(const uint8_t *sym, uint8_t *rep, uint64_t nwin, int k, int r, int L,
-                             uint64_t step_bytes, hipStream_t s) {
+                             uint64_t step_bytes, hipStream_t s, const uint32_t *wrow = nullptr,
+                             uint64_t nrows = 0) {
   if (!knob(K_WINDOW_SC) || L % 16 || ((uintptr_t)sym | (uintptr_t)rep) % 16) return false;
-  if (step_bytes >= (uint64_t)k * (uint64_t)L && knob(K_WINDOW_SC) != 2) return false;  // 2: force (tests)
-  const uint64_t span = (2048u / (uint32_t)L + 2u) * (step_bytes > (uint64_t)r * L ? step_bytes : (uint64_t)r * L);
-  if (span + (uint64_t)L >= (1ull << 31)) return false;
+  if (wrow) {  // start table: absolute 32-bit load offsets
+    if ((nrows + (uint64_t)k) * (uint64_t)L >= (1ull << 31)) return false;
+    if ((2048u / (uint32_t)L + 2u) * (uint64_t)r * L + (uint64_t)L >= (1ull << 31)) return false;
+  } else {
+    if (step_bytes >= (uint64_t)k * (uint64_t)L && knob(K_WINDOW_SC) != 2) return false;  // 2: force (tests)
+    const uint64_t span = (2048u / (uint32_t)L + 2u) * (step_bytes > (uint64_t)r * L ? step_bytes : (uint64_t)r * L);
+    if (span + (uint64_t)L >= (1ull << 31)) return false;
+  }
   const uint64_t nch = (nwin * (uint64_t)L + 2047) / 2048;
   for (int r0 = 0; r0 < r; r0 += 8) {
     const int rt = r - r0 < 8 ? r - r0 : 8;
     const size_t lds = (size_t)k * FEC_BS_COEF_ROW_BYTES(8);
     if (rt >= 5)
       hipLaunchKernelGGL((k_rlc_encode_sc<8>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
-                         step_bytes, r0);
+                         step_bytes, r0, wrow);
     else if (rt >= 3)
       hipLaunchKernelGGL((k_rlc_encode_sc<4>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
-                         step_bytes, r0);
+                         step_bytes, r0, wrow);
     else if (rt == 2)
       hipLaunchKernelGGL((k_rlc_encode_sc<2>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
-                         step_bytes, r0);
+                         step_bytes, r0, wrow);
     else
       hipLaunchKernelGGL((k_rlc_encode_sc<1>), dim3(grid_for(nch)), dim3(64), lds, s, sym, rep, nwin, k, r, L,
-                         step_bytes, r0);
+                         step_bytes, r0, wrow);
   }
   return true;
 }
@@ -2954,6 +2967,23 @@ int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t st
                       (hipStream_t)stream)
     }
   }
+  HIPCHK(hipGetLastError());
+  g_stats[0]++;
+  g_stats[1] += nwindows;
+  return FECGPU_OK;
+}
+
+int fecgpu_rlc_window_encode_table(const void *symbols, uint64_t nrows, const uint32_t *wrow, uint64_t nwindows,
+                                   uint32_t k, uint32_t r, uint32_t symbol_size, void *rep, void *stream) {
+  int rc = check_common(symbols, rep, nwindows, k, r, symbol_size);
+  if (rc || nwindows == 0 || r == 0) return rc;
+  if (!wrow || nrows < k) return set_err(FECGPU_ERR_INVALID, "%s", "window start table missing or stream shorter than k");
+  if (symbol_size % 16 || ((uintptr_t)symbols | (uintptr_t)rep) % 16)
+    return set_err(FECGPU_ERR_INVALID, "%s", "window table encode needs 16-B rows (symbol_size %% 16 == 0, aligned)");
+  if (int rc2 = bs_table_check()) return rc2;
+  if (!launch_encode_sc((const uint8_t *)symbols, (uint8_t *)rep, nwindows, (int)k, (int)r, (int)symbol_size, 0,
+                        (hipStream_t)stream, wrow, nrows))
+    return set_err(FECGPU_ERR_INVALID, "%s", "window table encode: stream of 2 GiB or more, or window_sc knob 0");
   HIPCHK(hipGetLastError());
   g_stats[0]++;
   g_stats[1] += nwindows;

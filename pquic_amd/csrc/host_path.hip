@@ -162,6 +162,7 @@ int fecgpu_rlc_decode_to_internal(const void *src, const void *rep, void *dst, u
                                   uint32_t r, uint32_t L, uint32_t fbn_base, const uint32_t *fbn,
                                   const uint32_t *seeds, const uint64_t *sp, const uint64_t *rp, uint8_t *status,
                                   uint64_t *recovered, void *ws, size_t wsb, void *stream);  // fec_engine.hip
+int fecgpu_knob_window_sc(void);  // fec_engine.hip (library-internal)
 static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 
 static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t per_block) {
@@ -246,6 +247,50 @@ int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       df = fbn ? (const uint32_t *)(a + nblocks * (k + r) * 8) : nullptr;
     }
     rc = fecgpu_rlc_encode_rows(ds, dr, nblocks, k, r, L, 0, df, s.st);
+  } while (0);
+  return finish(c, rc);
+}
+
+int fecgpu_rlc_window_encode_host(fecgpu_host_ctx_t *c, const void *symbols, uint64_t nrows, const uint32_t *wrow,
+                                  uint64_t nwin, uint32_t k, uint32_t r, uint32_t L, void *rep) {
+  if (!c || !symbols || !wrow || !rep || !k) return FECGPU_ERR_INVALID;
+  if (!nwin || !r) return FECGPU_OK;
+  for (uint64_t w = 0; w < nwin; w++)  // the rows every window names exist (the kernel reads them unchecked)
+    if ((uint64_t)wrow[w] + k > nrows) return FECGPU_ERR_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  Slot &s = c->slot[0];
+  const size_t sb = nrows * (size_t)L, rb = nwin * (size_t)r * L;
+  uint8_t *zr = zc_read() ? mapped_host(rep, rb) : nullptr;
+  const bool table = fecgpu_knob_window_sc() != 0;
+  int rc = FECGPU_OK;
+  do {
+    LCHK(grow(&s.d_src, &s.cap_src, sb));
+    LCHK(hipMemcpyAsync(s.d_src, symbols, sb, hipMemcpyHostToDevice, s.st));
+    uint8_t *dr = zr;
+    if (!dr) {
+      LCHK(grow(&s.d_rep, &s.cap_rep, rb));
+      dr = (uint8_t *)s.d_rep;
+    }
+    if (table) {
+      LCHK(grow(&s.d_aux, &s.cap_aux, nwin * 4));
+      LCHK(hipMemcpyAsync(s.d_aux, wrow, nwin * 4, hipMemcpyHostToDevice, s.st));
+      if ((rc = fecgpu_rlc_window_encode_table(s.d_src, nrows, (const uint32_t *)s.d_aux, nwin, k, r, L, dr, s.st)))
+        break;
+    } else {  // row tables: window w's rows and repairs by address, block number 0
+      std::vector<uint64_t> rows(nwin * (size_t)(k + r));
+      const uint64_t sd = (uint64_t)(uintptr_t)s.d_src, rd = (uint64_t)(uintptr_t)dr;
+      for (uint64_t w = 0; w < nwin; w++) {
+        for (uint32_t j = 0; j < k; j++) rows[w * k + j] = sd + ((uint64_t)wrow[w] + j) * L;
+        for (uint32_t i = 0; i < r; i++) rows[nwin * k + w * r + i] = rd + (w * r + i) * (uint64_t)L;
+      }
+      LCHK(grow(&s.d_aux, &s.cap_aux, rows.size() * 8));
+      LCHK(hipMemcpyAsync(s.d_aux, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, s.st));
+      const uint64_t *t = (const uint64_t *)s.d_aux;
+      if ((rc = fecgpu_rlc_encode_rows(t, t + nwin * k, nwin, k, r, L, 0, nullptr, s.st))) break;
+      LCHK(hipStreamSynchronize(s.st));  // `rows` is pageable and leaves scope
+    }
+    if (!zr) LCHK(hipMemcpyAsync(rep, dr, rb, hipMemcpyDeviceToHost, s.st));
   } while (0);
   return finish(c, rc);
 }
@@ -401,6 +446,27 @@ void fecgpu_host_free(void *p) {
   if (!p) return;
   pinned_remove((uintptr_t)p, nullptr);
   (void)hipHostFree(p);
+}
+
+int fecgpu_device_local_cpus(int device, char *buf, size_t len) {
+  if (!buf || len < 2) return FECGPU_ERR_INVALID;
+  char bus[64];
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return FECGPU_ERR_NO_DEVICE;
+  }
+  for (char *c = bus; *c; c++)
+    if (*c >= 'A' && *c <= 'F') *c = (char)(*c - 'A' + 'a');  // sysfs names are lower case
+  char path[128];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/local_cpulist", bus);
+  FILE *f = fopen(path, "r");
+  if (!f) return FECGPU_ERR_INVALID;
+  const bool ok = fgets(buf, (int)len, f) != nullptr;
+  fclose(f);
+  if (!ok) return FECGPU_ERR_INVALID;
+  for (char *c = buf; *c; c++)
+    if (*c == '\n') *c = 0;
+  return FECGPU_OK;
 }
 
 int fecgpu_host_register(void *p, size_t bytes) {

@@ -321,6 +321,7 @@ typedef struct {
     pquic_source_symbol_t *before[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
     long ret;
     int done, calls, k, r;
+    int shared;  /* window block: its source symbols belong to a stream */
 } ticket_t;
 
 static pquic_fec_batcher_t *g_batcher;
@@ -414,6 +415,47 @@ long mh_batch_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t 
     return t;
 }
 
+/* Sliding-window sender streams: each stream owns its source symbols (the framework's window,
+ * window_framework_sender.h), and window blocks point into it, so consecutive windows share symbols.
+ * Each stream is its own connection.  Streams live until mh_batch_close. */
+enum { MH_MAX_STREAMS = 256 };
+static pquic_source_symbol_t **g_stream[MH_MAX_STREAMS];
+static int g_stream_len[MH_MAX_STREAMS], g_nstreams;
+static picoquic_cnx_t g_stream_cnx[MH_MAX_STREAMS];
+
+/* returns the stream id or -1; symbol x carries source FPID first_fpid + x */
+int mh_stream_open(int nsym, const uint8_t *data, const uint16_t *len, int stride, uint32_t first_fpid) {
+    if (g_nstreams >= MH_MAX_STREAMS || nsym < 1) return -1;
+    pquic_source_symbol_t **v = calloc((size_t)nsym, sizeof *v);
+    if (!v) return -1;
+    for (int x = 0; x < nsym; x++) {
+        v[x] = mk_source(0, 0, data + (size_t)x * stride, len[x]);
+        v[x]->fpid.raw = first_fpid + (uint32_t)x;
+    }
+    g_stream[g_nstreams] = v;
+    g_stream_len[g_nstreams] = nsym;
+    return g_nstreams++;
+}
+
+/* window block over symbols [start, start + k) of a stream, submitted as the window sender would
+ * (block number 0); returns the ticket or -1 */
+long mh_batch_generate_window(int stream, int start, int k, int r, uint64_t now_us) {
+    if (stream < 0 || stream >= g_nstreams || start < 0 || start + k > g_stream_len[stream]) return -1;
+    pquic_fec_block_t *fb = calloc(1, sizeof *fb);
+    for (int j = 0; j < k; j++) fb->source_symbols[j] = g_stream[stream][start + j];
+    fb->current_source_symbols = fb->total_source_symbols = (uint8_t)k;
+    fb->total_repair_symbols = (uint8_t)r;
+    long t = new_ticket(fb, k, r);
+    g_tickets[t].shared = 1;
+    if (pquic_fec_batch_generate_window(g_batcher, &g_stream_cnx[stream], fb, now_us, on_done, (void *)(intptr_t)t)) {
+        memset(fb->source_symbols, 0, sizeof fb->source_symbols);
+        free_block(fb);
+        g_nt--;
+        return -1;
+    }
+    return t;
+}
+
 int mh_batch_poll(uint64_t now_us) { return pquic_fec_batch_poll(g_batcher, now_us); }
 int mh_batch_drain(void) { return pquic_fec_batch_drain(g_batcher); }
 
@@ -448,18 +490,29 @@ void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recove
     *cur_ss = tk->fb->current_source_symbols;
 }
 
-void mh_batch_get_stats(uint64_t out[8]) {
+void mh_batch_get_stats(uint64_t out[10]) {
     pquic_fec_batch_stats_t s;
     pquic_fec_batch_get_stats(g_batcher, &s);
     out[0] = s.submitted; out[1] = s.completed; out[2] = s.batches; out[3] = s.flushed_full;
     out[4] = s.flushed_deadline; out[5] = s.flushed_drain; out[6] = s.immediate; out[7] = s.engine_errors;
+    out[8] = s.windows; out[9] = s.window_rows;
 }
 
 /* frees every ticket's block and the batcher */
 void mh_batch_close(void) {
     pquic_fec_batcher_destroy(g_batcher);
     g_batcher = NULL;
-    for (long t = 0; t < g_nt; t++) free_block(g_tickets[t].fb);
+    for (long t = 0; t < g_nt; t++) {
+        if (g_tickets[t].shared) memset(g_tickets[t].fb->source_symbols, 0, sizeof g_tickets[t].fb->source_symbols);
+        free_block(g_tickets[t].fb);
+    }
+    picoquic_cnx_t c;
+    for (int i = 0; i < g_nstreams; i++) {
+        for (int x = 0; x < g_stream_len[i]; x++) { mh_free(&c, g_stream[i][x]->data); mh_free(&c, g_stream[i][x]); }
+        free(g_stream[i]);
+        g_stream[i] = NULL;
+    }
+    g_nstreams = 0;
     free(g_tickets);
     g_tickets = NULL;
     g_nt = g_capt = 0;

@@ -38,7 +38,11 @@ class Batch:
         L.mh_batch_recovered.argtypes = [C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int),
                                          C.c_void_p]
         L.mh_batch_poll.argtypes = [C.c_uint64]
+        L.mh_stream_open.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
+        L.mh_batch_generate_window.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
+        L.mh_batch_generate_window.restype = C.c_long
         self.L = L
+        self.stream_stride = {}
         assert L.mh_bind(0) == 0
         self.base = L.mh_live_allocations()
         if arena:  # symbols in a plugin-style arena the batcher gathers rows from (registered heap)
@@ -59,6 +63,24 @@ class Batch:
         t = self.L.mh_batch_generate(int(xor), fbn, k, r, buf.ctypes.data, lens.ctypes.data, stride, now)
         assert t >= 0
         self.meta[t] = (k, r, stride)
+        return t
+
+    def open_stream(self, syms, first_fpid=0):
+        """A window sender's symbols (one connection); window blocks point into it."""
+        stride = max(len(x) for x in syms)
+        buf = np.zeros((len(syms), stride), np.uint8)
+        lens = np.array([len(x) for x in syms], np.uint16)
+        for j, x in enumerate(syms):
+            buf[j, : len(x)] = x
+        sid = self.L.mh_stream_open(len(syms), buf.ctypes.data, lens.ctypes.data, stride, first_fpid)
+        assert sid >= 0
+        self.stream_stride[sid] = stride
+        return sid
+
+    def generate_window(self, sid, start, k, r, now=0):
+        t = self.L.mh_batch_generate_window(sid, start, k, r, now)
+        assert t >= 0
+        self.meta[t] = (k, r, self.stream_stride[sid])
         return t
 
     def recover(self, xor, fbn, srcs, reps, fpids, now=0):
@@ -114,10 +136,10 @@ class Batch:
         return {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}, cur.value
 
     def stats(self):
-        s = (C.c_uint64 * 8)()
+        s = (C.c_uint64 * 10)()
         self.L.mh_batch_get_stats(s)
         keys = ["submitted", "completed", "batches", "flushed_full", "flushed_deadline", "flushed_drain",
-                "immediate", "engine_errors"]
+                "immediate", "engine_errors", "windows", "window_rows"]
         return dict(zip(keys, list(s)))
 
     def close(self):
@@ -370,4 +392,107 @@ def test_batch_generate_allocation_failure_matches_sync(fail_at):
     assert [len(x) for x in reps_b] == [1200] * n + [0] * (r - n) == [int(x) for x in rl]
     assert fps_b == [int(x) for x in fp]
     assert all(a.tobytes() == rep[i].tobytes() for i, a in enumerate(reps_b[:n]))
+    bt.close()
+
+
+class _WindowSc:
+    """fecgpu_set_knob("window_sc", v) for a block (1: the shared-coefficient stream kernel, 0: the
+    row-table fallback), through the library the mini host links."""
+
+    def __init__(self, bt, v):
+        self.L, self.v = bt.L, v
+
+    def __enter__(self):
+        self.old = C.c_int(0)
+        assert self.L.fecgpu_get_knob(b"window_sc", C.byref(self.old)) == 0
+        assert self.L.fecgpu_set_knob(b"window_sc", self.v) == 0
+
+    def __exit__(self, *a):
+        self.L.fecgpu_set_knob(b"window_sc", self.old.value)
+
+
+@pytest.mark.parametrize("batch_blocks,window_sc", [(7, 1), (64, 1), (4096, 1), (64, 0)])
+def test_batch_window_generate_sliding(batch_blocks, window_sc):
+    """pquic_fec_batch_generate_window: sliding windows of several connections (window sender:
+    block number 0, window_framework_sender.h:215-235), submitted interleaved in sending order, with
+    steps 1-7, a gap, a repeated window, k changing mid-stream, ragged and tiny symbols and k = r = 1.
+    Each window's repairs and FPIDs equal the oracle's block-number-0 encode of its symbols (zero-padded
+    to the window's longest), and each connection's symbols are staged once per batch, not per window."""
+    rng = np.random.default_rng(batch_blocks + window_sc)
+    bt = Batch(batch_blocks, max_symbol=1500)
+    o = Oracle()
+    streams = []  # (symbols, [(start, k)], r)
+    lens_kinds = [lambda: 1200, lambda: 1200, lambda: int(rng.integers(1, 1501)), lambda: int(rng.integers(1, 40))]
+    for c in range(8):
+        n = 160
+        syms = [rng.integers(0, 256, lens_kinds[c % 4](), dtype=np.uint8) for _ in range(n)]
+        step = [1, 2, 3, 7, 1, 5, 2, 4][c]
+        k = [30, 20, 30, 12, 1, 30, 16, 25][c]
+        r = [4, 4, 8, 2, 1, 6, 4, 5][c]
+        wins = [(s0, k) for s0 in range(0, n - k - 40, step)]
+        wins.append((wins[-1][0] + k + 3, k))  # a gap: nothing shared with the window before
+        wins.append(wins[-1])                  # the same window again
+        k2 = max(1, k - 3)                      # window length changes (another queue)
+        wins += [(s0, k2) for s0 in range(wins[-1][0] + 1, n - k2, step)]
+        streams.append((syms, wins, r))
+    sids = [bt.open_stream(syms) for syms, _, _ in streams]
+    pending = [list(w) for _, w, _ in streams]
+    tickets = []
+    now = 0
+    with _WindowSc(bt, window_sc):
+        while any(pending):
+            for c, (syms, _, r) in enumerate(streams):
+                if pending[c]:
+                    s0, k = pending[c].pop(0)
+                    tickets.append((c, s0, k, r, bt.generate_window(sids[c], s0, k, r, now=now)))
+                    now += 1
+                    if now % 97 == 0:
+                        bt.L.mh_batch_poll(now)
+        bt.L.mh_batch_drain()
+    for c, s0, k, r, t in tickets:
+        assert bt.status(t) == (0, 1)
+        reps, fps = bt.repairs(t)
+        want = o.rlc_encode_block(0, streams[c][0][s0: s0 + k], r)[1]
+        assert [x.tobytes() for x in reps] == [x.tobytes() for x in want], (c, s0, k)
+        assert fps == list(range(r))
+    st = bt.stats()
+    assert st["engine_errors"] == 0 and st["windows"] == len(tickets)
+    total = sum(k for _, _, k, _, _ in tickets)
+    if batch_blocks >= 64:  # every connection's run is staged once: rows ~ symbols, far below sum(k)
+        assert st["window_rows"] < total / 3, (st["window_rows"], total)
+    bt.close()
+
+
+def test_batch_window_generate_fixtures():
+    """Window generate on the window fixtures' RLC blocks encoded as block number 0 (window_cases.json,
+    reference-generated): the repairs equal the oracle's, and fed with the fixture's erasures to the
+    batched recover they give back exactly the symbols the reference recovered."""
+    bt = Batch(16)
+    o = Oracle()
+    d = load("window_cases.json")
+    jobs = []
+    for i, case in enumerate(d["cases"]):
+        if case["scheme"] != "rlc" or case["mixed_seeds"] or case["crashed"]:
+            continue
+        srcs, want, fpids = window_inputs(case, o)
+        sid = bt.open_stream(srcs)
+        jobs.append((case, srcs, want, fpids, bt.generate_window(sid, 0, case["k"], case["r"], now=i)))
+    assert len(jobs) > 40
+    bt.L.mh_batch_drain()
+    rec_jobs = []
+    for case, srcs, want, fpids, t in jobs:
+        assert bt.status(t) == (0, 1), case["tag"]
+        reps, _ = bt.repairs(t)
+        assert [x.tobytes() for x in reps] == [x.tobytes() for x in want], case["tag"]
+        k, r = case["k"], case["r"]
+        s_in = [None if j in case["src_missing"] else srcs[j] for j in range(k)]
+        r_in = [reps[x] if x in case["rep_present"] else None for x in range(r)]
+        rec_jobs.append((case, bt.recover(False, case["fbn"], s_in, r_in, fpids)))
+    bt.L.mh_batch_drain()
+    for case, t in rec_jobs:
+        ret, calls = bt.status(t)
+        assert calls == 1 and ret == case["ret"], case["tag"]
+        rec, _ = bt.recovered(t)
+        assert {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())} == case["recovered"], case["tag"]
+    assert bt.stats()["windows"] == len(jobs)
     bt.close()

@@ -15,6 +15,9 @@
 #include <sys/mman.h>
 #include <time.h>
 
+#include <sched.h>
+
+#include "fecgpu.h"
 #include "pquic_fec_batch.h"
 
 struct st_picoquic_cnx_t { int id; protoop_arg_t in[16], out[16]; };
@@ -65,6 +68,24 @@ static void bl_free(picoquic_cnx_t *c, void *p) {
     g_free_slots = s;
 }
 
+/* the device's local CPUs (fecgpu_device_local_cpus) within `aff`; 0 when non-empty */
+static int near_cpus(int device, const cpu_set_t *aff, cpu_set_t *out) {
+    char list[512];
+    CPU_ZERO(out);
+    if (fecgpu_device_local_cpus(device, list, sizeof list) != FECGPU_OK) return -1;
+    for (char *p = list; *p;) {
+        char *end;
+        long a = strtol(p, &end, 10), b = a;
+        if (end == p) break;
+        if (*end == '-') b = strtol(end + 1, &end, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            if (c >= 0 && CPU_ISSET(c, aff)) CPU_SET(c, out);
+        if (*end != ',') break;
+        p = end + 1;
+    }
+    return CPU_COUNT(out) ? 0 : -1;
+}
+
 static uint64_t now_us(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -104,6 +125,11 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
            int nstreams, double offered_gib_s, int register_heap, double out[8]) {
     pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device)) return -1;
+    /* the sender runs on the device's socket, like the batcher's threads, so the arena it first
+     * touches is local to the device */
+    cpu_set_t saved, near;
+    const int pinned = !sched_getaffinity(0, sizeof saved, &saved) && !near_cpus(device, &saved, &near) &&
+                       !sched_setaffinity(0, sizeof near, &near);
     pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
     pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
     if (!b) return -1;
@@ -189,7 +215,110 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     out[7] = out[4] > 0 ? out[6] / out[4] : 0;
     free(slots); free(ss); free(g_lat); free(cnx);
     g_lat = NULL;
+    if (pinned) sched_setaffinity(0, sizeof saved, &saved);
     g_free_slots = NULL;  /* every slot lives in the arena or was malloc'd and leaks here (tool only) */
+    munmap(g_arena, g_arena_bytes);
+    g_arena = NULL;
+    return 0;
+}
+
+/* Sliding-window sender load (window_framework_sender.h:209-260): `nconn` connections each send a
+ * stream of L-byte source symbols and, after every `step` new symbols, generate repairs for a window of
+ * the last k (block number 0, as malloc_fec_block(cnx, 0) at :215), through
+ * pquic_fec_batch_generate_window (window_api 1: each connection's symbols staged once per batch,
+ * windows coded on the shared-coefficient kernel) or pquic_fec_batch_generate (0: every window a block
+ * of its own).  Symbols live in per-connection rings sized past the windows that can be in flight.
+ * out: [0] stream GiB/s (new symbols protected), [1] p50 us, [2] p99 us, [3] max us, [4] batches,
+ *      [5] wall s, [6] windows completed, [7] window GiB/s (k symbols per window).  Returns 0 or -1. */
+int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwindows, unsigned batch_blocks,
+                  unsigned max_delay_us, int nstreams, int window_api, double out[8]) {
+    if (k < 1 || k > 64 || r < 1 || step < 1 || nconn < 1 || L < 1 || L > 2048) return -1;
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
+    if (pquic_fec_bind_host(&api, device)) return -1;
+    cpu_set_t saved, near;
+    const int pinned = !sched_getaffinity(0, sizeof saved, &saved) && !near_cpus(device, &saved, &near) &&
+                       !sched_setaffinity(0, sizeof near, &near);
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
+    pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
+    if (!b) return -1;
+    const long nslots = (long)batch_blocks * 4 + nconn + 64;
+    const long ring = ((nslots / nconn + 4) * step + k) * 2;  /* symbols per connection ring */
+    const size_t pool_syms = 4096, pool_bytes = pool_syms * (size_t)L;
+    g_free_slots = NULL;
+    g_arena_bytes = (((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes + 4095) & ~(size_t)4095;
+    g_arena_used = 0;
+    g_arena = mmap(NULL, g_arena_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (g_arena == MAP_FAILED) return -1;
+    uint8_t *pool = g_arena;
+    g_arena_used = (pool_bytes + 63) & ~(size_t)63;
+    slot_t *slots = calloc(nslots, sizeof *slots);
+    pquic_source_symbol_t *rings = calloc((size_t)nconn * ring, sizeof *rings);
+    long *sent = calloc(nconn, sizeof *sent);
+    g_lat = malloc(sizeof *g_lat * (size_t)(nwindows + nwindows / 5 + 1));
+    g_nlat = 0;
+    picoquic_cnx_t *cnx = calloc(nconn, sizeof *cnx);
+    if (!slots || !rings || !sent || !g_lat || !cnx) return -1;
+    uint64_t x = 0x5EEDF3C0;
+    for (size_t o = 0; o < pool_bytes; o++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; pool[o] = (uint8_t)x; }
+    for (int c = 0; c < nconn; c++) {
+        cnx[c].id = c;
+        sent[c] = k > step ? k - step : 0;  /* symbols already sent: the first window then ends at k */
+    }
+    long next_slot = 0;
+    uint64_t t0 = 0;
+    pquic_fec_batch_stats_t st0;
+    memset(&st0, 0, sizeof st0);
+    for (int pass = 0; pass < 2; pass++) {
+        const long nw = pass ? nwindows : nwindows / 5 + 1;
+        if (pass) {
+            pquic_fec_batch_drain(b);
+            pquic_fec_batch_get_stats(b, &st0);
+            g_nlat = 0;
+        }
+        t0 = now_us();
+        for (long w = 0; w < nw; w++) {
+            slot_t *s = &slots[next_slot];
+            while (s->busy) pquic_fec_batch_poll(b, now_us());
+            next_slot = (next_slot + 1) % nslots;
+            const int c = (int)(w % nconn);
+            pquic_source_symbol_t *rc = rings + (size_t)c * ring;
+            for (long q = w < nconn ? 0 : sent[c]; q < sent[c] + step; q++) {  /* new symbols (all, at first) */
+                pquic_source_symbol_t *sym = &rc[q % ring];
+                sym->fpid.raw = (uint32_t)q;
+                sym->data = pool + (size_t)((q * 31 + c * 977) % (long)pool_syms) * L;
+                sym->data_length = (uint16_t)L;
+            }
+            sent[c] += step;
+            memset(&s->fb, 0, sizeof s->fb);
+            for (int j = 0; j < k; j++) s->fb.source_symbols[j] = &rc[(sent[c] - k + j) % ring];
+            s->fb.current_source_symbols = s->fb.total_source_symbols = (uint8_t)k;
+            s->fb.total_repair_symbols = (uint8_t)r;
+            s->busy = 1;
+            s->t_submit = now_us();
+            const int rc2 = window_api ? pquic_fec_batch_generate_window(b, &cnx[c], &s->fb, s->t_submit, on_done, s)
+                                       : pquic_fec_batch_generate(b, &cnx[c], &s->fb, 0, s->t_submit, on_done, s);
+            if (rc2) return -1;
+            if ((w & 15) == 0) pquic_fec_batch_poll(b, now_us());
+        }
+    }
+    pquic_fec_batch_drain(b);
+    const double wall = (now_us() - t0) * 1e-6;
+    pquic_fec_batch_stats_t st;
+    pquic_fec_batch_get_stats(b, &st);
+    pquic_fec_batcher_destroy(b);
+    qsort(g_lat, g_nlat, sizeof *g_lat, cmp_u64);
+    out[0] = (double)nwindows * step * L / wall / 1073741824.0;
+    out[1] = g_nlat ? (double)g_lat[g_nlat / 2] : 0;
+    out[2] = g_nlat ? (double)g_lat[(long)(g_nlat * 0.99)] : 0;
+    out[3] = g_nlat ? (double)g_lat[g_nlat - 1] : 0;
+    out[4] = (double)(st.batches - st0.batches);
+    out[5] = wall;
+    out[6] = (double)(st.completed - st0.completed);
+    out[7] = (double)nwindows * k * L / wall / 1073741824.0;
+    free(slots); free(rings); free(sent); free(g_lat); free(cnx);
+    g_lat = NULL;
+    if (pinned) sched_setaffinity(0, sizeof saved, &saved);
+    g_free_slots = NULL;
     munmap(g_arena, g_arena_bytes);
     g_arena = NULL;
     return 0;
