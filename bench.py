@@ -430,21 +430,44 @@ def batching_legs(dev_index, args):
     lib = C.CDLL(path)
     lib.bl_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint, C.c_uint, C.c_int,
                            C.c_double, C.c_int, C.POINTER(C.c_double)]
+    lib.bl_run_window.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint,
+                                  C.c_uint, C.c_int, C.c_int, C.POINTER(C.c_double)]
     legs = {}
-    for name, nblocks, batch, delay, offered, reg in (("saturated", 200000, 4096, 2000, 0.0, 1),
-                                                      ("saturated_staged", 200000, 4096, 2000, 0.0, 0),
-                                                      ("paced_2GiBps", 100000, 4096, 250, 2.0, 1)):
-        out = (C.c_double * 8)()
-        rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, reg, out)
-        if rc:
+    # host-side rates on a shared CPU slice vary from run to run: the saturated legs report the run
+    # with the median rate of three, and every run's rate
+    for name, nblocks, batch, delay, offered, reg, runs in (("saturated", 200000, 4096, 2000, 0.0, 1, 3),
+                                                            ("saturated_staged", 200000, 4096, 2000, 0.0, 0, 3),
+                                                            ("paced_2GiBps", 100000, 4096, 250, 2.0, 1, 1)):
+        res = []
+        for _ in range(runs):
+            out = (C.c_double * 8)()
+            rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, reg, out)
+            if rc:
+                break
+            res.append(list(out))
+        if len(res) < runs:
             legs["batch_" + name] = {"error": rc}
             continue
+        out = sorted(res, key=lambda o: o[0])[len(res) // 2]
         legs["batch_" + name] = {
             "k": args.k, "r": args.r, "L": args.symbol, "blocks": nblocks, "connections": 64,
             "batch_blocks": batch, "max_delay_us": delay, "offered_GiB_s": offered or None,
             "rows": "gathered in place (registered arena)" if reg else "staged by copies",
             "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
-            "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1)}
+            "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1),
+            "runs_payload_GiB_s": [round(o[0], 2) for o in res]}
+    # the sliding-window sender (window_framework_sender.h:209-260) at the redundancy controllers'
+    # shapes: a window of the <= 30 symbols in flight every K new ones, N - K repairs
+    for k, r, step in ((30, 1, 5), (30, 5, 25)):
+        leg = {"k": k, "r": r, "L": args.symbol, "step": step, "windows": 200000, "connections": 64,
+               "batch_blocks": 4096, "max_delay_us": 2000}
+        for api, tag in ((1, "window_api"), (0, "block_api")):
+            out = (C.c_double * 8)()
+            rc = lib.bl_run_window(dev_index, k, r, args.symbol, step, 64, 200000, 4096, 2000, 2, api, out)
+            leg[tag] = {"error": rc} if rc else {
+                "stream_GiB_s": round(out[0], 2), "window_GiB_s": round(out[7], 2), "latency_us_p50": out[1],
+                "latency_us_p99": out[2], "batches": int(out[4])}
+        legs[f"batch_window_k{k}_r{r}_step{step}"] = leg
     return legs
 
 

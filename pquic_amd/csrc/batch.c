@@ -44,7 +44,7 @@
 
 enum { OP_GENERATE = 0, OP_RECOVER = 1, OP_WINDOW = 2 /* generate, window blocks */ };
 #define GENERATES(op) ((op) != OP_RECOVER)
-enum { MAX_OPEN = 32, MAX_STAGERS = 16, STAGE_CHUNK = 256 /* blocks per staging work item */, MAX_HEAPS = 64 };
+enum { MAX_OPEN = 32, MAX_STAGERS = 16, MAX_ENGINES = 4, STAGE_CHUNK = 256 /* blocks per staging work item */, MAX_HEAPS = 64 };
 
 typedef struct {
     uintptr_t base;
@@ -94,10 +94,12 @@ typedef struct job {
 struct pquic_fec_batcher {
     pquic_fec_batch_cfg_t cfg;
     uint32_t stride;
-    fecgpu_host_ctx_t *ctx;
+    fecgpu_host_ctx_t *ctx[MAX_ENGINES];  /* one per engine thread: its own streams and device buffers */
     job_t *open[MAX_OPEN];
     job_t *free_jobs;
-    pthread_t worker;
+    pthread_t worker[MAX_ENGINES];
+    int nengines;
+    struct engine_arg { struct pquic_fec_batcher *b; int idx; } earg[MAX_ENGINES];
     pthread_t stager[MAX_STAGERS];
     int nstagers;
     pthread_mutex_t mu;
@@ -254,8 +256,7 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
     return j;
 }
 
-static void run_engine(pquic_fec_batcher_t *b, job_t *j) {
-    fecgpu_host_ctx_t *c = b->ctx;
+static void run_engine(fecgpu_host_ctx_t *c, job_t *j) {
     const uint32_t S = j->stride;
     if (j->op == OP_WINDOW)
         j->rc = fecgpu_rlc_window_encode_host(c, j->src, j->nrows, j->wrow, j->n, j->k, j->r, S, j->rep);
@@ -471,8 +472,12 @@ static void local_cpus(int device, cpu_set_t *out) {
     }
 }
 
+/* Engine threads (PQUIC_FEC_BATCH_ENGINES, default 2): each runs staged jobs through its own host
+ * context, so one job's kernels (reading and writing page-locked rows over PCIe) overlap the next job's
+ * launch and the previous one's synchronisation instead of leaving the bus idle between jobs. */
 static void *worker_main(void *arg) {
-    pquic_fec_batcher_t *b = arg;
+    const struct engine_arg *ea = arg;
+    pquic_fec_batcher_t *b = ea->b;
     pthread_mutex_lock(&b->mu);
     for (;;) {
         while (!b->staged_head && b->stagers_done < b->nstagers) pthread_cond_wait(&b->cv_staged, &b->mu);
@@ -481,7 +486,7 @@ static void *worker_main(void *arg) {
         b->staged_head = j->next;
         if (!b->staged_head) b->staged_tail = NULL;
         pthread_mutex_unlock(&b->mu);
-        run_engine(b, j);
+        run_engine(b->ctx[ea->idx], j);
         pthread_mutex_lock(&b->mu);
         if (GENERATES(j->op) && !j->rc && (!j->gather || j->ncopy)) {  /* repair rows to their symbols */
             j->post = 1;
@@ -506,10 +511,16 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     b->cfg = *cfg;
     b->stride = fec_pad4(cfg->max_symbol);
     const size_t chunk = (size_t)cfg->batch_blocks * 20 * b->stride / (size_t)cfg->nstreams;
-    b->ctx = fecgpu_host_ctx_create(cfg->device, cfg->nstreams, chunk < (1u << 20) ? (1u << 20) : chunk);
-    if (!b->ctx) {
-        free(b);
-        return NULL;
+    const char *ne = getenv("PQUIC_FEC_BATCH_ENGINES");
+    b->nengines = ne && atoi(ne) > 0 ? atoi(ne) : 2;
+    if (b->nengines > MAX_ENGINES) b->nengines = MAX_ENGINES;
+    for (int e = 0; e < b->nengines; e++) {
+        b->ctx[e] = fecgpu_host_ctx_create(cfg->device, cfg->nstreams, chunk < (1u << 20) ? (1u << 20) : chunk);
+        if (!b->ctx[e]) {
+            for (int x = 0; x < e; x++) fecgpu_host_ctx_destroy(b->ctx[x]);
+            free(b);
+            return NULL;
+        }
     }
     pthread_mutex_init(&b->mu, NULL);
     pthread_cond_init(&b->cv_todo, NULL);
@@ -529,20 +540,26 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     if (CPU_COUNT(&near)) pthread_attr_setaffinity_np(&attr, sizeof near, &near);
     for (; started < b->nstagers; started++)
         if (pthread_create(&b->stager[started], &attr, stager_main, b)) break;
-    const int werr = started < b->nstagers || pthread_create(&b->worker, &attr, worker_main, b);
+    int engines = 0;
+    if (started == b->nstagers)
+        for (; engines < b->nengines; engines++) {
+            b->earg[engines] = (struct engine_arg){b, engines};
+            if (pthread_create(&b->worker[engines], &attr, worker_main, &b->earg[engines])) break;
+        }
     pthread_attr_destroy(&attr);
-    if (werr) {
+    if (engines < b->nengines) {
         pthread_mutex_lock(&b->mu);
         b->stop = 1;
         b->nstagers = started;
         pthread_cond_broadcast(&b->cv_todo);
         pthread_mutex_unlock(&b->mu);
         for (int i = 0; i < started; i++) pthread_join(b->stager[i], NULL);
+        for (int i = 0; i < engines; i++) pthread_join(b->worker[i], NULL);
         pthread_cond_destroy(&b->cv_todo);
         pthread_cond_destroy(&b->cv_staged);
         pthread_cond_destroy(&b->cv_done);
         pthread_mutex_destroy(&b->mu);
-        fecgpu_host_ctx_destroy(b->ctx);
+        for (int e = 0; e < b->nengines; e++) fecgpu_host_ctx_destroy(b->ctx[e]);
         free(b);
         return NULL;
     }
@@ -737,14 +754,14 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
     pthread_cond_broadcast(&b->cv_todo);
     pthread_mutex_unlock(&b->mu);
     for (int i = 0; i < b->nstagers; i++) pthread_join(b->stager[i], NULL);
-    pthread_join(b->worker, NULL);
+    for (int e = 0; e < b->nengines; e++) pthread_join(b->worker[e], NULL);
     while (b->free_jobs) {
         job_t *j = b->free_jobs;
         b->free_jobs = j->next;
         job_free(j);
     }
     for (int i = 0; i < b->nheaps; i++) fecgpu_host_unregister((void *)b->heaps[i].base);
-    fecgpu_host_ctx_destroy(b->ctx);
+    for (int e = 0; e < b->nengines; e++) fecgpu_host_ctx_destroy(b->ctx[e]);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->cv_todo);
     pthread_cond_destroy(&b->cv_staged);

@@ -60,6 +60,9 @@ TABLE_B = 32768
 EARLY_PF = T64 and os.environ.get("FEC_GEN_EARLY_PF", "1") != "0"
 # EARLY_CO (with EARLY_PF): a step's coefficient fields are read before its transpose, not after
 EARLY_CO = os.environ.get("FEC_GEN_EARLY_CO", "0") != "0"
+# register-prefetch bodies compute exec-masked to the lanes that own pieces (vm0: at L = 1200, 38 of
+# 64), as the ring bodies do; idle lanes then neither load nor switch
+EXECMASK = os.environ.get("FEC_GEN_EXECMASK", "0") != "0"
 
 
 def table_map(B):
@@ -422,6 +425,9 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a(f"s_mov_b32 s{S_SAVEM0}, m0")
     a(f"s_mov_b64 s[{S_SAVEEX}:{S_SAVEEX + 1}], exec")
+    live = "%[vm0]" if EXECMASK else f"s[{S_SAVEEX}:{S_SAVEEX + 1}]"  # exec of the compute
+    if EXECMASK:
+        a(f"s_mov_b64 exec, {live}")
     for i, m in enumerate(MASKS):
         a(f"s_mov_b32 s{S_MASK[i]}, 0x{m:08x}")
     a(f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]")
@@ -630,14 +636,14 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
             a(f"v_mov_b32 v{TMP[1]}, 1")
             a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
             a(f"ds_write_b8 v{OUTPTR}, v{TMP[1]} offset:{DEC_REC_NZ + i}")  # non-zero flag (LDS)
-            a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+            a(f"s_mov_b64 exec, {live}")
             a("s_waitcnt lgkmcnt(0)")
             a(f"v_readfirstlane_b32 s{S_O2}, v{TMP[2]}")
             a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{TMP[3]}")
         for q in range(NP):
             a(f"s_mov_b64 exec, %[vm{q}]")
             a(f"{st} %[{'so' if sc else 'off'}{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
-        a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
+        a(f"s_mov_b64 exec, {live}")
         if mode == "enc":
             a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
             a(f"s_addc_u32 s{S_O2 + 1}, s{S_O2 + 1}, 0")

@@ -284,10 +284,12 @@ int fecgpu_rlc_window_encode_host(fecgpu_host_ctx_t *c, const void *symbols, uin
         for (uint32_t j = 0; j < k; j++) rows[w * k + j] = sd + ((uint64_t)wrow[w] + j) * L;
         for (uint32_t i = 0; i < r; i++) rows[nwin * k + w * r + i] = rd + (w * r + i) * (uint64_t)L;
       }
-      LCHK(grow(&s.d_aux, &s.cap_aux, rows.size() * 8));
+      LCHK(grow(&s.d_aux, &s.cap_aux, rows.size() * 8 + nwin * 4));
       LCHK(hipMemcpyAsync(s.d_aux, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, s.st));
       const uint64_t *t = (const uint64_t *)s.d_aux;
-      if ((rc = fecgpu_rlc_encode_rows(t, t + nwin * k, nwin, k, r, L, 0, nullptr, s.st))) break;
+      uint32_t *zero_fbn = (uint32_t *)(t + rows.size());  // every window is block number 0
+      LCHK(hipMemsetAsync(zero_fbn, 0, nwin * 4, s.st));
+      if ((rc = fecgpu_rlc_encode_rows(t, t + nwin * k, nwin, k, r, L, 0, zero_fbn, s.st))) break;
       LCHK(hipStreamSynchronize(s.st));  // `rows` is pageable and leaves scope
     }
     if (!zr) LCHK(hipMemcpyAsync(rep, dr, rb, hipMemcpyDeviceToHost, s.st));
