@@ -48,10 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
-                                           "small_lds", "block_svc"};
+                                           "small_lds", "block_svc", "ws_lds"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -89,6 +89,9 @@ static void knobs_from_env() {
   // fecgpu_block_svc_*: the resident worker serves requests (1) or every call returns
   // FECGPU_ERR_INVALID so the caller takes the launch path (0)
   g_knob[K_BLOCK_SVC] = num(getenv("FECGPU_BLOCK_SVC"), 1) != 0;
+  // recover data pass: a group's workspace records copied into LDS in one round trip (1) or read
+  // where they lie during the setup (0)
+  g_knob[K_WS_LDS] = num(getenv("FECGPU_WS_LDS"), 1) != 0;
 }
 
 static inline int knob(KnobId id) {
@@ -114,6 +117,8 @@ static int set_err(int code, const char *fmt, const char *what) {
 // =============================================================================================
 // Workspace layout of the decode plan (bytes per block).
 // =============================================================================================
+constexpr size_t kWsLdsMax = 4096;  // bytes of workspace records a recover group stages in LDS
+
 struct WsLayout {
   uint32_t em;      // e_max = min(k, r)
   uint32_t off_unk, off_sel, off_slot, off_nz, off_D, off_dep, stride;
@@ -1364,10 +1369,14 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
       uint16_t *row0 = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB);
       uint16_t *row = row0 + FEC_BS_FIELD_SLOT(RT, i);  // field i of source j
       if (g < ng && i < rt) {
+#ifdef FEC_PROBE_CONSTCOEF  // timing probe only (wrong repairs): no TinyMT32 in the group setup
+        for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD((uint32_t)(0x53 + j + i) & 0xffu, i);
+#else
         Tmt t;
         const uint32_t f = fbn ? fbn[b] : (uint32_t)((fbn_base + b * fbn_step) & 0xffffffu);
         tmt_init(t, rlc_seed(f, (uint32_t)(r0w + i)));
         for (int j = 0; j < k; j++) row[j * (CSB / 2)] = FEC_BS_FIELD(tmt_coef(t), i);
+#endif
       } else {
         for (int j = 0; j < k; j++) row[j * (CSB / 2)] = 0;  // ends the chain: repair i is not live
       }
@@ -1436,7 +1445,7 @@ template <int RT, int VEC>
 __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_t *__restrict__ src,
                                  const uint8_t *__restrict__ rep, uint64_t nblocks, int k, int r, int L, int nchunks,
                                  int chunk_bytes, uint8_t *ws, int r0, int G, uint8_t *status, uint64_t *recovered,
-                                 int ilv, uint8_t *dst, uint8_t *lds) {
+                                 int ilv, uint8_t *dst, uint8_t *lds, uint8_t *wsl = nullptr) {
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   RecoverLds<RT> S(lds, G, k);
@@ -1444,12 +1453,33 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
     const uint64_t b0 = ilv ? q : q * G;
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
+    // wsl: the group's workspace records are copied into LDS first, 16 B per lane-piece, so the setup
+    // below costs one memory round trip per group instead of a chain of dependent ones (header ->
+    // coefficient rows / slots -> unknowns and dependencies)
+    if (wsl) {
+      const int per = (int)(WL.stride >> 4), np = ng * per;
+      for (int x = lane; x < np; x += 64) {
+        const int g = x / per, o = x - g * per;
+        reinterpret_cast<uint4 *>(wsl)[x] =
+            reinterpret_cast<const uint4 *>(ws + (b0 + g * bstep) * (uint64_t)WL.stride)[o];
+      }
+      __syncthreads();
+    }
+    // record of block g of the group (LDS copy or workspace)
+    auto recg = [&](int g) -> const uint8_t * {
+      return wsl ? wsl + (size_t)g * WL.stride : ws + (b0 + g * bstep) * (uint64_t)WL.stride;
+    };
     bool act = false;
     int st = FECGPU_BLOCK_NOTHING, e = 0;
     if (lane < ng) {
-      const uint8_t *h = ws + (b0 + lane * bstep) * (uint64_t)WL.stride;
+#ifdef FEC_PROBE_NOWS  // timing probe only (wrong bytes): the group setup reads no workspace
+      st = FECGPU_BLOCK_RECOVERED;
+      e = RT < r ? RT : r;
+#else
+      const uint8_t *h = recg(lane);
       st = h[0];
       e = h[1];
+#endif
       act = st == FECGPU_BLOCK_RECOVERED && e > r0;
     }
     const uint64_t am = __ballot(act);
@@ -1466,13 +1496,21 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
       const int t = x / k, j = x - t * k;
       const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
-      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      const uint8_t *h = recg(S.gid[t]);
       constexpr int NF = RecoverLds<RT>::CSB / 2;  // fields per source (>= 4)
       uint16_t *row = reinterpret_cast<uint16_t *>(S.coef + (size_t)x * RecoverLds<RT>::CSB);
+#ifdef FEC_PROBE_NOWS
+      (void)h;
+#pragma unroll
+      for (int u = 0; u < NF; u++)
+        row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD((uint32_t)(0x53 + j + u) & 0xffu, u) : (uint16_t)0;
+      const uint32_t sl = j < k - rt ? (uint32_t)(j + rt) : (uint32_t)(0x80 | (j - (k - rt)));
+#else
 #pragma unroll
       for (int u = 0; u < NF; u++)  // case offset of D[u][j]; 0 past the live unknowns ends the chain
         row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD(h[WL.off_D + (r0 + u) * k + j], u) : (uint16_t)0;
       const uint32_t sl = h[WL.off_slot + j];
+#endif
       const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
                                      : src + (b * (uint64_t)k + sl) * (uint64_t)L;
       S.intab[x] = (uint64_t)(uintptr_t)p;
@@ -1482,21 +1520,28 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
       const int t = x >> 4, u = x & 15;
       const uint64_t b = b0 + S.gid[t] * bstep;
       const int rt = S.ecnt[t];
-      const uint8_t *h = ws + b * (uint64_t)WL.stride;
+      const uint8_t *h = recg(S.gid[t]);
       uint8_t *rc = S.rec + (size_t)t * kDecRec;
       rc[kDecRecNz + u] = 0;
       if (u < rt) {
+#ifdef FEC_PROBE_NOWS
+        const int j = u;
+#else
         const int j = h[WL.off_unk + r0 + u];
+#endif
         reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
+#ifndef FEC_PROBE_NOWS
           for (int v = u + 1; v < rt; v++) m |= (uint32_t)(h[WL.off_dep + u * WL.em + v] != 0) << v;
+#endif
           S.unk[x] = (uint8_t)j;
           S.depm[x] = m;
         }
       }
       if (u == 0) {
-        reinterpret_cast<uint64_t *>(rc)[kDecRecNzPtr] = (uint64_t)(uintptr_t)(h + WL.off_nz + r0);
+        reinterpret_cast<uint64_t *>(rc)[kDecRecNzPtr] =
+            (uint64_t)(uintptr_t)(ws + b * (uint64_t)WL.stride + WL.off_nz + r0);
         reinterpret_cast<uint32_t *>(rc)[kDecRecRt] = (uint32_t)rt;
       }
     }
@@ -1556,13 +1601,13 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
                                                        uint8_t *status, uint64_t *recovered, int ilv,
-                                                       uint8_t *dst) {
+                                                       uint8_t *dst, uint32_t wsl_off) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x)
     recover_bs_group<RT, VEC>(q, NG, bstep, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, r0, G, status,
-                              recovered, ilv, dst, lds);
+                              recovered, ilv, dst, lds, wsl_off ? lds + wsl_off : nullptr);
 }
 
 // Encode with the rows given by address (fecgpu_rlc_encode_rows): the batching adapter hands the
@@ -2011,10 +2056,17 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                               uint8_t *dst) {
   const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, nb);
-  const size_t lds = RecoverLds<RT>::bytes(G, k);
+  size_t lds = RecoverLds<RT>::bytes(G, k);
+  // the group's workspace records staged in LDS by one round trip (knob ws_lds) when they are small
+  const size_t wsb = (size_t)G * ws_layout((uint32_t)k, (uint32_t)r).stride;
+  uint32_t wsl_off = 0;
+  if (knob(K_WS_LDS) && wsb <= kWsLdsMax && ((uintptr_t)ws & 15) == 0) {
+    wsl_off = (uint32_t)((lds + 15) & ~(size_t)15);
+    lds = wsl_off + wsb;
+  }
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst);
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, wsl_off);
 }
 
 template <int RT, int VEC>
@@ -2352,11 +2404,17 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       uint8_t *rc = S.rec + (size_t)t * kDecRec;
       rc[kDecRecNz + u] = 0;
       if (u < rt) {
+#ifdef FEC_PROBE_NOWS
+        const int j = u;
+#else
         const int j = h[WL.off_unk + r0 + u];
+#endif
         reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
+#ifndef FEC_PROBE_NOWS
           for (int v = u + 1; v < rt; v++) m |= (uint32_t)(h[WL.off_dep + u * WL.em + v] != 0) << v;
+#endif
           S.unk[x] = (uint8_t)j;
           S.depm[x] = m;
         }

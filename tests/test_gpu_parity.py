@@ -211,6 +211,42 @@ def test_decode_vs_oracle(eng, oracle, k, r, L, nb, emax):
     assert {DEC_RECOVERED, DEC_NOTHING} <= set(st.tolist())
 
 
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 12288), (32, 8, 1200, 4100), (12, 6, 1204, 9000)])
+def test_decode_ws_lds_vs_oracle(eng, oracle, k, r, L, nb):
+    """Batches large enough for multi-block groups in the recover data pass: the group's plan
+    records staged in LDS by one round trip (knob ws_lds = 1, default) or read in place (0) give
+    the oracle's statuses, masks and bytes."""
+    rng = np.random.default_rng(k * 7 + nb)
+    src_h = synth_bytes(nb * k * L, 91 + k).reshape(nb, k, L)
+    fbn_base = int(rng.integers(0, 1 << 24))
+    rep_h = oracle.rlc_encode_batch(src_h, r, fbn_base)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    full_k, full_r = (1 << k) - 1, (1 << r) - 1
+    for b in range(nb):
+        e = int(rng.integers(0, r + 1))
+        miss = rng.choice(k, e, replace=False)
+        sp[b, 0] = full_k & ~int(sum(1 << int(j) for j in miss))
+        drop = rng.choice(r, int(rng.integers(0, 2)), replace=False)  # sometimes one repair short
+        rp[b, 0] = full_r & ~int(sum(1 << int(i) for i in drop))
+    ref = src_h.copy()
+    for b in range(nb):
+        for j in range(k):
+            if not (int(sp[b, 0]) >> j) & 1:
+                ref[b, j] = 0xA5
+    st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
+    jbit = np.uint64(1) << np.arange(k, dtype=np.uint64)
+    keep = ((rec_ref[:, 0:1] | sp[:, 0:1]) & jbit) != 0  # recovered or received: [nb, k]
+    for v in (1, 0):
+        with eng.knob("ws_lds", v):
+            _, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+        assert np.array_equal(st, st_ref), v
+        assert np.array_equal(rec, rec_ref), v
+        assert np.array_equal(got[keep], src_h[keep]), v
+        assert np.array_equal(ref[keep], src_h[keep])
+    assert (st_ref == DEC_RECOVERED).sum() > nb // 2
+
+
 @pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 1), (16, 4, 1200, 64), (32, 8, 1200, 7), (5, 5, 20, 33),
                                       (64, 16, 9000, 3), (20, 16, 2052, 9), (3, 1, 4, 2), (32, 9, 1200, 5),
                                       (1, 1, 16, 3), (31, 8, 100, 17)])
