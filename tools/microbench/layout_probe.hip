@@ -29,7 +29,16 @@ struct Lay {
   }
 };
 
-template <int G, bool DEC>
+// Random-erasure decode (round 3): MODE 1 = the R erased sources of block b are a random R-subset
+// (one of 64 fixed masks, picked by a hash of b), read in slot order as the recover pass does;
+// MODE 2 = the same, the recovered rows written packed (out[b][i]) instead of at their slots.
+__constant__ uint32_t kEras[64];
+__device__ __forceinline__ int nth_bit(uint32_t m, int n) {
+  for (int i = 0; i < n; i++) m &= m - 1;
+  return __ffs(m) - 1;
+}
+
+template <int G, bool DEC, int MODE = 0>
 __global__ __launch_bounds__(64) void pattern(const uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                               uint8_t *__restrict__ out, uint64_t nblocks, int sm) {
   const int lane = threadIdx.x;
@@ -51,7 +60,12 @@ __global__ __launch_bounds__(64) void pattern(const uint8_t *__restrict__ src, c
         for (int jj = 0; jj < 8; jj++) {
           const int j = j0 + jj;
           const uint8_t *p = src + ly.row(b, j, K);
-          if (DEC && j >= e0 && j < e0 + R) p = rep + ly.row(b, j - e0, R);
+          if (MODE) {
+            const uint32_t m = kEras[(b * 0x9E3779B1u >> 7) & 63];
+            if ((m >> j) & 1) p = rep + ly.row(b, __popc(m & ((1u << j) - 1)), R);
+          } else if (DEC && j >= e0 && j < e0 + R) {
+            p = rep + ly.row(b, j - e0, R);
+          }
           a0[jj] = j < K ? __builtin_nontemporal_load((const u32x4 *)(p + o0)) : (u32x4)0;
           a1[jj] = (ok1 && j < K) ? __builtin_nontemporal_load((const u32x4 *)(p + o1)) : (u32x4)0;
         }
@@ -61,10 +75,55 @@ __global__ __launch_bounds__(64) void pattern(const uint8_t *__restrict__ src, c
 #pragma unroll
       for (int i = 0; i < R; i++) {
         uint8_t *p = DEC ? out + ly.row(b, e0 + i, K) : out + ly.row(b, i, R);
+        if (MODE == 1) p = out + ly.row(b, nth_bit(kEras[(b * 0x9E3779B1u >> 7) & 63], i), K);
+        if (MODE == 2) p = out + ly.row(b, i, R);
         __builtin_nontemporal_store(x0 + (uint32_t)i, (u32x4 *)(p + o0));
         if (ok1) __builtin_nontemporal_store(x1 + (uint32_t)i, (u32x4 *)(p + o1));
       }
     }
+  }
+}
+
+// Split pattern (round 3): W waves per block (one workgroup per block), wave w XORs the rows
+// w, w + W, ... (ILV: the W waves read W adjacent rows at a time) or the contiguous chunk
+// [w K/W, (w + 1) K/W); the partials meet in LDS and wave w writes the output rows i = w mod W.  The
+// resident waves then work on W times fewer blocks at once (a smaller window of HBM pages).
+template <int W, bool ILV>
+__global__ __launch_bounds__(64 * W) void split(const uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
+                                                uint8_t *__restrict__ out, uint64_t nblocks, int) {
+  __shared__ u32x4 red[W][2][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int A = (L / 16 + 1) / 2;
+  constexpr int KW = K / W;
+  const uint32_t o0 = 16 * lane, o1 = 16 * (lane + A);
+  const bool ok0 = lane < A, ok1 = lane + A < L / 16;
+  for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    u32x4 x0 = 0, x1 = 0;
+    for (int i0 = 0; i0 < KW; i0 += 4) {
+      u32x4 a0[4], a1[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const int i = i0 + jj;
+        const int j = ILV ? w + W * i : w * KW + i;
+        const uint8_t *p = src + (b * K + j) * (uint64_t)L;
+        a0[jj] = (ok0 && i < KW) ? __builtin_nontemporal_load((const u32x4 *)(p + o0)) : (u32x4)0;
+        a1[jj] = (ok1 && i < KW) ? __builtin_nontemporal_load((const u32x4 *)(p + o1)) : (u32x4)0;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) { x0 ^= a0[jj]; x1 ^= a1[jj]; }
+    }
+    red[w][0][lane] = x0;
+    red[w][1][lane] = x1;
+    __syncthreads();
+    u32x4 y0 = 0, y1 = 0;
+#pragma unroll
+    for (int v = 0; v < W; v++) { y0 ^= red[v][0][lane]; y1 ^= red[v][1][lane]; }
+    for (int i = w; i < R; i += W) {
+      uint8_t *p = out + (b * R + i) * (uint64_t)L;
+      if (ok0) __builtin_nontemporal_store(y0 + (uint32_t)i, (u32x4 *)(p + o0));
+      if (ok1) __builtin_nontemporal_store(y1 + (uint32_t)i, (u32x4 *)(p + o1));
+    }
+    __syncthreads();
   }
 }
 
@@ -87,7 +146,56 @@ int main() {
     printf("%-58s %8.3f ms  %7.0f GB/s\n", name, best, bytes / (best * 1e-3) / 1e9);
     fflush(stdout);
   };
+  auto runw = [&](const char *name, size_t lds, auto kern, int W) {
+    float best = 1e9;
+    for (int it = 0; it < 6; it++) {
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(kern, dim3((uint32_t)nb), dim3(64 * W), lds, 0, src, rep, rep, nb, 0);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (it) best = std::min(best, ms);
+    }
+    const double bytes = (double)nb * (K + R) * L;
+    printf("%-58s %8.3f ms  %7.0f GB/s\n", name, best, bytes / (best * 1e-3) / 1e9);
+    fflush(stdout);
+  };
   printf("# k%d r%d L%d, %llu blocks\n", K, R, L, (unsigned long long)nb);
+  {
+    uint32_t em[64];
+    srand(7);
+    for (int i = 0; i < 64; i++) {
+      uint32_t m = 0;
+      while (__builtin_popcount(m) < R) m |= 1u << (rand() % K);
+      em[i] = m;
+    }
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(kEras), em, sizeof em));
+  }
+  if (getenv("DEC_ONLY")) {  // decode patterns: contiguous erased run / random erasures / random + packed output
+    for (size_t lds : {(size_t)13 << 10, (size_t)10 << 10}) {
+      const int wps = lds == ((size_t)13 << 10) ? 3 : 4;
+      char nm[96];
+#define RUND(G_, M_)                                                                              \
+      snprintf(nm, sizeof nm, "decode G%-2d %s %d waves/SIMD", G_,                                \
+               M_ == 0 ? "erased run      " : M_ == 1 ? "random erasures " : "random, packed  ", wps); \
+      run(nm, lds, pattern<G_, true, M_>, (nb + G_ - 1) / G_, 0, true);
+      RUND(8, 0) RUND(8, 1) RUND(8, 2) RUND(2, 1) RUND(2, 2) RUND(1, 1) RUND(1, 2)
+      snprintf(nm, sizeof nm, "encode G2  block-major  %d waves/SIMD", wps);
+      run(nm, lds, pattern<2, false>, (nb + 1) / 2, 0, false);
+    }
+    return 0;
+  }
+  if (getenv("SPLIT_ONLY")) {  // encode pattern: one wave per block vs W waves per block
+    for (size_t per : {(size_t)13 << 10, (size_t)10 << 10}) {  // LDS per wave: 3 / 4 waves per SIMD
+      const int wps = per == ((size_t)13 << 10) ? 3 : 4;
+      char nm[96];
+      snprintf(nm, sizeof nm, "encode G1  block-major  %d waves/SIMD", wps);
+      run(nm, per, pattern<1, false>, nb, 0, false);
+#define RUNS(W_, I_)                                                                              \
+      snprintf(nm, sizeof nm, "encode split W%d %s %d waves/SIMD", W_, I_ ? "rows-ilv  " : "rows-chunk", wps); \
+      runw(nm, per * W_ - sizeof(u32x4) * W_ * 128, split<W_, I_>, W_);
+      RUNS(2, true) RUNS(2, false) RUNS(4, true) RUNS(4, false)
+    }
+    return 0;
+  }
   for (size_t lds : {(size_t)13 << 10, (size_t)10 << 10}) {  // 3 / 4 waves per SIMD
     for (int dec = 0; dec < 2; dec++)
       for (int sm = 0; sm < 2; sm++) {
