@@ -93,15 +93,19 @@ def make_erasures(torch, nb, k, e, seed, dev):
 
 
 def check_recovered(torch, dst, src, ok, miss, nb, k, L, what):
-    """Decode gate: in every recovered block, the rows written for the erased symbols equal the
-    originals (recovered rows go to their own buffer, src's layout; only erased rows are written)."""
+    """Decode gate: in every recovered block, the recovered symbols equal the originals.  dst holds
+    them packed (fecgpu_rlc_decode_apply_packed: row u of block b = its u-th erased source, ascending),
+    one new row per recovered symbol, as the reference's fec_recover allocates each anew."""
     e = miss.shape[1]
-    miss = miss.to(src.device)
+    miss = miss.to(src.device).sort(dim=1).values
+    em = dst.shape[1]
     for c0 in range(0, nb, 1 << 16):  # chunked: no full-size temporaries
         c1 = min(nb, c0 + (1 << 16))
         b = torch.arange(c0, c1, device=src.device)
-        rows = (b.unsqueeze(1) * k + miss[c0:c1]).reshape(-1)[ok[c0:c1].repeat_interleave(e)]
-        assert bool((dst.view(nb * k, L)[rows] == src.view(nb * k, L)[rows]).all()), what
+        okc = ok[c0:c1].repeat_interleave(e)
+        rows = (b.unsqueeze(1) * k + miss[c0:c1]).reshape(-1)[okc]
+        drows = (b.unsqueeze(1) * em + torch.arange(e, device=src.device)).reshape(-1)[okc]
+        assert bool((dst.view(nb * em, L)[drows] == src.view(nb * k, L)[rows]).all()), what
 
 
 def encode_kernel_name(k, r, L):
@@ -140,10 +144,10 @@ def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
     rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
     ws = eng.alloc_workspace(nb, k, r)
-    rec_rows = torch.empty_like(src)  # recovered symbols (new buffers, as fec_recover allocates them)
+    rec_rows = torch.empty((nb, min(k, r), L), dtype=torch.uint8, device=dev)  # recovered symbols, packed
     stream = torch.cuda.current_stream(dev)
     eng.rlc_encode(src, rep, k, r, L)
-    eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, dst=rec_rows)
+    eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, dst=rec_rows, packed=True)
     torch.cuda.synchronize()
     ok = st == 0
     check_recovered(torch, rec_rows, src, ok, miss, nb, k, L, f"k{k} r{r} decode did not restore the sources")
@@ -152,7 +156,7 @@ def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
     for _ in range(reps):
         ev[0].record(stream)
         eng.rlc_encode(src, rep, k, r, L)
-        eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, events=ev[1:], dst=rec_rows)
+        eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, events=ev[1:], dst=rec_rows, packed=True)
         torch.cuda.synchronize()
         for i in range(3):
             t[i] += ev[i].elapsed_time(ev[i + 1]) / reps
@@ -624,14 +628,15 @@ def main():
         recovered = torch.empty((nb, 2), dtype=torch.int64, device=dev)
         ws = eng.alloc_workspace(nb, k, r)
         # decode input: the received block (erased slots hold stale bytes), copied once.  The recovered
-        # symbols go to their own buffer -- the reference's fec_recover allocates new source symbols
-        # rather than writing into the received block (rlc_fec_scheme_gf256.c:218-236) -- which also
-        # keeps the writes out of the rows being read (in place measured 5 % slower,
-        # profiles/r01_ab_apply_to.log)
+        # symbols go to their own rows -- the reference's fec_recover allocates every recovered source
+        # symbol anew rather than writing into the received block (rlc_fec_scheme_gf256.c:218-236) --
+        # packed per block (row u = the u-th erased source): in place measured 5 % slower
+        # (profiles/r01_ab_apply_to.log), rows at their src-layout slots 2.3 % slower than packed
+        # (profiles/r03_ab_apply_packed.log: each leaves two half-written 128-B lines)
         work.copy_(src)
         idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.to(dev)).reshape(-1)
         work.view(nb * k, L)[idx] = 0xA5
-        rec_rows = torch.empty_like(src)
+        rec_rows = torch.empty((nb, min(k, r), L), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     # The decode plan needs only the presence masks and block numbers, not the repairs: it runs on a
     # second stream beside the encode (independent work, as a receiver plans from packet headers while
@@ -664,7 +669,7 @@ def main():
                 stream.wait_event(planned)
                 if tm:
                     tm[2].record(stream)
-                eng.rlc_decode_apply_to(work, rep, rec_rows, status, recovered, k, r, L, m, ws)
+                eng.rlc_decode_apply_packed(work, rep, rec_rows, status, recovered, k, r, L, m, ws)
                 if tm:
                     tm[3].record(stream)
             elif tm:
@@ -834,7 +839,8 @@ def main():
                 "passes_per_step": passes,
                 "parallelism": f"independent FEC blocks, {world} GPU(s), no collective"}
         if e:
-            conf["decode_output"] = "recovered symbols into their own buffer (as fec_recover allocates them)"
+            conf["decode_output"] = ("recovered symbols into new rows, packed per block (as fec_recover "
+                                     "allocates each recovered symbol anew)")
         if passes > 1:
             conf["note"] = (f"a GPU's share ({share} blocks) exceeds HBM: each step codes it in {passes} passes "
                             f"over {nb} resident blocks, block numbers advancing per pass")

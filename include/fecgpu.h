@@ -126,6 +126,18 @@ int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint
                                uint32_t k, uint32_t r, uint32_t symbol_size, uint8_t *status,
                                uint64_t *recovered, void *workspace, size_t workspace_bytes,
                                void *stream);
+/* apply with the recovered symbols packed: dst is [nblocks][min(k, r)][symbol_size] and row u of
+ * block b receives the u-th missing source of b in ascending source order (the u-th clear bit of
+ * src_present below k); rows past the block's erasures and rows whose recovered[] bit stays clear are
+ * unspecified.  The reference's fec_recover allocates every recovered symbol anew
+ * (rlc_fec_scheme_gf256.c:218-236), so a packed row per recovered symbol is as faithful as src's
+ * layout, and a block's rows are contiguous: no written row shares a cache line with bytes the pass
+ * does not write (recovered rows at their src-layout slots leave two half-written 128-B lines each,
+ * which the memory system fetches to merge). */
+int fecgpu_rlc_decode_apply_packed(const void *src, const void *rep, void *dst, uint64_t nblocks,
+                                   uint32_t k, uint32_t r, uint32_t symbol_size, uint8_t *status,
+                                   uint64_t *recovered, void *workspace, size_t workspace_bytes,
+                                   void *stream);
 
 /* RLC decode with the coefficients of every received repair seeded by its own FPID, as the
  * reference does (get_coefs(..., rs->repair_fec_payload_id.source_fpid.raw, ...),

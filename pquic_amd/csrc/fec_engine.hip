@@ -1438,6 +1438,14 @@ struct RecoverLds {
   }
 };
 
+// Row of dst that receives the recovered source j (unknown number `unk` of block b): src's layout
+// ([block][k] rows, dst_rows == 0) or packed ([block][dst_rows] rows, unknowns in ascending source
+// order; fecgpu_rlc_decode_apply_packed).  Packed rows of a block are contiguous, so no written row
+// leaves a 128-B line half written next to bytes the pass does not own.
+__device__ __forceinline__ uint64_t rec_row(uint64_t b, int k, int j, int dst_rows, int unk) {
+  return dst_rows ? b * (uint64_t)dst_rows + (uint64_t)unk : b * (uint64_t)k + (uint64_t)j;
+}
+
 // One group of the recover data pass (group q of NG, blocks b0, b0 + bstep, ...); every lane of the
 // wave calls it.  k_rlc_recover_bs runs it over a grid-stride loop; k_rlc_decode_small after the
 // wave plan of the group's block.
@@ -1445,7 +1453,7 @@ template <int RT, int VEC>
 __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_t *__restrict__ src,
                                  const uint8_t *__restrict__ rep, uint64_t nblocks, int k, int r, int L, int nchunks,
                                  int chunk_bytes, uint8_t *ws, int r0, int G, uint8_t *status, uint64_t *recovered,
-                                 int ilv, uint8_t *dst, uint8_t *lds, uint8_t *wsl = nullptr) {
+                                 int ilv, uint8_t *dst, uint8_t *lds, uint8_t *wsl = nullptr, int dst_rows = 0) {
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x;
   RecoverLds<RT> S(lds, G, k);
@@ -1529,7 +1537,7 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
 #else
         const int j = h[WL.off_unk + r0 + u];
 #endif
-        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
+        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + rec_row(b, k, j, dst_rows, r0 + u) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
 #ifndef FEC_PROBE_NOWS
@@ -1601,13 +1609,13 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
                                                        uint8_t *status, uint64_t *recovered, int ilv,
-                                                       uint8_t *dst, uint32_t wsl_off) {
+                                                       uint8_t *dst, uint32_t wsl_off, int dst_rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
   const uint64_t bstep = ilv ? NG : 1;
   for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x)
     recover_bs_group<RT, VEC>(q, NG, bstep, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, r0, G, status,
-                              recovered, ilv, dst, lds, wsl_off ? lds + wsl_off : nullptr);
+                              recovered, ilv, dst, lds, wsl_off ? lds + wsl_off : nullptr, dst_rows);
 }
 
 // Encode with the rows given by address (fecgpu_rlc_encode_rows): the batching adapter hands the
@@ -2054,7 +2062,7 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
 template <int RT, int VEC>
 static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                               uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
-                              uint8_t *dst) {
+                              uint8_t *dst, int dst_rows) {
   const int G = bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT) + 8, kDecRec + 80, false, c.nchunks, nb);
   size_t lds = RecoverLds<RT>::bytes(G, k);
   // the group's workspace records staged in LDS by one round trip (knob ws_lds) when they are small
@@ -2066,7 +2074,8 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
   }
   const uint64_t groups = (nb + G - 1) / G;
   hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, wsl_off);
+                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, wsl_off,
+                     dst_rows);
 }
 
 template <int RT, int VEC>
@@ -2349,7 +2358,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint8_t *ws, int r0, int G,
                                                         uint8_t *status, uint64_t *recovered, int ilv,
-                                                        uint8_t *dst, uint32_t slotb) {
+                                                        uint8_t *dst, uint32_t slotb, int dst_rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x & 63;
@@ -2409,7 +2418,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
 #else
         const int j = h[WL.off_unk + r0 + u];
 #endif
-        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + (b * (uint64_t)k + j) * (uint64_t)L);
+        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + rec_row(b, k, j, dst_rows, r0 + u) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
 #ifndef FEC_PROBE_NOWS
@@ -2531,7 +2540,7 @@ static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int
 template <int RT>
 static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
                                uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
-                               uint8_t *dst) {
+                               uint8_t *dst, int dst_rows) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
   const size_t ring_bytes = (size_t)Bs2Depth16::dec * slotb;
   const int per_j = FEC_BS_COEF_ROW_BYTES(RT) + 8, per_block = kDecRec + 80;
@@ -2539,14 +2548,14 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
     const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + kCwWaves * ring_bytes;
     hipLaunchKernelGGL((k_rlc_recover_bs2<RT, true>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * kCwWaves), lds, s,
                        src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered,
-                       interleave_groups(), dst, slotb);
+                       interleave_groups(), dst, slotb, dst_rows);
     return;
   }
   const int G = bs2_group(RT, k, per_j, per_block, false, c.nchunks, ring_bytes, bs2_waves_per_cu(RT), nb);
   const size_t stage = pad16((uint32_t)RecoverLds<RT>::bytes(G, k));
   hipLaunchKernelGGL((k_rlc_recover_bs2<RT, false>), dim3(grid_for((nb + G - 1) / G)), dim3(64), stage + ring_bytes, s,
                      src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(),
-                     dst, slotb);
+                     dst, slotb, dst_rows);
 }
 
 // The ring path applies to 16-repair / 16-unknown tiles of 16-B pieces (symbol_size >= 16) and blocks
@@ -3209,7 +3218,7 @@ static int launch_finalize(uint64_t nblocks, uint32_t k, uint32_t r, uint8_t *st
 // is the in-place form).  Inputs are only ever read from src/rep, outputs only written to dst.
 static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
                              uint32_t r, uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
-                             void *workspace, size_t workspace_bytes, hipStream_t s) {
+                             void *workspace, size_t workspace_bytes, hipStream_t s, int dst_rows = 0) {
   static const uint64_t dummy = 0;
   int rc = decode_args(src, rep, nblocks, k, r, symbol_size, &dummy, &dummy, status, recovered, workspace,
                        workspace_bytes);
@@ -3231,11 +3240,11 @@ static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64
     if (ring) {
       FEC_BS2_DISPATCH(launch_recover_bs2, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
                        (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
-                       (uint8_t *)dst)
+                       (uint8_t *)dst, dst_rows)
     } else {
       FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
                       (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
-                      (uint8_t *)dst)
+                      (uint8_t *)dst, dst_rows)
     }
   }
   HIPCHK(hipGetLastError());
@@ -3254,6 +3263,14 @@ int fecgpu_rlc_decode_apply_to(const void *src, const void *rep, void *dst, uint
                                void *workspace, size_t workspace_bytes, void *stream) {
   return decode_apply_impl(src, rep, dst, nblocks, k, r, symbol_size, status, recovered, workspace,
                            workspace_bytes, (hipStream_t)stream);
+}
+
+int fecgpu_rlc_decode_apply_packed(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                                   uint32_t r, uint32_t symbol_size, uint8_t *status, uint64_t *recovered,
+                                   void *workspace, size_t workspace_bytes, void *stream) {
+  const uint32_t em = k < r ? k : r;
+  return decode_apply_impl(src, rep, dst, nblocks, k, r, symbol_size, status, recovered, workspace,
+                           workspace_bytes, (hipStream_t)stream, em ? (int)em : 1);
 }
 
 extern "C++" {

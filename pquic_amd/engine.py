@@ -55,6 +55,7 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_rlc_decode_seeded.argtypes = [v, v, u64, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply_to.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
+    L.fecgpu_rlc_decode_apply_packed.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
     L.fecgpu_set_knob.argtypes = [C.c_char_p, C.c_int]
@@ -209,10 +210,11 @@ class Engine:
         return status, recovered
 
     def rlc_decode_stages(self, src, rep, src_present, rep_present, status, recovered, k, r, L, nblocks,
-                          workspace, fbn_base=0, stream=None, events=None, dst=None):
+                          workspace, fbn_base=0, stream=None, events=None, dst=None, packed=False):
         """fecgpu_rlc_decode as its two stages (plan, apply); events[i] (if given) recorded before
         stage i and events[2] after the last, on the launch stream.  dst: write the recovered rows
-        there (src's layout, fecgpu_rlc_decode_apply_to) instead of into src."""
+        there (src's layout, fecgpu_rlc_decode_apply_to; packed=True: [nblocks][min(k, r)] rows,
+        fecgpu_rlc_decode_apply_packed) instead of into src."""
         st = self._stream(stream)
         torch_stream = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         rec = (lambda i: events[i].record(torch_stream)) if events else (lambda i: None)
@@ -221,7 +223,12 @@ class Engine:
                                                     _addr(rep_present), _addr(workspace), workspace.numel(), st),
                     "fecgpu_rlc_decode_plan")
         rec(1)
-        if dst is None:
+        if dst is not None and packed:
+            self._check(self.lib.fecgpu_rlc_decode_apply_packed(_addr(src), _addr(rep), _addr(dst), nblocks, k, r,
+                                                                L, _addr(status), _addr(recovered),
+                                                                _addr(workspace), workspace.numel(), st),
+                        "fecgpu_rlc_decode_apply_packed")
+        elif dst is None:
             self._check(self.lib.fecgpu_rlc_decode_apply(_addr(src), _addr(rep), nblocks, k, r, L, _addr(status),
                                                          _addr(recovered), _addr(workspace), workspace.numel(), st),
                         "fecgpu_rlc_decode_apply")
@@ -252,6 +259,15 @@ class Engine:
                                                         _addr(status), _addr(recovered), _addr(workspace),
                                                         workspace.numel(), self._stream(stream)),
                     "fecgpu_rlc_decode_apply_to")
+        return status, recovered
+
+    def rlc_decode_apply_packed(self, src, rep, dst, status, recovered, k, r, L, nblocks, workspace, stream=None):
+        """fecgpu_rlc_decode_apply_packed: as apply, recovered symbols packed into dst [nblocks][min(k, r)][L]
+        (row u = the u-th missing source of the block, ascending)."""
+        self._check(self.lib.fecgpu_rlc_decode_apply_packed(_addr(src), _addr(rep), _addr(dst), nblocks, k, r, L,
+                                                            _addr(status), _addr(recovered), _addr(workspace),
+                                                            workspace.numel(), self._stream(stream)),
+                    "fecgpu_rlc_decode_apply_packed")
         return status, recovered
 
     def xor_decode(self, src, rep, src_present, rep_present, status, recovered, k: int, L: int,

@@ -757,6 +757,50 @@ def test_decode_apply_to_separate_buffer(eng, oracle):
                 assert (got[b, j] == 0xC3).all()
 
 
+@pytest.mark.parametrize("k,r,L,nb,group", [(16, 4, 1200, 300, 0), (16, 4, 1200, 12288, 0), (16, 4, 1200, 12288, 2),
+                                            (32, 8, 1200, 4100, 0), (64, 16, 9000, 40, 0), (40, 20, 4100, 30, 0),
+                                            (10, 3, 4, 200, 0)])
+def test_decode_apply_packed(eng, oracle, k, r, L, nb, group):
+    """fecgpu_rlc_decode_apply_packed: row u of dst[b] receives the u-th missing source of block b
+    (ascending), every recovered one equal to the original; rows past the block's erasures are
+    untouched; src is only read.  Single and multi-pass tiles (e > 16), ring and register bodies."""
+    em = min(k, r)
+    rng = np.random.default_rng(k * 3 + nb)
+    src_h = synth_bytes(nb * k * L, 93 + k).reshape(nb, k, L)
+    rep_h = oracle.rlc_encode_batch(src_h, r, 11)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = masks_from_lists(nb, r, [list(range(r))] * nb)
+    work_h = src_h.copy()
+    missing = []
+    for b in range(nb):
+        miss = sorted(rng.choice(k, int(rng.integers(0, em + 1)), replace=False).tolist())
+        missing.append(miss)
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        work_h[b, miss] = 0x33
+    work, rep = to_dev(work_h), to_dev(rep_h)
+    dst = torch.full((nb, em, L), 0xC3, dtype=torch.uint8, device=DEV)
+    st = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+    ws = eng.alloc_workspace(nb, k, r)
+    with eng.knob("group", group):
+        eng.rlc_decode_plan(to_dev(sp), to_dev(rp), k, r, nb, ws, fbn_base=11)
+        eng.rlc_decode_apply_packed(work, rep, dst, st, rec, k, r, L, nb, ws)
+        torch.cuda.synchronize()
+    ref = work_h.copy()
+    st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, 11)
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    rec_h = rec.cpu().numpy().view(np.uint64)
+    assert np.array_equal(rec_h, rec_ref)
+    got = dst.cpu().numpy()
+    assert np.array_equal(work.cpu().numpy(), work_h)  # src untouched
+    for b in range(nb):
+        recd = set(bits(rec_h[b], k))
+        for u, j in enumerate(missing[b]):
+            if j in recd:
+                assert np.array_equal(got[b, u], src_h[b, j]), (b, u, j)
+        assert (got[b, len(missing[b]):] == 0xC3).all(), b
+
+
 def test_host_decode_zero_copy_pinned(oracle):
     """fecgpu_rlc_decode_host on page-locked buffers: the apply kernel writes the recovered rows
     straight into the host block (no source rows copied back); same bytes as the pageable path."""
