@@ -184,11 +184,14 @@ int main() {
     return 0;
   }
   if (getenv("SPLIT_ONLY")) {  // encode pattern: one wave per block vs W waves per block
-    for (size_t per : {(size_t)13 << 10, (size_t)10 << 10}) {  // LDS per wave: 3 / 4 waves per SIMD
+    for (int rep = 0; rep < 6; rep++) {  // alternating, so drift hits every variant alike
+      const size_t per = rep & 1 ? (size_t)10 << 10 : (size_t)13 << 10;  // LDS per wave: 3 / 4 waves per SIMD
       const int wps = per == ((size_t)13 << 10) ? 3 : 4;
       char nm[96];
       snprintf(nm, sizeof nm, "encode G1  block-major  %d waves/SIMD", wps);
       run(nm, per, pattern<1, false>, nb, 0, false);
+      snprintf(nm, sizeof nm, "encode G2  block-major  %d waves/SIMD", wps);
+      run(nm, per, pattern<2, false>, (nb + 1) / 2, 0, false);
 #define RUNS(W_, I_)                                                                              \
       snprintf(nm, sizeof nm, "encode split W%d %s %d waves/SIMD", W_, I_ ? "rows-ilv  " : "rows-chunk", wps); \
       runw(nm, per * W_ - sizeof(u32x4) * W_ * 128, split<W_, I_>, W_);
