@@ -48,10 +48,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
-                                           "small_lds", "block_svc", "ws_lds"};
+                                           "small_lds", "block_svc", "ws_lds", "dec_waves"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -92,6 +92,9 @@ static void knobs_from_env() {
   // recover data pass: a group's workspace records copied into LDS in one round trip (1) or read
   // where they lie during the setup (0)
   g_knob[K_WS_LDS] = num(getenv("FECGPU_WS_LDS"), 1) != 0;
+  // recover data pass (register-prefetch bodies): 0 = the occupancy its registers allow, n = at most
+  // n waves per SIMD
+  g_knob[K_DEC_WAVES] = num(getenv("FECGPU_DEC_WAVES"), 0);
 }
 
 static inline int knob(KnobId id) {
@@ -168,6 +171,13 @@ __device__ uint64_t g_fec_stamps[16];
 #endif
 
 static uint32_t grid_for(uint64_t units);
+// The data-pass kernels run one group per workgroup (no grid-stride loop); a batch of more groups
+// than one grid holds (grid_for's cap) is launched in slices, q0 = the slice's first group.
+#define FEC_LAUNCH_GROUPS(KERNEL, GROUPS, BLOCK, LDS, STREAM, ...)                                  \
+  for (uint64_t q0_ = 0; q0_ < (GROUPS); q0_ += grid_for(GROUPS)) {                               \
+    const uint64_t n_ = (GROUPS) - q0_ < grid_for(GROUPS) ? (GROUPS) - q0_ : grid_for(GROUPS);   \
+    hipLaunchKernelGGL(KERNEL, dim3((uint32_t)n_), dim3(BLOCK), LDS, STREAM, __VA_ARGS__, q0_);   \
+  }
 
 // =============================================================================================
 // RLC decode: plan (coefficients only), recover (data), finalize (zero propagation)
@@ -1345,7 +1355,8 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? FEC_V1_ENC8_WAVES : RT == 4 ? FEC_V
 void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
-                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv) {
+                                                       int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
+                                                       uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
@@ -1357,7 +1368,9 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
   // at one time stream neighbouring blocks (dense HBM pages); otherwise blocks qG .. qG + G - 1.
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
-  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+  {  // one group per workgroup: no grid-stride loop invariants live across the asm body
+    const uint64_t q = q0 + blockIdx.x;
+    if (q >= NG) return;
     const uint64_t b0 = ilv ? q : q * G;
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
@@ -1388,7 +1401,7 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
     }
     __syncthreads();
     FEC_STAMP_AT(6);
-    if (rt <= 0) continue;
+    if (rt <= 0) return;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
@@ -1422,10 +1435,12 @@ struct RecoverLds {
   uint8_t *rec;      // [G] x kDecRec records read by the asm body
   uint8_t *gid;      // [64] compacted slot -> block in group
   uint8_t *ecnt;     // [64] unknowns of the block in this pass
+  uint8_t *hst, *he; // [64] status and unknown count of block g (read back after the data pass, so they
+                     // need no registers across it)
   uint8_t *unk;      // [G][16] unknown -> source index (fused finalize)
   uint32_t *depm;    // [G][16] unknowns row u still references after elimination (fused finalize)
   __host__ __device__ static size_t bytes(int G, int k) {
-    return (size_t)G * ((size_t)k * (CSB + 8) + kDecRec + 16 + 64) + 128;
+    return (size_t)G * ((size_t)k * (CSB + 8) + kDecRec + 16 + 64) + 256;
   }
   __device__ RecoverLds(uint8_t *l, int G, int k) {
     coef = l;
@@ -1435,6 +1450,8 @@ struct RecoverLds {
     unk = reinterpret_cast<uint8_t *>(depm + G * 16);
     gid = unk + G * 16;
     ecnt = gid + 64;
+    hst = ecnt + 64;
+    he = hst + 64;
   }
 };
 
@@ -1466,6 +1483,7 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
     // coefficient rows / slots -> unknowns and dependencies)
     if (wsl) {
       const int per = (int)(WL.stride >> 4), np = ng * per;
+#pragma unroll 1
       for (int x = lane; x < np; x += 64) {
         const int g = x / per, o = x - g * per;
         reinterpret_cast<uint4 *>(wsl)[x] =
@@ -1493,6 +1511,10 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
     const uint64_t am = __ballot(act);
     const int nact = __popcll(am);
     __syncthreads();
+    if (status && lane < ng) {
+      S.hst[lane] = (uint8_t)st;
+      S.he[lane] = (uint8_t)e;
+    }
     if (act) {
       const int t = __popcll(am & ((1ull << lane) - 1));
       S.gid[t] = (uint8_t)lane;
@@ -1571,14 +1593,18 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
     }
     __syncthreads();
     if (status) {
+      const int st2 = lane < ng ? S.hst[lane] : FECGPU_BLOCK_NOTHING;
+      const int e2 = lane < ng ? S.he[lane] : 0;
+      const bool act2 = st2 == FECGPU_BLOCK_RECOVERED && e2 > r0;
+      const uint64_t am2 = __ballot(act2);
       if (lane < ng) {
         const uint64_t b = b0 + lane * bstep;
         uint64_t m0 = 0, m1 = 0;
-        if (act) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
-          const int t = __popcll(am & ((1ull << lane) - 1));
+        if (act2) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
+          const int t = __popcll(am2 & ((1ull << lane) - 1));
           const uint8_t *nzf = S.rec + (size_t)t * kDecRec + kDecRecNz;
           uint32_t det = 0;
-          for (int u = e - 1; u >= 0; u--) {
+          for (int u = e2 - 1; u >= 0; u--) {
             if (nzf[u] && (S.depm[t * 16 + u] & ~det) == 0) {
               det |= 1u << u;
               const int j = S.unk[t * 16 + u];
@@ -1586,7 +1612,7 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
             }
           }
         }
-        status[b] = (uint8_t)st;
+        status[b] = (uint8_t)st2;
         recovered[2 * b] = m0;
         recovered[2 * b + 1] = m1;
       }
@@ -1609,11 +1635,15 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint8_t *ws, int r0, int G,
                                                        uint8_t *status, uint64_t *recovered, int ilv,
-                                                       uint8_t *dst, uint32_t wsl_off, int dst_rows) {
+                                                       uint8_t *dst, uint32_t wsl_off, int dst_rows, uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
   const uint64_t bstep = ilv ? NG : 1;
-  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x)
+  // one group per workgroup (the launcher splits batches of more groups than one grid holds): no
+  // grid-stride loop whose invariants the compiler would keep live across the asm body (they cost
+  // the wave-per-SIMD budget, 168 VGPRs for 3 waves)
+  const uint64_t q = q0 + blockIdx.x;
+  if (q < NG)
     recover_bs_group<RT, VEC>(q, NG, bstep, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, r0, G, status,
                               recovered, ilv, dst, lds, wsl_off ? lds + wsl_off : nullptr, dst_rows);
 }
@@ -2055,8 +2085,8 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
   const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, nb) : 1;
   const size_t lds = (size_t)W * G * k * FEC_BS_COEF_ROW_BYTES(RT);
   const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_encode_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64 * W), lds, s, src, rep, nb, k,
-                     r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups());
+  FEC_LAUNCH_GROUPS((k_rlc_encode_bs<RT, VEC>), groups, 64 * W, lds, s, src, rep, nb, k, r, L, c.nchunks,
+                    c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups())
 }
 
 template <int RT, int VEC>
@@ -2073,9 +2103,13 @@ static void launch_recover_bs(uint8_t *src, const uint8_t *rep, uint64_t nb, int
     lds = wsl_off + wsb;
   }
   const uint64_t groups = (nb + G - 1) / G;
-  hipLaunchKernelGGL((k_rlc_recover_bs<RT, VEC>), dim3(grid_for(groups)), dim3(64), lds, s, src, rep, nb, k, r,
-                     L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, wsl_off,
-                     dst_rows);
+  // knob dec_waves = n: at most n waves per SIMD (the workgroup's LDS sized so 4 n fit a CU's 160 KiB)
+  if (const int dw = knob(K_DEC_WAVES)) {
+    const size_t cap = (size_t)160 * 1024 / (4 * (size_t)dw) & ~(size_t)15;
+    if (lds < cap) lds = cap;
+  }
+  FEC_LAUNCH_GROUPS((k_rlc_recover_bs<RT, VEC>), groups, 64, lds, s, src, rep, nb, k, r, L, c.nchunks,
+                    c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, wsl_off, dst_rows)
 }
 
 template <int RT, int VEC>
@@ -2279,7 +2313,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
                                                         int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
-                                                        uint32_t slotb) {
+                                                        uint32_t slotb, uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2293,7 +2327,9 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
   const int rt = r - r0 < RT ? r - r0 : RT;  // <= 0: this wave has no repairs (waits at barriers)
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
-  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+  {  // one group per workgroup: no grid-stride loop invariants live across the asm body
+    const uint64_t q = q0 + blockIdx.x;
+    if (q >= NG) return;
     const uint64_t b0 = ilv ? q : q * G;
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
@@ -2319,7 +2355,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
       }
     }
     __syncthreads();
-    if (rt <= 0) continue;
+    if (rt <= 0) return;
     if constexpr (CW) {  // items (block g, chunk ch), one block's k rows per body call
       for (int it = wave; it < ng * nchunks; it += kCwWaves) {
         const int g = it / nchunks, ch = it - g * nchunks;
@@ -2358,7 +2394,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint8_t *ws, int r0, int G,
                                                         uint8_t *status, uint64_t *recovered, int ilv,
-                                                        uint8_t *dst, uint32_t slotb, int dst_rows) {
+                                                        uint8_t *dst, uint32_t slotb, int dst_rows, uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const WsLayout WL = ws_layout((uint32_t)k, (uint32_t)r);
   const int lane = threadIdx.x & 63;
@@ -2369,7 +2405,9 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
                         (uint32_t)wave * Bs2Depth16::dec * slotb;
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
-  for (uint64_t q = blockIdx.x; q < NG; q += gridDim.x) {
+  {  // one group per workgroup: no grid-stride loop invariants live across the asm body
+    const uint64_t q = q0 + blockIdx.x;
+    if (q >= NG) return;
     const uint64_t b0 = ilv ? q : q * G;
     const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
@@ -2453,7 +2491,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       }
     }
     __syncthreads();
-    if (wave != 0) continue;
+    if (wave != 0) return;
     if (status) {
       if (lane < ng) {
         const uint64_t b = b0 + lane * bstep;
@@ -2523,18 +2561,17 @@ static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int
   if (int G = (W == 1 && c.nchunks > 1) ? cw_group(RT, k, CSB, 0, ring_bytes, nb) : 0) {
     if (sbs != (uint64_t)k * L) G = 1;  // overlapping blocks (windows): one per group
     const size_t lds = pad16((uint32_t)(G * k * CSB)) + kCwWaves * ring_bytes;
-    hipLaunchKernelGGL((k_rlc_encode_bs2<RT, true>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * kCwWaves), lds, s,
-                       src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step,
-                       interleave_groups(), slotb);
+    FEC_LAUNCH_GROUPS((k_rlc_encode_bs2<RT, true>), (nb + G - 1) / G, 64 * kCwWaves, lds, s, src, rep, nb, k, r, L,
+                      c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups(), slotb)
     return;
   }
   const int G = sbs == (uint64_t)k * L
                     ? bs2_group(RT, k, CSB, 0, true, c.nchunks, ring_bytes, bs2_waves_per_cu(RT), nb)
                     : 1;
   const size_t coef = pad16((uint32_t)(G * k * CSB));
-  hipLaunchKernelGGL((k_rlc_encode_bs2<RT, false>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * W),
-                     (size_t)W * (coef + ring_bytes), s, src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn,
-                     r0, G, sbs, fbn_step, interleave_groups(), slotb);
+  FEC_LAUNCH_GROUPS((k_rlc_encode_bs2<RT, false>), (nb + G - 1) / G, 64 * W, (size_t)W * (coef + ring_bytes), s,
+                    src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step,
+                    interleave_groups(), slotb)
 }
 
 template <int RT>
@@ -2546,16 +2583,14 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
   const int per_j = FEC_BS_COEF_ROW_BYTES(RT) + 8, per_block = kDecRec + 80;
   if (const int G = c.nchunks > 1 ? cw_group(RT, k, per_j, per_block, ring_bytes, nb) : 0) {
     const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + kCwWaves * ring_bytes;
-    hipLaunchKernelGGL((k_rlc_recover_bs2<RT, true>), dim3(grid_for((nb + G - 1) / G)), dim3(64 * kCwWaves), lds, s,
-                       src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered,
-                       interleave_groups(), dst, slotb, dst_rows);
+    FEC_LAUNCH_GROUPS((k_rlc_recover_bs2<RT, true>), (nb + G - 1) / G, 64 * kCwWaves, lds, s, src, rep, nb, k, r, L,
+                      c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, slotb, dst_rows)
     return;
   }
   const int G = bs2_group(RT, k, per_j, per_block, false, c.nchunks, ring_bytes, bs2_waves_per_cu(RT), nb);
   const size_t stage = pad16((uint32_t)RecoverLds<RT>::bytes(G, k));
-  hipLaunchKernelGGL((k_rlc_recover_bs2<RT, false>), dim3(grid_for((nb + G - 1) / G)), dim3(64), stage + ring_bytes, s,
-                     src, rep, nb, k, r, L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(),
-                     dst, slotb, dst_rows);
+  FEC_LAUNCH_GROUPS((k_rlc_recover_bs2<RT, false>), (nb + G - 1) / G, 64, stage + ring_bytes, s, src, rep, nb, k, r,
+                    L, c.nchunks, c.chunk_bytes, ws, r0, G, status, recovered, interleave_groups(), dst, slotb, dst_rows)
 }
 
 // The ring path applies to 16-repair / 16-unknown tiles of 16-B pieces (symbol_size >= 16) and blocks
@@ -2898,6 +2933,7 @@ static bool knob_value_ok(int id, int v) {
     case K_RING: return v == 0 || v == 2;
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;
+    case K_DEC_WAVES: return v >= 0 && v <= 8;
     default: return v == 0 || v == 1;  // on / off knobs
   }
 }

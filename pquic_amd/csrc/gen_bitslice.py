@@ -1106,17 +1106,21 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     """Register prefetch depth P (source rows in flight per wave).  Prefer 3 waves/SIMD
     (<= 168 VGPRs) when that still leaves P >= PMIN3 (4 for encode, 2 for decode); otherwise
     take everything up to 256 VGPRs at 2 waves/SIMD.  Bounded by the 6-bit vmcnt: NP * (P - 1) <= 63.
-    The decode wrapper keeps ~14 more VGPRs live across the asm than the asm's own window
-    (measured with -Rpass-analysis=kernel-resource-usage), so its budgets carry a margin --
-    without it the recover kernels tip over a VGPR granule and lose a wave per SIMD."""
+    The recover kernels run one group per workgroup (no grid-stride loop), so the compiler keeps
+    nothing live across the asm beyond v0-v31 and the decode budgets need no margin (round 2 carried
+    14 VGPRs of loop invariants; -Rpass-analysis=kernel-resource-usage, profiles/r03_kernel_resources.txt)."""
     NP = 32 // VEC
-    margin = int(os.environ.get("FEC_GEN_DEC_MARGIN", "14")) if mode == "dec" else 0
+    margin = int(os.environ.get("FEC_GEN_DEC_MARGIN", "0")) if mode == "dec" else 0
     budget3 = int(os.environ.get("FEC_GEN_VGPR3", "168")) - margin
     # 2-wave budget for decode: RT=8 needs a larger margin than RT=16 (measured: a 242 budget at
     # RT=8 compiled to 256 VGPRs + 4 AGPRs = 1 wave/SIMD, k32 e8 apply 13 ms -> 7.6 ms at 222)
     budget2 = 256 - margin - (8 if mode == "dec" and RT <= 8 else 0)
     fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - (0 if EARLY_PF else 1)) <= 63
-    forced = os.environ.get(f"FEC_GEN_LIMIT_{mode.upper()}_RT{RT}") or os.environ.get(f"FEC_GEN_LIMIT_RT{RT}")
+    # 4-unknown decode tiles take the 2-wave budget: 19 rows in flight at 2 waves/SIMD streamed the k16 e4
+    # apply 2.3 % faster than 8 at 3 waves (profiles/r03_ab_dec_occupancy.log); 8-unknown tiles keep 3
+    # waves (2 waves: +13-20 %)
+    forced = os.environ.get(f"FEC_GEN_LIMIT_{mode.upper()}_RT{RT}") or os.environ.get(f"FEC_GEN_LIMIT_RT{RT}") or \
+        ("256" if mode == "dec" and RT == 4 else None)
     if forced:  # A/B: VGPR limit for this tile size
         return max([P for P in range(2, 33) if fits(P, int(forced) - margin)] or [2])
     p3 = max([P for P in range(2, 33) if fits(P, budget3)] or [0])

@@ -55,7 +55,10 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_rlc_decode_seeded.argtypes = [v, v, u64, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply.argtypes = [v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_rlc_decode_apply_to.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
-    L.fecgpu_rlc_decode_apply_packed.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
+    if private and not hasattr(L, "fecgpu_rlc_decode_apply_packed"):  # an older build (A/B baselines)
+        pass
+    else:
+        L.fecgpu_rlc_decode_apply_packed.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, sz, v]
     L.fecgpu_synth_fill.argtypes = [v, u64, u64, u64, v]
     L.fecgpu_get_stats.argtypes = [C.POINTER(FecGpuStats)]
     L.fecgpu_set_knob.argtypes = [C.c_char_p, C.c_int]
