@@ -271,7 +271,8 @@ int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset
  * "small_lds" (batches of <= 64 blocks with their rows staged in LDS: 1 = default, 0 the bitsliced
  * kernels), "block_svc" (the resident single-block service: 1 = default, 0 refused), "ws_lds" (the
  * recover data pass copies a group's plan records into LDS in one round trip: 1 = default, 0 reads
- * them in place).  Returns FECGPU_OK, or FECGPU_ERR_INVALID
+ * them in place), "dec_waves" (0 = default, n = at most n waves per SIMD for the register-prefetch
+ * recover tiles).  Returns FECGPU_OK, or FECGPU_ERR_INVALID
  * for an unknown name or a value outside its range. */
 int fecgpu_set_knob(const char *name, int value);
 int fecgpu_get_knob(const char *name, int *value);
