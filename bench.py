@@ -436,6 +436,7 @@ def batching_legs(dev_index, args):
                            C.c_double, C.c_int, C.POINTER(C.c_double)]
     lib.bl_run_window.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint,
                                   C.c_uint, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    lib.bl_run_senders.argtypes = [C.c_int] + lib.bl_run.argtypes[:9] + [C.c_int, C.POINTER(C.c_double)]
     legs = {}
     # host-side rates on a shared CPU slice vary from run to run: the saturated legs report the run
     # with the median rate of three, and every run's rate
@@ -457,9 +458,31 @@ def batching_legs(dev_index, args):
             "k": args.k, "r": args.r, "L": args.symbol, "blocks": nblocks, "connections": 64,
             "batch_blocks": batch, "max_delay_us": delay, "offered_GiB_s": offered or None,
             "rows": "gathered in place (registered arena)" if reg else "staged by copies",
+            "source_pool_blocks": 32768,
             "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
             "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1),
             "runs_payload_GiB_s": [round(o[0], 2) for o in res]}
+    # two sender threads, each with its own batcher, arena and 64 connections: a server running one
+    # single-threaded PQUIC process per core on one GPU (one sender alone is bound by its own thread)
+    res = []
+    for _ in range(3):
+        out = (C.c_double * 8)()
+        if lib.bl_run_senders(2, dev_index, args.k, args.r, args.symbol, 64, 200000, 4096, 2000, 2, 1, out):
+            break
+        res.append(list(out))
+    if len(res) == 3:
+        out = sorted(res, key=lambda o: o[0])[1]
+        legs["batch_saturated_2senders"] = {
+            "k": args.k, "r": args.r, "L": args.symbol, "senders": 2, "blocks_per_sender": 200000,
+            "connections_per_sender": 64, "batch_blocks": 4096, "max_delay_us": 2000, "source_pool_blocks": 32768,
+            "rows": "gathered in place (registered arenas)",
+            "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
+            "latency_us_max": out[3], "batches": int(out[4]),
+            "runs_payload_GiB_s": [round(o[0], 2) for o in res],
+            "note": "both senders start each pass at a barrier; rate = all blocks over first start to last drain; "
+                    "latency = the worse sender's percentile"}
+    else:
+        legs["batch_saturated_2senders"] = {"error": -1}
     # the sliding-window sender (window_framework_sender.h:209-260) at the redundancy controllers'
     # shapes: a window of the <= 30 symbols in flight every K new ones, N - K repairs
     for k, r, step in ((30, 1, 5), (30, 5, 25)):

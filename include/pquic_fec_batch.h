@@ -40,6 +40,10 @@ typedef struct {
     uint32_t max_delay_us;   /* ... or when its oldest block has waited this long (poll) */
     uint32_t max_symbol;     /* largest symbol length accepted (<= 32767, fec.h:95,109) */
     int nstreams;            /* HIP streams the engine pipelines a batch over (>= 1) */
+    uint32_t poll_blocks;    /* poll completes at most this many blocks per call (0: every finished one);
+                              * a sender's event loop that polls between submissions then frees and
+                              * reallocates symbols in small interleaved runs, so its allocator's free
+                              * list stays in cache */
 } pquic_fec_batch_cfg_t;
 
 /* Called once per submitted block, on the caller's thread (see above). */
@@ -52,6 +56,8 @@ typedef struct {
     uint64_t immediate;             /* blocks completed at submit (preconditions failed) */
     uint64_t engine_errors;
     uint64_t windows, window_rows;  /* window blocks coded from shared streams; stream rows staged for them */
+    uint64_t engine_us, stage_us;   /* thread time in engine calls / in stager work items (all threads) */
+    uint64_t complete_us;           /* caller-thread time in completions (poll / drain) */
 } pquic_fec_batch_stats_t;
 
 /* NULL on failure (bad configuration, no device, out of pinned memory). */
@@ -89,7 +95,8 @@ int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_f
                             uint64_t now_us, pquic_fec_block_done_fn done, void *user);
 
 /* Flushes every queue that is full or past its deadline at `now_us`, then runs `done` for
- * every block whose batch has finished.  Non-blocking.  Returns the number of completions. */
+ * the blocks whose batch has finished, in submission order per batch: all of them, or at most
+ * cfg.poll_blocks.  Non-blocking.  Returns the number of completions. */
 int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us);
 /* Flushes everything and waits until every queued block has completed.  Returns the number
  * of completions. */

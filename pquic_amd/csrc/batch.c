@@ -38,6 +38,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "fec_core.h"
 #include "fecgpu.h"
@@ -106,6 +107,9 @@ struct pquic_fec_batcher {
     pthread_cond_t cv_todo, cv_staged, cv_done;
     job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *post_head, *post_tail, *done_head, *done_tail;
     int inflight, stop, stagers_done;
+    int last_slot;                 /* open[] slot of the last submission (caller thread) */
+    job_t *completing;             /* finished job whose completions a bounded poll left part-done */
+    uint32_t completing_i;         /* its next entry */
     pquic_fec_batch_stats_t stats;
     heap_t heaps[MAX_HEAPS];
     int nheaps;
@@ -382,6 +386,12 @@ static void copy_out_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     }
 }
 
+static uint64_t mono_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
 static void push(job_t **head, job_t **tail, job_t *j) {
     j->next = NULL;
     if (*tail) (*tail)->next = j; else *head = j;
@@ -409,12 +419,15 @@ static void *stager_main(void *arg) {
             if (!*head) *tail = NULL;
         }
         pthread_mutex_unlock(&b->mu);
+        const uint64_t t0 = mono_us();
         const uint32_t i0 = c * STAGE_CHUNK, i1 = i0 + STAGE_CHUNK < j->n ? i0 + STAGE_CHUNK : j->n;
         if (j->post) copy_out_blocks(j, i0, i1);
         else if (j->op == OP_WINDOW) stage_windows(j);
         else if (j->gather) gather_blocks(b, j, i0, i1);
         else stage_blocks(j, i0, i1);
+        const uint64_t dt = mono_us() - t0;
         pthread_mutex_lock(&b->mu);
+        b->stats.stage_us += dt;
         if (++j->chunks_done == nchunks) {
             if (j->post) {
                 push(&b->done_head, &b->done_tail, j);
@@ -486,8 +499,11 @@ static void *worker_main(void *arg) {
         b->staged_head = j->next;
         if (!b->staged_head) b->staged_tail = NULL;
         pthread_mutex_unlock(&b->mu);
+        const uint64_t t0 = mono_us();
         run_engine(b->ctx[ea->idx], j);
+        const uint64_t dt = mono_us() - t0;
         pthread_mutex_lock(&b->mu);
+        b->stats.engine_us += dt;
         if (GENERATES(j->op) && !j->rc && (!j->gather || j->ncopy)) {  /* repair rows to their symbols */
             j->post = 1;
             j->next_chunk = j->chunks_done = 0;
@@ -588,6 +604,11 @@ static void flush_job(pquic_fec_batcher_t *b, int slot, uint64_t *counter) {
 
 /* The open job for a key, opening one (and if every slot is taken, flushing the oldest). */
 static job_t *open_job(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r, int *slot_out) {
+    job_t *hit = b->open[b->last_slot];  /* consecutive blocks of one sender share a key */
+    if (hit && hit->op == op && hit->xor_scheme == xor_scheme && hit->k == k && hit->r == r) {
+        *slot_out = b->last_slot;
+        return hit;
+    }
     int free_slot = -1, oldest = -1;
     for (int s = 0; s < MAX_OPEN; s++) {
         job_t *j = b->open[s];
@@ -596,7 +617,7 @@ static job_t *open_job(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t 
             continue;
         }
         if (j->op == op && j->xor_scheme == xor_scheme && j->k == k && j->r == r) {
-            *slot_out = s;
+            *slot_out = b->last_slot = s;
             return j;
         }
         if (oldest < 0 || j->t_first < b->open[oldest]->t_first) oldest = s;
@@ -608,7 +629,7 @@ static job_t *open_job(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t 
     job_t *j = job_get(b, op, xor_scheme, k, r);
     if (!j) return NULL;
     b->open[free_slot] = j;
-    *slot_out = free_slot;
+    *slot_out = b->last_slot = free_slot;
     return j;
 }
 
@@ -678,19 +699,37 @@ int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_f
     return submit(b, cnx, fb, OP_RECOVER, xor_scheme ? 1 : 0, now_us, done, user);
 }
 
-/* Completes every finished job: the finish halves of the protocol operations, then done(). */
-static int collect(pquic_fec_batcher_t *b) {
-    pthread_mutex_lock(&b->mu);
-    job_t *j = b->done_head;
-    b->done_head = b->done_tail = NULL;
-    pthread_mutex_unlock(&b->mu);
+/* Completes finished jobs, at most `budget` blocks (0: all): the finish halves of the protocol
+ * operations, then done().  A job left part-done continues at the next call. */
+static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
+    job_t *j = b->completing;
+    if (!j || __atomic_load_n(&b->done_head, __ATOMIC_RELAXED)) {  /* and the finished jobs behind it */
+        pthread_mutex_lock(&b->mu);
+        job_t *more = b->done_head;
+        b->done_head = b->done_tail = NULL;
+        pthread_mutex_unlock(&b->mu);
+        if (!j) {
+            j = more;
+        } else if (more) {
+            job_t *t = j;
+            while (t->next) t = t->next;
+            t->next = more;
+        }
+    }
+    if (!j) return 0;
+    const uint64_t t0 = mono_us();
+    uint32_t i = b->completing_i;
     int n = 0;
     while (j) {
-        job_t *next = j->next;
         const uint32_t S = j->stride;
-        if (j->rc) b->stats.engine_errors++;
-        for (uint32_t i = 0; i < j->n; i++) {
+        if (i == 0) {  /* per-job accounting, once */
+            if (j->rc) b->stats.engine_errors++;
+            if (GENERATES(j->op)) FEC_STAT_ADD(generate_calls, j->n); else FEC_STAT_ADD(recover_calls, j->n);
+        }
+        const uint32_t end = budget && j->n - i > budget - (uint32_t)n ? i + (budget - (uint32_t)n) : j->n;
+        for (; i < end; i++) {
             entry_t *e = &j->ent[i];
+            if (i + 4 < j->n) __builtin_prefetch(j->ent[i + 4].fb, 1);  /* the blocks were last touched at submission */
             protoop_arg_t ret;
             pquic_repair_symbol_t **reps = GENERATES(j->op) ? j->reps + (size_t)i * j->r : NULL;
             if (j->rc) {
@@ -706,20 +745,29 @@ static int collect(pquic_fec_batcher_t *b) {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);
             }
-            if (GENERATES(j->op)) FEC_STAT_ADD(generate_calls, 1); else FEC_STAT_ADD(recover_calls, 1);
             e->done(e->user, e->fb, ret);
             n++;
         }
+        if (i < j->n) break;  /* budget spent inside this job */
         b->stats.completed += j->n;
         if (j->op == OP_WINDOW && !j->rc) {
             b->stats.windows += j->n;
             b->stats.window_rows += j->nrows;
         }
+        job_t *next = j->next;
         j->n = 0;
         j->next = b->free_jobs;
         b->free_jobs = j;
         j = next;
+        i = 0;
+        if (budget && (uint32_t)n >= budget) break;
     }
+    b->completing = j;
+    b->completing_i = i;
+    const uint64_t dt = mono_us() - t0;
+    pthread_mutex_lock(&b->mu);
+    b->stats.complete_us += dt;
+    pthread_mutex_unlock(&b->mu);
     return n;
 }
 
@@ -729,7 +777,7 @@ int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us) {
         job_t *j = b->open[s];
         if (j && j->n && now_us - j->t_first >= b->cfg.max_delay_us) flush_job(b, s, &b->stats.flushed_deadline);
     }
-    return collect(b);
+    return collect(b, b->cfg.poll_blocks);
 }
 
 int pquic_fec_batch_drain(pquic_fec_batcher_t *b) {
@@ -739,11 +787,15 @@ int pquic_fec_batch_drain(pquic_fec_batcher_t *b) {
     pthread_mutex_lock(&b->mu);
     while (b->inflight) pthread_cond_wait(&b->cv_done, &b->mu);
     pthread_mutex_unlock(&b->mu);
-    return collect(b);
+    return collect(b, 0);
 }
 
 void pquic_fec_batch_get_stats(const pquic_fec_batcher_t *b, pquic_fec_batch_stats_t *out) {
-    if (b && out) *out = b->stats;
+    if (!b || !out) return;
+    pthread_mutex_t *mu = (pthread_mutex_t *)&b->mu;  /* the worker threads add their times under it */
+    pthread_mutex_lock(mu);
+    *out = b->stats;
+    pthread_mutex_unlock(mu);
 }
 
 void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {

@@ -337,8 +337,9 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     t->calls++;
 }
 
-int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsigned max_symbol, int nstreams) {
-    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, max_symbol, nstreams};
+int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsigned max_symbol, int nstreams,
+                  unsigned poll_blocks) {
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, max_symbol, nstreams, poll_blocks};
     g_batcher = pquic_fec_batcher_create(&cfg);
     return g_batcher ? 0 : -1;
 }

@@ -24,7 +24,7 @@ def _p(a, t=C.c_uint8):
 
 
 class Batch:
-    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2, arena=False):
+    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2, arena=False, poll_blocks=0):
         L = C.CDLL(MINIHOST)
         L.mh_arena_enable.argtypes = [C.c_size_t]
         for f in ("mh_batch_generate", "mh_batch_recover", "mh_batch_status", "mh_live_allocations"):
@@ -47,7 +47,7 @@ class Batch:
         self.base = L.mh_live_allocations()
         if arena:  # symbols in a plugin-style arena the batcher gathers rows from (registered heap)
             assert L.mh_arena_enable(256 << 20) == 0
-        assert L.mh_batch_open(0, batch_blocks, max_delay_us, max_symbol, nstreams) == 0
+        assert L.mh_batch_open(0, batch_blocks, max_delay_us, max_symbol, nstreams, poll_blocks) == 0
         if arena:
             assert L.mh_batch_register_arena() == 0
         self.meta = {}
@@ -182,6 +182,29 @@ def _check_generate(bt, t, job):
     else:
         assert sha(np.stack(reps).tobytes()) == want[1]
     assert fps == fpids
+
+
+@pytest.mark.parametrize("poll_blocks", [1, 3, 7])
+def test_batch_bounded_poll(poll_blocks):
+    """cfg.poll_blocks: each poll completes at most that many blocks, a batch's completions spread over
+    several polls; every block completes once, with the reference's results."""
+    import time
+    bt = Batch(4, poll_blocks=poll_blocks)
+    jobs = [j for j in _encode_jobs() if j[4] is not None][:23]
+    tickets = [bt.generate(*j[:4], now=i) for i, j in enumerate(jobs)]
+    bt.L.mh_batch_poll(10 ** 9)  # flushes the part-filled queue (past its deadline)
+    order, t0 = [], time.time()
+    while len(order) < len(tickets) and time.time() - t0 < 30:
+        n = bt.L.mh_batch_poll(10 ** 9)
+        assert 0 <= n <= poll_blocks
+        order += [t for t in tickets if t not in order and bt.status(t)[1] == 1]
+        if not n:
+            time.sleep(0.001)
+    assert sorted(order) == sorted(tickets), "every block completes"
+    for t, j in zip(tickets, jobs):
+        _check_generate(bt, t, j)
+    assert bt.L.mh_batch_drain() == 0
+    bt.close()
 
 
 @pytest.mark.parametrize("batch_blocks", [1, 5, 64])

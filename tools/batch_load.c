@@ -15,6 +15,7 @@
 #include <sys/mman.h>
 #include <time.h>
 
+#include <pthread.h>
 #include <sched.h>
 
 #include "fecgpu.h"
@@ -35,9 +36,10 @@ static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t
  * (and an exhausted arena) fall back to the heap, tagged. */
 enum { SLOT = 2112 };  /* 2100 B rounded to 64, plus room for the tag */
 typedef union slot_u { union slot_u *next; uint8_t bytes[SLOT]; } slot_u;
-static slot_u *g_free_slots;
-static uint8_t *g_arena;
-static size_t g_arena_bytes, g_arena_used;
+/* per sender thread (bl_run_senders runs several, each a PQUIC process's single thread with its own heap) */
+static __thread slot_u *g_free_slots;
+static __thread uint8_t *g_arena;
+static __thread size_t g_arena_bytes, g_arena_used;
 static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
     (void)c;
     if (n > SLOT - 16) {
@@ -98,8 +100,32 @@ typedef struct {
     int busy;
 } slot_t;
 
-static uint64_t *g_lat;
-static long g_nlat;
+static __thread uint64_t *g_lat;
+static __thread long g_nlat;
+static unsigned g_poll_blocks;  /* pquic_fec_batch_cfg_t.poll_blocks of the next runs (0: all) */
+static int g_hugepages;         /* the next runs' arena on transparent huge pages */
+static int g_detail;            /* time every submission (one more clock read per block) */
+static long g_pool_blocks = 32768;  /* blocks of distinct source payload (bl_run) */
+
+void bl_set_options(unsigned poll_blocks, int hugepages, int detail, long pool_blocks) {
+    g_poll_blocks = poll_blocks;
+    g_hugepages = hugepages;
+    g_detail = detail;
+    if (pool_blocks > 0) g_pool_blocks = pool_blocks;
+}
+
+/* nanoseconds per now_us() call (the load generator stamps every block at submission and completion) */
+double bl_clock_cost(void) {
+    const uint64_t t0 = now_us();
+    uint64_t acc = 0;
+    for (int i = 0; i < 1000000; i++) acc += now_us();
+    return (double)(now_us() - t0) * 1e3 / 1e6 + (double)(acc & 0);
+}
+
+static pthread_barrier_t *g_sync;  /* bl_run_senders: the senders' pass barrier */
+static __thread uint64_t g_span[2];  /* the last measured pass: start, end (us) */
+static __thread double g_phases[6];  /* the last bl_run's measured pass: engine, stager, completion thread-us; wall us;
+                             * caller us waiting for a free slot; caller us inside pquic_fec_batch_generate */
 
 static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     slot_t *s = user;
@@ -121,47 +147,125 @@ static int cmp_u64(const void *a, const void *b) {
  *      [6] blocks completed, [7] mean blocks per batch.  register_heap: the symbols' arena (slot
  * allocator and payload) is registered with the batcher, which then gathers rows in place.
  * Returns 0 or -1. */
+static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks,
+                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, double out[8]);
+
 int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks, unsigned max_delay_us,
            int nstreams, double offered_gib_s, int register_heap, double out[8]) {
     pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device)) return -1;
+    return run_sender(device, k, r, L, nconn, nblocks, batch_blocks, max_delay_us, nstreams, offered_gib_s,
+                      register_heap, out);
+}
+
+/* `nsenders` bl_run senders at once, one thread each with its own batcher, arena and connections -- a
+ * server running one PQUIC process per core (each process single-threaded, plugin.c:1357-1360) on one
+ * GPU.  out: [0] the senders' payload GiB/s summed, [1] / [2] / [3] the largest p50 / p99 / max of any
+ * sender, [4] batches summed, [5] the longest wall s, [6] blocks summed, [7] mean blocks per batch. */
+struct sender_arg {
+    int device, k, r, L, nconn, nstreams, reg, rc;
+    long nblocks;
+    unsigned batch, delay;
+    double out[8];
+    uint64_t span[2];
+};
+static void *sender_main(void *p) {
+    struct sender_arg *a = p;
+    a->rc = run_sender(a->device, a->k, a->r, a->L, a->nconn, a->nblocks, a->batch, a->delay, a->nstreams, 0.0,
+                       a->reg, a->out);
+    a->span[0] = g_span[0];
+    a->span[1] = g_span[1];
+    return NULL;
+}
+int bl_run_senders(int nsenders, int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks,
+                   unsigned max_delay_us, int nstreams, int register_heap, double out[8]) {
+    if (nsenders < 1 || nsenders > 16) return -1;
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
+    if (pquic_fec_bind_host(&api, device)) return -1;
+    struct sender_arg a[16];
+    pthread_t th[16];
+    pthread_barrier_t bar;
+    if (pthread_barrier_init(&bar, NULL, (unsigned)nsenders)) return -1;
+    g_sync = nsenders > 1 ? &bar : NULL;
+    int started = 0, rc = 0;
+    for (; started < nsenders; started++) {
+        a[started] = (struct sender_arg){device, k, r, L, nconn, nstreams, register_heap, -1, nblocks, batch_blocks,
+                                         max_delay_us, {0}, {0, 0}};
+        if (pthread_create(&th[started], NULL, sender_main, &a[started])) break;
+    }
+    if (started < nsenders) abort();  /* the started senders would wait at the barrier for ever */
+    for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
+    g_sync = NULL;
+    pthread_barrier_destroy(&bar);
+    /* every sender's measured pass starts at the barrier: the job's rate is all their blocks over the
+     * span from the first start to the last drain */
+    memset(out, 0, 8 * sizeof *out);
+    uint64_t t_first = UINT64_MAX, t_last = 0;
+    for (int i = 0; i < nsenders; i++) {
+        if (a[i].rc) rc = -1;
+        t_first = a[i].span[0] < t_first ? a[i].span[0] : t_first;
+        t_last = a[i].span[1] > t_last ? a[i].span[1] : t_last;
+        for (int x = 1; x <= 3; x++) out[x] = a[i].out[x] > out[x] ? a[i].out[x] : out[x];
+        out[4] += a[i].out[4];
+        out[6] += a[i].out[6];
+    }
+    out[5] = (t_last - t_first) * 1e-6;
+    out[0] = out[5] > 0 ? (double)nsenders * nblocks * k * L / out[5] / 1073741824.0 : 0;
+    out[7] = out[4] > 0 ? out[6] / out[4] : 0;
+    return rc;
+}
+
+/* A sender that fails still meets the other senders at the pass barriers it has not reached. */
+static int sender_fail(int waits) {
+    for (; g_sync && waits < 2; waits++) pthread_barrier_wait(g_sync);
+    return -1;
+}
+
+static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks,
+                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, double out[8]) {
+    int waits = 0;  /* pass barriers this sender has passed (bl_run_senders) */
     /* the sender runs on the device's socket, like the batcher's threads, so the arena it first
      * touches is local to the device */
     cpu_set_t saved, near;
     const int pinned = !sched_getaffinity(0, sizeof saved, &saved) && !near_cpus(device, &saved, &near) &&
                        !sched_setaffinity(0, sizeof near, &near);
-    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams, g_poll_blocks};
     pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
-    if (!b) return -1;
+    if (!b) return sender_fail(waits);
     /* blocks in flight at most: every queued batch plus one being filled, per connection slot */
     const long nslots = (long)batch_blocks * 4 + nconn + 64;
     slot_t *slots = calloc(nslots, sizeof *slots);
-    const size_t pool_bytes = (size_t)64 * k * L;  /* 64 blocks of distinct payload, reused */
+    /* Distinct payload for g_pool_blocks blocks, reused in turn.  The default pool (32768 blocks, 629 MB at
+     * k16 L1200) is well past the device's caches, so every source row the kernels read in place crosses
+     * PCIe; a small pool (64 blocks) stays cached on the device and overstates the gathered read rate. */
+    const long pool_blocks = g_pool_blocks > 0 ? g_pool_blocks : 1;
+    const size_t pool_bytes = (size_t)pool_blocks * k * L;
     /* the arena: 2 slots per repair symbol of every block in flight (struct + data), plus the payload */
     g_free_slots = NULL;
     g_arena_bytes = ((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes;
     g_arena_bytes = (g_arena_bytes + 4095) & ~(size_t)4095;
     g_arena_used = 0;
     g_arena = mmap(NULL, g_arena_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (g_arena == MAP_FAILED) return -1;
+    if (g_arena == MAP_FAILED) return sender_fail(waits);
+    if (g_hugepages) madvise(g_arena, g_arena_bytes, MADV_HUGEPAGE);  /* before first touch */
     uint8_t *pool = g_arena;  /* the payload (source symbols) lives in the arena as well */
     g_arena_used = (pool_bytes + 63) & ~(size_t)63;
-    if (register_heap && pquic_fec_batch_register_heap(b, g_arena, g_arena_bytes)) return -1;
+    if (register_heap && pquic_fec_batch_register_heap(b, g_arena, g_arena_bytes)) return sender_fail(waits);
     pquic_source_symbol_t *ss = calloc((size_t)nslots * k, sizeof *ss);
     g_lat = malloc(sizeof *g_lat * (size_t)(nblocks + nblocks / 5 + 1));
     g_nlat = 0;
     picoquic_cnx_t *cnx = calloc(nconn, sizeof *cnx);
-    if (!slots || !pool || !ss || !g_lat || !cnx) return -1;
+    if (!slots || !pool || !ss || !g_lat || !cnx) return sender_fail(waits);
     uint64_t x = 0x5EEDF3C0;
-    for (size_t o = 0; o < pool_bytes; o++) {  /* xorshift payload */
+    for (size_t o = 0; o < pool_bytes; o += 8) {  /* xorshift payload */
         x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-        pool[o] = (uint8_t)x;
+        memcpy(pool + o, &x, pool_bytes - o < 8 ? pool_bytes - o : 8);
     }
     for (int c = 0; c < nconn; c++) cnx[c].id = c;
     const double bytes_per_block = (double)k * L;
     long next_slot = 0;
     /* pass 0 warms up (pinned queue buffers allocated, device buffers grown), pass 1 is measured */
-    uint64_t t0 = 0;
+    uint64_t t0 = 0, t_wait = 0, t_submit = 0;
     pquic_fec_batch_stats_t st0;
     memset(&st0, 0, sizeof st0);
     for (int pass = 0; pass < 2; pass++) {
@@ -171,14 +275,20 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
             pquic_fec_batch_get_stats(b, &st0);
             g_nlat = 0;
         }
+        if (g_sync) pthread_barrier_wait(g_sync), waits++;  /* bl_run_senders: every sender starts each pass together */
         t0 = now_us();
+        t_wait = t_submit = 0;
         for (long blk = 0; blk < nb; blk++) {
             if (offered_gib_s > 0) {  /* pace: block blk is due at t0 + blk * bytes / rate */
                 const uint64_t due = t0 + (uint64_t)(blk * bytes_per_block / (offered_gib_s * 1073741824.0) * 1e6);
                 while (now_us() < due) pquic_fec_batch_poll(b, now_us());
             }
             slot_t *s = &slots[next_slot];
-            while (s->busy) pquic_fec_batch_poll(b, now_us());  /* back-pressure: slot still in flight */
+            if (s->busy) {
+                const uint64_t w0 = now_us();
+                while (s->busy) pquic_fec_batch_poll(b, now_us());  /* back-pressure: slot still in flight */
+                t_wait += now_us() - w0;
+            }
             const long si = next_slot;
             next_slot = (next_slot + 1) % nslots;
             memset(&s->fb, 0, sizeof s->fb);
@@ -187,7 +297,7 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
             for (int j = 0; j < k; j++) {
                 pquic_source_symbol_t *sym = &ss[si * k + j];
                 sym->fpid.raw = (fbn << 8) | (uint32_t)j;
-                sym->data = pool + ((size_t)(blk % 64) * k + j) * L;
+                sym->data = pool + ((size_t)(blk % pool_blocks) * k + j) * L;
                 sym->data_length = (uint16_t)L;
                 s->fb.source_symbols[j] = sym;
             }
@@ -195,12 +305,16 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
             s->fb.total_repair_symbols = (uint8_t)r;
             s->busy = 1;
             s->t_submit = now_us();
-            if (pquic_fec_batch_generate(b, &cnx[blk % nconn], &s->fb, 0, s->t_submit, on_done, s)) return -1;
+            if (pquic_fec_batch_generate(b, &cnx[blk % nconn], &s->fb, 0, s->t_submit, on_done, s)) return sender_fail(waits);
+            if (g_detail) t_submit += now_us() - s->t_submit;
             if ((blk & 15) == 0) pquic_fec_batch_poll(b, now_us());
         }
     }
     pquic_fec_batch_drain(b);
-    const double wall = (now_us() - t0) * 1e-6;
+    const uint64_t t_end = now_us();
+    const double wall = (t_end - t0) * 1e-6;
+    g_span[0] = t0;
+    g_span[1] = t_end;
     pquic_fec_batch_stats_t st;
     pquic_fec_batch_get_stats(b, &st);
     pquic_fec_batcher_destroy(b);  /* unregisters the arena */
@@ -213,6 +327,12 @@ int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned ba
     out[5] = wall;
     out[6] = (double)(st.completed - st0.completed);
     out[7] = out[4] > 0 ? out[6] / out[4] : 0;
+    g_phases[0] = (double)(st.engine_us - st0.engine_us);
+    g_phases[1] = (double)(st.stage_us - st0.stage_us);
+    g_phases[2] = (double)(st.complete_us - st0.complete_us);
+    g_phases[3] = wall * 1e6;
+    g_phases[4] = (double)t_wait;
+    g_phases[5] = (double)t_submit;
     free(slots); free(ss); free(g_lat); free(cnx);
     g_lat = NULL;
     if (pinned) sched_setaffinity(0, sizeof saved, &saved);
@@ -238,7 +358,7 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
     cpu_set_t saved, near;
     const int pinned = !sched_getaffinity(0, sizeof saved, &saved) && !near_cpus(device, &saved, &near) &&
                        !sched_setaffinity(0, sizeof near, &near);
-    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams};
+    pquic_fec_batch_cfg_t cfg = {device, batch_blocks, max_delay_us, (uint32_t)L, nstreams, g_poll_blocks};
     pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
     if (!b) return -1;
     const long nslots = (long)batch_blocks * 4 + nconn + 64;
@@ -396,4 +516,66 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
     bl_free(NULL, (void *)(uintptr_t)scheme);
     free(pool); free(ss); free(lat);
     return 0;
+}
+
+/* Where the last bl_run's measured pass spent its time: out[0] engine-thread us (all engines, inside
+ * the engine calls), [1] stager-thread us, [2] caller-thread us in completions, [3] wall us, [4] caller
+ * us waiting for a free block slot (completions inside it included), [5] caller us in submissions. */
+void bl_last_phases(double out[6]) {
+    for (int i = 0; i < 6; i++) out[i] = g_phases[i];
+}
+
+/* The gathered generate path without the batcher: `ncalls` calls of fecgpu_rlc_encode_rows_host on
+ * `nblocks` blocks whose rows lie in a registered arena the way bl_run lays them out (sources in
+ * distinct L-byte rows, repairs in 2112-B slots), row tables page-locked.  mode 0: as bl_run (the
+ * sources of 64 blocks reused); 1: every block's sources distinct.  For comparison, [2] is the same
+ * blocks staged in page-locked rows through fecgpu_rlc_encode_host (H2D, kernel, D2H).
+ * out: [0] gathered payload GiB/s, [1] gathered ms per call, [2] staged GiB/s, [3] staged ms per call. */
+int bl_rows_probe(int device, int k, int r, int L, long nblocks, int ncalls, int mode, double out[4]) {
+    if (k < 1 || r < 1 || L < 4 || nblocks < 1 || ncalls < 1) return -1;
+    const long src_blocks = mode ? nblocks : (nblocks < 64 ? nblocks : 64);
+    const size_t pool = (size_t)src_blocks * k * L, slots = (size_t)nblocks * r * SLOT;
+    const size_t bytes = ((pool + 4095) & ~(size_t)4095) + slots;
+    uint8_t *arena = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (arena == MAP_FAILED) return -1;
+    uint64_t x = 0x5EEDF3C0;
+    for (size_t o = 0; o < pool; o++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; arena[o] = (uint8_t)x; }
+    memset(arena + pool, 0, bytes - pool);
+    uint64_t dev = 0;
+    fecgpu_host_ctx_t *c = fecgpu_host_ctx_create(device, 2, (size_t)64 << 20);
+    uint64_t *srow = fecgpu_host_alloc((size_t)nblocks * k * 8), *rrow = fecgpu_host_alloc((size_t)nblocks * r * 8);
+    uint32_t *fbn = fecgpu_host_alloc((size_t)nblocks * 4);
+    uint8_t *ssrc = fecgpu_host_alloc((size_t)nblocks * k * L), *srep = fecgpu_host_alloc((size_t)nblocks * r * L);
+    int rc = -1;
+    if (!c || !srow || !rrow || !fbn || !ssrc || !srep) goto out;
+    if (fecgpu_host_register(arena, bytes) != FECGPU_OK) goto out;
+    if (fecgpu_host_device_address(arena, bytes, &dev) != FECGPU_OK) goto unreg;
+    const size_t rep0 = (pool + 4095) & ~(size_t)4095;
+    for (long b = 0; b < nblocks; b++) {
+        fbn[b] = (uint32_t)b & 0xffffffu;
+        for (int j = 0; j < k; j++) srow[(size_t)b * k + j] = dev + ((size_t)(b % src_blocks) * k + j) * L;
+        for (int i = 0; i < r; i++) rrow[(size_t)b * r + i] = dev + rep0 + ((size_t)b * r + i) * SLOT + 16;
+    }
+    for (long b = 0; b < nblocks; b++) memcpy(ssrc + (size_t)b * k * L, arena + (size_t)(b % src_blocks) * k * L, (size_t)k * L);
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass ? fecgpu_rlc_encode_host(c, ssrc, srep, nblocks, k, r, L, 0, fbn)
+                 : fecgpu_rlc_encode_rows_host(c, srow, rrow, nblocks, k, r, L, fbn))
+            goto unreg;  /* warm-up call */
+        const uint64_t t0 = now_us();
+        for (int n = 0; n < ncalls; n++)
+            if (pass ? fecgpu_rlc_encode_host(c, ssrc, srep, nblocks, k, r, L, 0, fbn)
+                     : fecgpu_rlc_encode_rows_host(c, srow, rrow, nblocks, k, r, L, fbn))
+                goto unreg;
+        const double s = (now_us() - t0) * 1e-6;
+        out[2 * pass] = (double)ncalls * nblocks * k * L / s / 1073741824.0;
+        out[2 * pass + 1] = s * 1e3 / ncalls;
+    }
+    rc = 0;
+unreg:
+    fecgpu_host_unregister(arena);
+out:
+    fecgpu_host_free(srow); fecgpu_host_free(rrow); fecgpu_host_free(fbn); fecgpu_host_free(ssrc); fecgpu_host_free(srep);
+    if (c) fecgpu_host_ctx_destroy(c);
+    munmap(arena, bytes);
+    return rc;
 }
