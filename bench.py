@@ -561,9 +561,20 @@ CONFIGS = {
 }
 
 
-def dry_run_rank(args, world, rank, cpu):
+def rank_device(local):
+    """The GPU a rank drives: its LOCAL_RANK (one process per GPU).  PQUIC_BENCH_SHARE_GPU=1 (rehearsal
+    on a box with fewer GPUs than ranks, never set by the driver) folds ranks onto the devices present;
+    counting devices does not initialise HIP on this image."""
+    if os.environ.get("PQUIC_BENCH_SHARE_GPU") == "1":
+        import torch
+        return local % max(torch.cuda.device_count(), 1)
+    return local
+
+
+def dry_run_rank(args, world, rank, local, cpu):
     """--dry-run: the rank plumbing without a GPU (gloo): barrier, an empty timed region,
-    max-over-ranks and per-rank gather, then rank 0's line with value 0."""
+    max-over-ranks and per-rank gather (step time and the device each rank would drive), then rank 0's
+    line with value 0."""
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -571,7 +582,7 @@ def dry_run_rank(args, world, rank, cpu):
         dist.barrier()
     t0 = time.perf_counter()
     elapsed = time.perf_counter() - t0
-    per_rank = None
+    per_rank, devices = None, [rank_device(local)]
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -579,10 +590,13 @@ def dry_run_rank(args, world, rank, cpu):
         allr = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(allr, torch.tensor([elapsed], dtype=torch.float64))
         per_rank = [float(x.item()) for x in allr]
+        alld = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(alld, torch.tensor([devices[0]], dtype=torch.int64))
+        devices = [int(x.item()) for x in alld]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "dry_run": True, "cpu_baseline": cpu,
-                          "per_rank_ms_per_step": per_rank}))
+                          "per_rank_ms_per_step": per_rank, "per_rank_device": devices}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -611,7 +625,7 @@ def main():
         else:  # before any HIP call: the reference's workers are fork()ed from this process
             cpu = measure_cpu_baseline(args, cfg)
     if args.dry_run:
-        dry_run_rank(args, world, rank, cpu)
+        dry_run_rank(args, world, rank, local, cpu)
         return
     import torch
     from pquic_amd import Engine
@@ -621,8 +635,7 @@ def main():
     # PQUIC_BENCH_SHARE_GPU=1 maps rank -> device local % count, PQUIC_BENCH_BACKEND=gloo
     # because RCCL refuses two ranks on one device
     backend = os.environ.get("PQUIC_BENCH_BACKEND", "nccl")
-    if os.environ.get("PQUIC_BENCH_SHARE_GPU") == "1":
-        local = local % max(torch.cuda.device_count(), 1)
+    local = rank_device(local)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)

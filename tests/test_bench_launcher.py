@@ -47,6 +47,18 @@ def test_spawn_path_two_ranks(config):
         assert ("decode" in cpu["sample"]) == (config == "k16")
 
 
+@pytest.mark.parametrize("share", [False, True])
+def test_spawn_path_rank_devices(share):
+    """Each child rank drives the GPU of its LOCAL_RANK (cuda:0..N-1); only the rehearsal knob folds
+    ranks onto the devices present (none here, so all onto 0)."""
+    p = _run(["--gpus", "3", "--dry-run", "--no-cpu", "--steps", "1", "--warmup", "0"],
+             {"PQUIC_BENCH_SHARE_GPU": "1"} if share else {"PQUIC_BENCH_SHARE_GPU": "0"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    assert d["n_gpus"] == 3
+    assert d["per_rank_device"] == ([0, 0, 0] if share else [0, 1, 2])
+
+
 def test_world_size_must_match_gpus():
     p = _run(["--gpus", "4", "--dry-run", "--no-cpu"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert p.returncode == 2
