@@ -177,7 +177,10 @@ def rlc_leg(torch, eng, dev, k, r, L, nb, e, reps=3, seed=0x5EEDF3C0):
 
 
 def xor_leg(torch, eng, dev, k, L, nb, reps=3):
-    """XOR scheme (configs[0]'s scheme at GPU scale): encode, then recover one erasure per block."""
+    """XOR scheme (configs[0]'s scheme at GPU scale): encode, then recover one erasure per block into a
+    row of its own (fecgpu_xor_decode_to; the reference's fec_recover allocates the recovered symbol
+    anew, xor_fec_scheme.c:54-58; in place into the received block measured 8 % slower,
+    profiles/r03_ab_xor_decode_to.log)."""
     src = torch.empty((nb, k, L), dtype=torch.uint8, device=dev)
     eng.synth_fill(src, src.numel(), 0x5EEDF3C0, 0)
     rep = torch.empty((nb, 1, L), dtype=torch.uint8, device=dev)
@@ -189,26 +192,29 @@ def xor_leg(torch, eng, dev, k, L, nb, reps=3):
     rp[:, 1] = 0
     st = torch.empty(nb, dtype=torch.uint8, device=dev)
     rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
+    dst = torch.empty((nb, L), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     eng.xor_encode(src, rep, k, L)
-    eng.xor_decode(work, rep, sp, rp, st, rec, k, L)
+    eng.xor_decode_to(work, rep, dst, sp, rp, st, rec, k, L)
     torch.cuda.synchronize()
-    assert bool((st == 0).all()) and bool((work == src).all()), "xor decode did not restore the sources"
+    assert bool((st == 0).all()) and bool((dst == src.view(nb * k, L)[idx]).all()), \
+        "xor decode did not restore the sources"
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     te = td = 0.0
     for _ in range(reps):
         ev[0].record(stream)
         eng.xor_encode(src, rep, k, L)
         ev[1].record(stream)
-        eng.xor_decode(work, rep, sp, rp, st, rec, k, L)
+        eng.xor_decode_to(work, rep, dst, sp, rp, st, rec, k, L)
         ev[2].record(stream)
         torch.cuda.synchronize()
         te += ev[0].elapsed_time(ev[1]) / reps
         td += ev[1].elapsed_time(ev[2]) / reps
-    del src, rep, work
+    del src, rep, work, dst
     torch.cuda.empty_cache()
     pay = nb * k * L / 2**30
-    return {"blocks": nb, "k": k, "L": L, "encode_ms": round(te, 3), "decode_ms": round(td, 3),
+    return {"blocks": nb, "k": k, "L": L, "decode_output": "recovered symbol into a row of its own per block",
+            "encode_ms": round(te, 3), "decode_ms": round(td, 3),
             "payload_GiB_s": round(pay / ((te + td) * 1e-3), 2),
             "encode_GB_s": round((k + 1) * L * nb / (te * 1e-3) / 1e9, 1),
             "decode_GB_s": round((k + 1) * L * nb / (td * 1e-3) / 1e9, 1)}

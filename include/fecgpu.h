@@ -161,6 +161,13 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k,
                       uint32_t symbol_size, const uint64_t *src_present,
                       const uint64_t *rep_present, uint8_t *status, uint64_t *recovered,
                       void *stream);
+/* fecgpu_xor_decode with the recovered symbol of block b written to dst + b * symbol_size (one row per
+ * block, as fec_recover allocates the recovered symbol anew, xor_fec_scheme.c:54-58) instead of into
+ * src; src is not written.  Rows of blocks with nothing recovered are left as they were. */
+int fecgpu_xor_decode_to(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                         uint32_t symbol_size, const uint64_t *src_present,
+                         const uint64_t *rep_present, uint8_t *status, uint64_t *recovered,
+                         void *stream);
 
 /* ---- Host-resident path --------------------------------------------------------------------
  * The same operations on HOST buffers (pageable or pinned): H2D copy, kernels, D2H copy,

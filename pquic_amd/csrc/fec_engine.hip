@@ -2675,7 +2675,7 @@ template <typename V, int KC, typename I>
 __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V *__restrict__ rep,
                                                     uint64_t nblocks, int k_rt, int Lv_rt,
                                                     const uint64_t *sp, const uint64_t *rp,
-                                                    uint8_t *status, uint64_t *recovered) {
+                                                    uint8_t *status, uint64_t *recovered, V *__restrict__ dst) {
   const int k = KC ? KC : k_rt;
   const I Lv = (I)Lv_rt, total = (I)(nblocks * (uint64_t)Lv_rt);
   for (I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x; t < total; t += (I)gridDim.x * (I)blockDim.x) {
@@ -2705,7 +2705,9 @@ __global__ __launch_bounds__(256) void k_xor_decode(V *__restrict__ src, const V
         for (int j = 0; j < k; j++)
           if (j != miss) a = vxor(a, __builtin_nontemporal_load(p + (uint64_t)j * Lv));
       }
-      __builtin_nontemporal_store(a, src + ((uint64_t)b * k + miss) * Lv + c);
+      // dst: one row per block (the recovered symbol in a row of its own, as fec_recover allocates it
+      // anew, :54-58); else in place, at the missing source's slot
+      __builtin_nontemporal_store(a, dst ? dst + (uint64_t)b * Lv + c : src + ((uint64_t)b * k + miss) * Lv + c);
     }
     if (c == 0) {
       status[b] = (uint8_t)st;
@@ -3407,15 +3409,16 @@ extern "C" __attribute__((visibility("hidden"))) int fecgpu_rlc_decode_to_intern
                      (hipStream_t)stream);
 }
 
-int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,
-                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
-                      uint64_t *recovered, void *stream) {
+static int xor_decode_impl(void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k, uint32_t symbol_size,
+                           const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                           uint64_t *recovered, void *stream) {
   int rc = check_common(src, rep, nblocks, k, 1, symbol_size);
   if (rc || nblocks == 0) return rc;
   if (!src_present || !rep_present || !status || !recovered)
     return set_err(FECGPU_ERR_INVALID, "%s", "NULL mask/status");
   hipStream_t s = (hipStream_t)stream;
-  const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0;
+  const bool v4 = (symbol_size % 16) == 0 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)rep % 16) == 0 &&
+                  ((uintptr_t)dst % 16) == 0;
   const int Lv = (int)(v4 ? symbol_size / 16 : symbol_size / 4);
   const uint32_t gmax = 1u << 20;
   for (uint64_t b0 = 0, n; b0 < nblocks; b0 += n) {
@@ -3426,16 +3429,31 @@ int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, 
     if (v4)
       xor_dispatch_k<u32x4, XorDec, uint32_t>(k, grid, s, (u32x4 *)src + so, (const u32x4 *)rep + ro, n, (int)k, Lv,
                                               src_present + 2 * b0, rep_present + 2 * b0, status + b0,
-                                              recovered + 2 * b0);
+                                              recovered + 2 * b0, dst ? (u32x4 *)dst + ro : (u32x4 *)nullptr);
     else
       xor_dispatch_k<uint32_t, XorDec, uint32_t>(k, grid, s, (uint32_t *)src + so, (const uint32_t *)rep + ro, n,
                                                  (int)k, Lv, src_present + 2 * b0, rep_present + 2 * b0, status + b0,
-                                                 recovered + 2 * b0);
+                                                 recovered + 2 * b0, dst ? (uint32_t *)dst + ro : (uint32_t *)nullptr);
   }
   HIPCHK(hipGetLastError());
   g_stats[2]++;
   g_stats[3] += nblocks;
   return FECGPU_OK;
+}
+
+int fecgpu_xor_decode(void *src, const void *rep, uint64_t nblocks, uint32_t k, uint32_t symbol_size,
+                      const uint64_t *src_present, const uint64_t *rep_present, uint8_t *status,
+                      uint64_t *recovered, void *stream) {
+  return xor_decode_impl(src, rep, nullptr, nblocks, k, symbol_size, src_present, rep_present, status, recovered,
+                         stream);
+}
+
+int fecgpu_xor_decode_to(const void *src, const void *rep, void *dst, uint64_t nblocks, uint32_t k,
+                         uint32_t symbol_size, const uint64_t *src_present, const uint64_t *rep_present,
+                         uint8_t *status, uint64_t *recovered, void *stream) {
+  if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL dst");
+  return xor_decode_impl(const_cast<void *>(src), rep, dst, nblocks, k, symbol_size, src_present, rep_present,
+                         status, recovered, stream);
 }
 
 int fecgpu_write_repair_frames(const void *rep, uint64_t nblocks, uint32_t r, uint32_t symbol_size,

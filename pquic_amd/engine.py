@@ -50,6 +50,8 @@ def load_library(path: str = LIB_PATH, private: bool = False):
     L.fecgpu_rlc_decode_workspace.restype = sz
     L.fecgpu_rlc_decode.argtypes = [v, v, u64, u32, u32, u32, u32, v, v, v, v, v, v, sz, v]
     L.fecgpu_xor_decode.argtypes = [v, v, u64, u32, u32, v, v, v, v, v]
+    if hasattr(L, "fecgpu_xor_decode_to") or not private:  # a private (A/B) load may be an older build
+        L.fecgpu_xor_decode_to.argtypes = [v, v, v, u64, u32, u32, v, v, v, v, v]
     L.fecgpu_rlc_decode_plan.argtypes = [u64, u32, u32, u32, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_plan_seeded.argtypes = [u64, u32, u32, v, v, v, v, sz, v]
     L.fecgpu_rlc_decode_seeded.argtypes = [v, v, u64, u32, u32, u32, v, v, v, v, v, v, sz, v]
@@ -279,6 +281,15 @@ class Engine:
         self._check(self.lib.fecgpu_xor_decode(_addr(src), _addr(rep), nb, k, L, _addr(src_present),
                                                _addr(rep_present), _addr(status), _addr(recovered),
                                                self._stream(stream)), "fecgpu_xor_decode")
+        return status, recovered
+
+    def xor_decode_to(self, src, rep, dst, src_present, rep_present, status, recovered, k: int, L: int,
+                      nblocks: int | None = None, stream=None):
+        """fecgpu_xor_decode_to: the recovered symbol of block b into dst[b] (one row per block); src is read only."""
+        nb = nblocks if nblocks is not None else src.numel() // (k * L)
+        self._check(self.lib.fecgpu_xor_decode_to(_addr(src), _addr(rep), _addr(dst), nb, k, L, _addr(src_present),
+                                                  _addr(rep_present), _addr(status), _addr(recovered),
+                                                  self._stream(stream)), "fecgpu_xor_decode_to")
         return status, recovered
 
     def synth_fill(self, dst, nbytes: int, seed: int, offset: int = 0, stream=None):

@@ -358,6 +358,43 @@ def _xor_vs_oracle(eng, oracle):
         assert np.array_equal(got[okb], ref[okb]) and np.array_equal(got[okb], src_h[okb])
 
 
+def test_xor_decode_to_vs_oracle(eng, oracle):
+    """fecgpu_xor_decode_to: status and recovered mask as the oracle's; block b's recovered symbol in
+    dst[b] (one row per block), dst rows of other blocks untouched, the received block not written."""
+    rng = np.random.default_rng(19)
+    for k, L, nb in [(4, 1200, 1000), (7, 36, 300), (16, 1200, 30), (3, 1216, 50), (5, 4, 40), (128, 16, 9)]:
+        src_h = synth_bytes(nb * k * L, 100 + k).reshape(nb, k, L)
+        rep = torch.empty((nb, 1, L), dtype=torch.uint8, device=DEV)
+        eng.xor_encode(to_dev(src_h), rep, k, L)
+        sp = np.zeros((nb, 2), np.uint64)
+        rp = np.zeros((nb, 2), np.uint64)
+        for b in range(nb):
+            miss = set(rng.choice(k, min(int(rng.integers(0, 3)), k), replace=False).tolist())
+            sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+            rp[b] = masks_from_lists(1, 1, [[0]] if rng.random() < 0.8 else [[]])[0]
+        work_h = src_h.copy()
+        for b in range(nb):
+            for j in range(k):
+                if not (int(sp[b][j >> 6]) >> (j & 63)) & 1:
+                    work_h[b, j] = 0xA5
+        work = to_dev(work_h)
+        dst = torch.full((nb, L), 0x5A, dtype=torch.uint8, device=DEV)
+        st = torch.empty(nb, dtype=torch.uint8, device=DEV)
+        rec = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+        eng.xor_decode_to(work, rep, dst, to_dev(sp.view(np.int64)), to_dev(rp.view(np.int64)), st, rec, k, L)
+        torch.cuda.synchronize()
+        st_h, rec_h, dst_h = st.cpu().numpy(), rec.cpu().numpy().view(np.uint64), dst.cpu().numpy()
+        st_ref, rec_ref = oracle.xor_decode_batch(work_h.copy(), rep.cpu().numpy(), sp, rp)
+        assert np.array_equal(st_h, st_ref) and np.array_equal(rec_h, rec_ref)
+        assert np.array_equal(work.cpu().numpy(), work_h), "the received block was written"
+        for b in range(nb):
+            got = bits(rec_h[b], k)
+            if st_h[b] == DEC_RECOVERED:
+                assert len(got) == 1 and np.array_equal(dst_h[b], src_h[b, got[0]])
+            else:
+                assert (dst_h[b] == 0x5A).all()
+
+
 # ------------------------------------------------------------------------------- full size
 def test_full_size_roundtrip_k16(eng, oracle):
     """BASELINE configs 2-3 at full size (2^20 blocks): encode -> erase 4 -> decode.

@@ -27,7 +27,9 @@ st = torch.empty(nb, dtype=torch.uint8, device=dev)
 rec = torch.empty((nb, 2), dtype=torch.int64, device=dev)
 work = src.clone()
 work[torch.arange(nb, device=dev), miss] = 0
-times = {(n, c): [] for n, _ in variants for c in ("enc", "dec")}
+dst = torch.empty((nb, L), dtype=torch.uint8, device=dev)
+CASES = ("enc", "dec", "dto") if all(hasattr(e.lib, "fecgpu_xor_decode_to") for e in engines.values()) else ("enc", "dec")
+times = {(n, c): [] for n, _ in variants for c in CASES}
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 for n, _ in variants:  # warm-up and check
     e = engines[n]
@@ -40,15 +42,18 @@ for n, _ in variants:  # warm-up and check
 for _ in range(cycles):
     for n, _ in variants:
         e = engines[n]
-        for c in ("enc", "dec"):
+        for c in CASES:
             ev[0].record()
             if c == "enc":
                 e.xor_encode(src, rep, k, L)
+            elif c == "dto":  # recovered symbols into rows of their own
+                e.xor_decode_to(work, rep, dst, sp, rp, st, rec, k, L)
             else:
                 e.xor_decode(work, rep, sp, rp, st, rec, k, L)
             ev[1].record()
             torch.cuda.synchronize()
             times[(n, c)].append(ev[0].elapsed_time(ev[1]))
-print(f"{'variant':12s} {'xor enc k4':>18s} {'xor dec k4':>18s}   (median ms / min; 2^22 blocks, L=1200)")
+print(f"{'variant':12s} " + " ".join(f"{'xor ' + c + ' k4':>18s}" for c in CASES) +
+      "   (median ms / min; 2^22 blocks, L=1200; dto = recovered rows to their own buffer)")
 for n, _ in variants:
-    print(f"{n:12s} " + " ".join(f"{statistics.median(times[(n, c)]):8.3f}/{min(times[(n, c)]):8.3f}" for c in ("enc", "dec")))
+    print(f"{n:12s} " + " ".join(f"{statistics.median(times[(n, c)]):8.3f}/{min(times[(n, c)]):8.3f}" for c in CASES))
