@@ -36,7 +36,8 @@ METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (one rank each); default: WORLD_SIZE under a launcher, else 1")
     p.add_argument("--config", choices=["k16", "k32r8", "k64r16"], default="k16",
                    help="workload: k16 = the metric's configs[1]+[2] (default); k32r8 = configs[3] "
                         "(2^24 blocks split over the GPUs); k64r16 = configs[4]")
@@ -56,7 +57,10 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / rendezvous check without a GPU: ranks time an empty step on gloo; "
                         "value is 0 and the line says dry_run (tests only)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.gpus is None:  # torchrun --nproc-per-node N bench.py: N ranks
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    return a
 
 
 def load_traffic(kernel_tag: str, blocks: int | None = None):
@@ -336,22 +340,55 @@ def _free_port():
     return port
 
 
+def visible_gpu_count(timeout=300):
+    """GPUs a child rank could open, counted in a throw-away child process: whatever the count costs
+    (HIP initialisation, /dev/kfd) happens there, and the launcher itself never opens the device."""
+    import subprocess
+    code = "import torch; print(torch.cuda.device_count())"
+    try:
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+        return int(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else 0
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        return 0
+
+
+def gpu_device_fds():
+    """Open file descriptors of this process on a GPU device node (/dev/kfd, /dev/dri/*)."""
+    out = []
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                t = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            if t == "/dev/kfd" or t.startswith("/dev/dri/"):
+                out.append(t)
+    except OSError:
+        pass
+    return out
+
+
 def launch_ranks(args):
     """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment): this process never touches
-    the GPU.  It measures cpu_baseline first (its workers are fork()ed), then starts N child processes
-    of this script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), hands
-    them the baseline through a file, waits for all of them and exits with the first failure's code.
-    Rank 0 prints the JSON line.  No exec: the children are started as new processes."""
+    the GPU.  It counts the GPUs in a throw-away child (visible_gpu_count), measures cpu_baseline (its
+    workers are fork()ed), then starts N child processes of this script, one per GPU (RANK = LOCAL_RANK
+    = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), hands them the baseline through a file, waits for all
+    of them and exits with the first failure's code.  Rank 0 prints the JSON line.  No exec: the
+    children are started as new processes, and the launcher checks it holds no GPU device open first."""
     import signal
     import subprocess
     import tempfile
     n = args.gpus
     if not args.dry_run and os.environ.get("PQUIC_BENCH_SHARE_GPU") != "1":
-        import torch  # device_count() does not initialise the GPU on this image
-        have = torch.cuda.device_count()
+        have = visible_gpu_count()
         if have < n:
             print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr)
             return 2
+    held = gpu_device_fds()
+    if held:  # a parent that initialised the GPU must not start the ranks (forks of a HIP process)
+        print(f"bench.py: launcher holds GPU device files open ({', '.join(held)}); refusing to start ranks",
+              file=sys.stderr)
+        return 3
     cfg = workload_cfg(args)
     env = dict(os.environ)
     tmp = None

@@ -76,7 +76,10 @@ int fecgpu_rlc_window_encode(const void *symbols, uint64_t nwindows, uint32_t st
  * nrows rows of symbol_size bytes -- each connection's symbols once, in order -- and window w protects
  * the k rows starting at row wrow[w] (a device array), with block number 0 like every window:
  *   rep[w][i] = sum_j coef(0, i)[j] * symbols[wrow[w] + j].
- * symbol_size % 16 == 0, 16-B aligned buffers, nrows * symbol_size < 2 GiB; knob window_sc != 0. */
+ * symbol_size % 16 == 0, 16-B aligned buffers, nrows * symbol_size < 2 GiB; knob window_sc != 0.
+ * Every window must lie in the stream: wrow[w] + k <= nrows for all w.  wrow[] is device memory, so
+ * this entry point cannot check it and the kernel reads the rows it names unchecked (the host form,
+ * fecgpu_rlc_window_encode_host, checks it before any launch). */
 int fecgpu_rlc_window_encode_table(const void *symbols, uint64_t nrows, const uint32_t *wrow, uint64_t nwindows,
                                    uint32_t k, uint32_t r, uint32_t symbol_size, void *rep, void *stream);
 
@@ -86,6 +89,19 @@ int fecgpu_rlc_window_encode_table(const void *symbols, uint64_t nrows, const ui
  * fbn[] must themselves be device-accessible.  Same result as fecgpu_rlc_encode on packed rows. */
 int fecgpu_rlc_encode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nblocks, uint32_t k,
                            uint32_t r, uint32_t symbol_size, uint32_t fbn_base, const uint32_t *fbn, void *stream);
+
+/* RLC decode with every row given by its address (the batching adapter's received symbols where they
+ * lie in registered plugin arenas): src_rows[b * k + j] is the device address of source row j of block b
+ * -- for a received source the row read, for a missing one the row its recovered bytes are written to --
+ * and rep_rows[b * r + i] that of repair row i (entries of repairs not present are not read).  Every
+ * equation is seeded by rep_seed[b * r + i] (the repair's own FPID, as fecgpu_rlc_decode_seeded); masks,
+ * status, recovered and workspace as fecgpu_rlc_decode.  Rows are symbol_size bytes, 4-byte aligned;
+ * the tables and arrays must be device-accessible.  Same bytes, status and masks as
+ * fecgpu_rlc_decode_seeded on packed rows. */
+int fecgpu_rlc_decode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed, const uint64_t *src_present,
+                           const uint64_t *rep_present, uint8_t *status, uint64_t *recovered, void *workspace,
+                           size_t workspace_bytes, void *stream);
 
 /* XOR encode (r == 1): rep[b][0] = XOR_j src[b][j]. */
 int fecgpu_xor_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k,
@@ -197,6 +213,12 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *ctx, void *src, const void 
  * are read in place, others are copied), the rows themselves must be device-accessible. */
 int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
                                 uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *fbn);
+/* fecgpu_rlc_decode_rows from the host: the row tables, seeds, masks, status and recovered are host
+ * arrays (page-locked ones are used in place, others copied); the rows must be device-accessible. */
+int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
+                                uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size,
+                                const uint32_t *rep_seed, const uint64_t *src_present, const uint64_t *rep_present,
+                                uint8_t *status, uint64_t *recovered);
 /* fecgpu_rlc_window_encode_table from the host: the stream (host rows) crosses PCIe once, by one copy,
  * before the windows are coded from device memory -- a symbol serves up to k windows, so reading it in
  * place would cross the bus that many times; wrow[] is a host array; repairs go to page-locked `rep` in
@@ -216,8 +238,9 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
  * kernel launch.  The worker ends by itself after 20 ms without a request (and after 2 s in all);
  * the next call relaunches it.  Every buffer must be page-locked (fecgpu_host_alloc, registered
  * ranges); the rows are zero-copy.  Returns FECGPU_ERR_INVALID when the block does not fit the
- * worker (e > 16 unknowns, rows beyond its LDS), a buffer is not page-locked, or knob block_svc is 0
- * -- the caller then takes the host path.  Thread-safe (one request at a time per service). */
+ * worker (e > 16 unknowns, rows beyond its LDS), a buffer is not page-locked, knob block_svc is 0, or
+ * the request was withdrawn at its deadline (below) -- the caller then takes the host path.
+ * Thread-safe (one request at a time per service). */
 typedef struct fecgpu_block_svc fecgpu_block_svc_t;
 fecgpu_block_svc_t *fecgpu_block_svc_create(int device);
 void fecgpu_block_svc_destroy(fecgpu_block_svc_t *svc);
@@ -231,6 +254,14 @@ int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *svc, const void *src,
                                        uint64_t *recovered);
 /* worker generations launched so far (diagnostics: one per idle gap) */
 uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *svc);
+/* A call waits at most `deadline_us` (default 2000) for the worker to serve its request.  Past it the
+ * worker is ended and waited for: the request is then either done (the call succeeds) or withdrawn --
+ * no worker serves it later -- and the call returns FECGPU_ERR_INVALID, so the caller takes the host
+ * path; for the next 50 ms every call returns FECGPU_ERR_INVALID at once (the worker was most likely
+ * queued behind a long kernel).  0: withdraw whatever is not done at the first check (tests). */
+int fecgpu_block_svc_set_deadline(fecgpu_block_svc_t *svc, uint64_t deadline_us);
+/* requests withdrawn at the deadline so far */
+uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *svc);
 
 /* FEC frames for a batch of repair symbols, ready for packet buffers (the block framework's
  * get_repair_payload_from_queue + write_fec_frame, block_framework_sender.h:100-133,

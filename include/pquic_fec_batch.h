@@ -58,6 +58,8 @@ typedef struct {
     uint64_t windows, window_rows;  /* window blocks coded from shared streams; stream rows staged for them */
     uint64_t engine_us, stage_us;   /* thread time in engine calls / in stager work items (all threads) */
     uint64_t complete_us;           /* caller-thread time in completions (poll / drain) */
+    uint64_t rows_in_place;         /* symbol rows the kernels read or wrote where they lie (registered arenas) */
+    uint64_t rows_staged;           /* symbol rows copied through the page-locked staging rows instead */
 } pquic_fec_batch_stats_t;
 
 /* NULL on failure (bad configuration, no device, out of pinned memory). */
@@ -67,11 +69,19 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b);
 
 /* Register a host memory range that holds symbols -- a FEC plugin instance's memory arena
  * (picoquic_internal.h:576, char memory[PLUGIN_MEMORY], carved into 2100-B slots by
- * picoquic/memory.c:181-191, registered once after init_memory_management, memory.c:254).  It is
- * page-locked and mapped (fecgpu_host_register) until the batcher is destroyed, and RLC generate
- * batches then read source symbols and write repair symbols in it directly instead of copying them
- * through staging rows.  Call before submitting.  Returns 0 or -1. */
+ * picoquic/memory.c:181-191, registered once after init_memory_management, memory.c:254).  Every
+ * connection owns its plugin instances (plugin.c:835, 946-950), so a process registers one arena per
+ * connection: any number of them, kept sorted and looked up by binary search, registered and
+ * unregistered while batches run (call from the thread that submits).  It is page-locked and mapped
+ * (fecgpu_host_register) until unregistered or the batcher is destroyed.  RLC generate batches then
+ * read source symbols and write repair symbols in it directly, and RLC recover batches read the received
+ * sources and repairs in it and write each recovered source into a symbol allocated for it at submission
+ * (through the bound allocator, so in the connection's arena), instead of copying rows through staging
+ * rows.  Returns 0, or -1 (NULL / empty range, overlap with a registered range, registration failure). */
 int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t bytes);
+/* Unregister the range registered at `base` (a connection closing).  No block whose symbols lie in it
+ * may still be queued: the caller has had every done() for them.  Returns 0 or -1. */
+int pquic_fec_batch_unregister_heap(pquic_fec_batcher_t *b, void *base);
 
 /* Queue fec_generate_repair_symbols (xor_scheme = 0: RLC-GF(256), 1: XOR) for `fb`, whose
  * totals are set as the block framework sets them before the call
@@ -95,8 +105,12 @@ int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_f
                             uint64_t now_us, pquic_fec_block_done_fn done, void *user);
 
 /* Flushes every queue that is full or past its deadline at `now_us`, then runs `done` for
- * the blocks whose batch has finished, in submission order per batch: all of them, or at most
- * cfg.poll_blocks.  Non-blocking.  Returns the number of completions. */
+ * the blocks whose batch has finished: all of them, or at most cfg.poll_blocks.  Batches complete
+ * in the order they were flushed (a finished batch waits for the ones flushed before it), and the
+ * blocks of a batch in submission order, so the blocks of one queue -- one (operation, scheme, k, r)
+ * -- complete in submission order, as the synchronous operation completes them one by one; a block
+ * whose preconditions fail completes inside its submission call.  Non-blocking.  Returns the number
+ * of completions. */
 int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us);
 /* Flushes everything and waits until every queued block has completed.  Returns the number
  * of completions. */

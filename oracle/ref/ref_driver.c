@@ -2,18 +2,23 @@
  * oracle/ref/ref_driver.c -- TEST INFRASTRUCTURE ONLY (this container).
  *
  * Links the reference's own FEC scheme pluglets, compiled in place from
- * /root/reference/plugins/fec/fec_scheme_protoops/*.c by oracle/ref/Makefile, into
+ * /root/reference/plugins/fec/fec_scheme_protoops/*.c by oracle/Makefile, into
  * oracle/_ref/libfecref.so, and drives them the way plugin_run_protoop_internal
- * (picoquic/plugin.c:1279-1450) does: inputs through get_cnx(cnx, AK_CNX_INPUT, i),
- * outputs through set_cnx(cnx, AK_CNX_OUTPUT, i, v) (picoquic/getset.c:137-142,370-379).
+ * (picoquic/plugin.c:1279-1450) does: a picoquic_cnx_t whose protoop_inputv / protoop_outputv
+ * carry the arguments, read and written by the reference's own accessors -- picoquic/getset.c,
+ * compiled in place and linked (get_cnx at :137-148, set_cnx at :370-379; the CC scenario's
+ * path, packet context and packets through its get_path / get_pkt_ctx / set_pkt_ctx / get_pkt).
  *
- * Stubs for the six pluglet API symbols the scheme objects import:
- *   get_cnx / set_cnx   -> global argument arrays
+ * Stand-ins, only for what the accessors and pluglets import and the tree cannot provide here:
+ *   get_plugin_metadata / set_plugin_metadata (plugin.c, uthash-based) -> the one FEC state slot
+ *   picoquic_set_cnx_state (quicctx.c) -> never reached by these pluglets, aborts if it is
  *   my_malloc           -> malloc of max(size, 2100): the plugin allocator hands out
  *                          fixed 2100-B slots (picoquic/memory.c:72-95,181-191) and the
  *                          RLC encoder relies on it (knowns[] is under-allocated,
- *                          rlc_fec_scheme_generate_gf256.c:50)
+ *                          rlc_fec_scheme_generate_gf256.c:50); memory.c itself includes the
+ *                          absent michelfralloc submodule
  *   my_free / my_memcpy / my_memset -> libc
+ *   plugin_run_protoop -> the transport protoops the pluglets call (skip_frame, the CC hooks)
  * Recover runs in a fork()ed child because the reference decoder dereferences x[-1]
  * on some erasure patterns (rlc_fec_scheme_gf256.c:74-77).
  */
@@ -26,27 +31,47 @@
 #include <unistd.h>
 
 #include <stddef.h>
+#include <stdio.h>
+#include "picoquic_internal.h"   /* picoquic_cnx_t / path / packet context as getset.c sees them */
 #include "fec/fec_protoops.h"     /* fec.h + frame helpers; resolved with -I$(REF)/plugins */
 #include "fec/prng/tinymt32.c"
 
-/* ---- pluglet API stubs ---- */
+/* ---- the connection the pluglets run on ---- */
 static protoop_arg_t g_in[PROTOOPARGS_MAX];
 static protoop_arg_t g_out[PROTOOPARGS_MAX];
-
-static int g_cc_path;   /* the CC scenario's path object (below) */
+static picoquic_cnx_t g_cnx;
+static protoop_plugin_t g_plugin;       /* the FEC plugin "running" (get_cnx_metadata needs one) */
+static picoquic_path_t g_cc_path;       /* the CC scenario's path (below) */
+static picoquic_path_t *g_paths[1] = {&g_cc_path};
 static int g_cc_active;
 
-protoop_arg_t get_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param) {
-    (void)cnx;
-    if (ak == AK_CNX_PATH) return (protoop_arg_t)&g_cc_path;
-    if (ak == AK_CNX_INPUT) return g_in[param];
-    if (ak == AK_CNX_OUTPUT) return g_out[param];
+/* The connection as plugin_run_protoop_internal hands it to a pluglet (plugin.c:1300-1390): the
+ * arguments in protoop_inputv, no outputs yet, the plugin current. */
+static picoquic_cnx_t *call_cnx(void) {
+    g_cnx.protoop_inputv = g_in;
+    g_cnx.protoop_inputc = PROTOOPARGS_MAX;
+    g_cnx.protoop_outputv = g_out;
+    g_cnx.protoop_outputc_callee = 0;
+    g_cnx.current_plugin = &g_plugin;
+    g_cnx.path = g_paths;
+    g_cnx.nb_paths = 1;
+    return &g_cnx;
+}
+
+static bpf_state g_state;  /* the FEC plugin's per-connection state (metadata slot FEC_OPAQUE_ID) */
+int get_plugin_metadata(protoop_plugin_t *plugin, plugin_struct_metadata_t **metadata, int idx, uint64_t *out) {
+    (void)plugin; (void)metadata;
+    *out = idx == FEC_OPAQUE_ID ? (uint64_t)(uintptr_t)&g_state : 0;
     return 0;
 }
-void set_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, protoop_arg_t val) {
-    (void)cnx;
-    if (ak == AK_CNX_OUTPUT) g_out[param] = val;
-    else if (ak == AK_CNX_INPUT) g_in[param] = val;
+int set_plugin_metadata(protoop_plugin_t *plugin, plugin_struct_metadata_t **metadata, int idx, uint64_t val) {
+    (void)plugin; (void)metadata; (void)idx; (void)val;
+    return 0;
+}
+void picoquic_set_cnx_state(picoquic_cnx_t *cnx, picoquic_state_enum state) {
+    (void)cnx; (void)state;
+    fprintf(stderr, "ref_driver: picoquic_set_cnx_state reached\n");
+    abort();
 }
 void *my_malloc(picoquic_cnx_t *cnx, unsigned int size) {
     (void)cnx;
@@ -70,7 +95,7 @@ static ref_rlc_scheme_t *g_scheme;
 static ref_rlc_scheme_t *scheme(void) {
     if (!g_scheme) {
         memset(g_out, 0, sizeof g_out);
-        if (rlc_create(NULL) == 0) g_scheme = (ref_rlc_scheme_t *)g_out[0];
+        if (rlc_create(call_cnx()) == 0) g_scheme = (ref_rlc_scheme_t *)g_out[0];
     }
     return g_scheme;
 }
@@ -85,7 +110,7 @@ int ref_gf_tables(uint8_t *mul, uint8_t *inv) {
 
 int ref_create_outputs(int xor_scheme, uint64_t *out0, uint64_t *out1) {
     memset(g_out, 0, sizeof g_out);
-    int ret = (int)(xor_scheme ? xor_create(NULL) : rlc_create(NULL));
+    int ret = (int)(xor_scheme ? xor_create(call_cnx()) : rlc_create(call_cnx()));
     *out0 = g_out[0]; *out1 = g_out[1];
     return ret;
 }
@@ -122,7 +147,7 @@ int ref_encode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
     fb->current_source_symbols = (uint8_t)k;
     g_in[0] = (protoop_arg_t)fb;
     g_in[1] = (protoop_arg_t)scheme();
-    int ret = (int)(xor_scheme ? xor_encode(NULL) : rlc_encode(NULL));
+    int ret = (int)(xor_scheme ? xor_encode(call_cnx()) : rlc_encode(call_cnx()));
     if (ret == 0) {
         for (int i = 0; i < r; i++) {
             repair_symbol_t *rs = fb->repair_symbols[i];
@@ -176,7 +201,7 @@ int ref_decode(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src,
         memcpy(before, fb->source_symbols, sizeof before);
         g_in[0] = (protoop_arg_t)fb;
         g_in[1] = (protoop_arg_t)scheme();
-        int ret = (int)(xor_scheme ? xor_decode(NULL) : rlc_decode(NULL));
+        int ret = (int)(xor_scheme ? xor_decode(call_cnx()) : rlc_decode(call_cnx()));
         int32_t *hdr = (int32_t *)shm;
         hdr[0] = ret;
         uint8_t *rec = shm + 64, *lens = rec + k, *data = lens + 2 * (size_t)k;
@@ -236,7 +261,7 @@ int ref_rlc_encode_batch(const uint8_t *src, uint8_t *rep, uint64_t nblocks, int
         }
         g_in[0] = (protoop_arg_t)&fb;
         g_in[1] = (protoop_arg_t)scheme();
-        if (rlc_encode(NULL) != 0) return -1;
+        if (rlc_encode(call_cnx()) != 0) return -1;
         for (int i = 0; i < r; i++) {
             memcpy(rep + (b * r + i) * L, fb.repair_symbols[i]->data, L);
             my_free(NULL, fb.repair_symbols[i]->data);
@@ -318,7 +343,7 @@ long ref_write_recovered(const uint64_t *packets, int n, uint8_t *bytes, long by
     g_in[0] = (protoop_arg_t)bytes;
     g_in[1] = (protoop_arg_t)(bytes + bytes_len);
     g_in[2] = (protoop_arg_t)rp;
-    long ret = (long)ref_write_recovered_frame(NULL);  /* frees rp */
+    long ret = (long)ref_write_recovered_frame(call_cnx());  /* frees rp */
     *consumed = (long)g_out[0];
     return ret;
 }
@@ -329,7 +354,7 @@ long ref_parse_recovered(const uint8_t *bytes, long bytes_len, uint64_t *packets
     memset(g_out, 0, sizeof g_out);
     g_in[0] = (protoop_arg_t)bytes;
     g_in[1] = (protoop_arg_t)(bytes + bytes_len);
-    protoop_arg_t end = ref_parse_recovered_frame(NULL);
+    protoop_arg_t end = ref_parse_recovered_frame(call_cnx());
     uint8_t *sp = (uint8_t *)g_out[0];
     *n = 0;
     if (sp) {
@@ -362,9 +387,6 @@ int ref_skip_frame_synthetic(const uint8_t *bytes, size_t bytes_max, size_t *con
     return 0;
 }
 
-static bpf_state g_state;
-protoop_arg_t get_cnx_metadata(picoquic_cnx_t *cnx, int idx) { (void)cnx; (void)idx; return (protoop_arg_t)&g_state; }
-void set_cnx_metadata(picoquic_cnx_t *cnx, int idx, protoop_arg_t val) { (void)cnx; (void)idx; (void)val; }
 static protoop_arg_t cc_protoop(const char *pid, protoop_params_t *pp);
 protoop_arg_t plugin_run_protoop(picoquic_cnx_t *cnx, protoop_params_t *pp, char *pid_str, protoop_id_t *pid) {
     (void)cnx; (void)pid;
@@ -390,7 +412,7 @@ long ref_payload_to_source_symbol(const uint8_t *payload, uint32_t len, uint64_t
     g_in[1] = (protoop_arg_t)buffer;
     g_in[2] = (protoop_arg_t)len;
     g_in[3] = (protoop_arg_t)pn;
-    long ret = (long)ref_packet_payload_to_source_symbol(NULL);
+    long ret = (long)ref_packet_payload_to_source_symbol(call_cnx());
     *state_len = g_state.current_symbol_length;
     return ret;
 }
@@ -434,7 +456,7 @@ static long ref_work_range(const uint8_t *src, uint8_t *rep, uint64_t b0, uint64
         }
         g_in[0] = (protoop_arg_t)&fb;
         g_in[1] = (protoop_arg_t)scheme();
-        if (rlc_encode(NULL) != 0) return -1;
+        if (rlc_encode(call_cnx()) != 0) return -1;
         for (int i = 0; i < r; i++) {
             memcpy(rep + ((b - b0) * r + i) * (size_t)L, fb.repair_symbols[i]->data, L);
             my_free(NULL, fb.repair_symbols[i]->data);
@@ -469,7 +491,7 @@ static long ref_work_range(const uint8_t *src, uint8_t *rep, uint64_t b0, uint64
         memcpy(before, fb.source_symbols, sizeof before);
         g_in[0] = (protoop_arg_t)&fb;
         g_in[1] = (protoop_arg_t)scheme();
-        if (rlc_decode(NULL) != 0) return -1;
+        if (rlc_decode(call_cnx()) != 0) return -1;
         for (int j = 0; j < k; j++)
             if (fb.source_symbols[j] && fb.source_symbols[j] != before[j]) {
                 my_free(NULL, fb.source_symbols[j]->data);
@@ -568,13 +590,13 @@ long ref_work_serial(const uint8_t *src, uint64_t nblocks, int k, int r, int L, 
  *   1 retransmit_needed_by_packet(pn, now, timer_based_in)   2 packet_was_lost(pn)
  *   3 dequeue_retransmit_packet(pn, should_free)             4 congestion_algorithm_notify(notification,
  *   5 set latest CC notification time(t)                        lost pn, now) [rtt / bytes are 0] */
-typedef struct { uint64_t pn; int pure_ack, needed; } cc_pkt_t;
-static cc_pkt_t *g_cc_pkts;
+static picoquic_packet_t *g_cc_pkts;  /* the retransmit queue, linked through next_packet */
+static uint8_t *g_cc_needed;          /* retransmit_needed_by_packet's verdict per packet */
 static int g_cc_n;
-static uint64_t g_cc_srtt, g_cc_latest;
 static uint64_t *g_cc_ev;
 static int g_cc_nev, g_cc_maxev;
-static int g_cc_ctx;  /* its address stands in for the packet context (g_cc_path: the path) */
+
+static picoquic_packet_context_t *cc_ctx(void) { return &g_cc_path.pkt_ctx[picoquic_packet_context_application]; }
 
 static void cc_log(uint64_t k, uint64_t a, uint64_t b, uint64_t c) {
     if (g_cc_nev < g_cc_maxev) {
@@ -584,49 +606,27 @@ static void cc_log(uint64_t k, uint64_t a, uint64_t b, uint64_t c) {
     g_cc_nev++;
 }
 
-protoop_arg_t get_path(picoquic_path_t *path, access_key_t ak, uint16_t param) {
-    (void)path; (void)param;
-    if (ak == AK_PATH_PKT_CTX) return (protoop_arg_t)&g_cc_ctx;
-    if (ak == AK_PATH_SMOOTHED_RTT) return g_cc_srtt;
-    return 0;
-}
-protoop_arg_t get_pkt_ctx(picoquic_packet_context_t *ctx, access_key_t ak) {
-    (void)ctx;
-    if (ak == AK_PKTCTX_RETRANSMIT_OLDEST) return g_cc_n ? (protoop_arg_t)&g_cc_pkts[0] : 0;
-    if (ak == AK_PKTCTX_LATEST_RETRANSMIT_CC_NOTIFICATION_TIME) return g_cc_latest;
-    return 0;
-}
-void set_pkt_ctx(picoquic_packet_context_t *ctx, access_key_t ak, protoop_arg_t val) {
-    (void)ctx;
-    if (ak == AK_PKTCTX_LATEST_RETRANSMIT_CC_NOTIFICATION_TIME) {
-        g_cc_latest = val;
-        cc_log(5, val, 0, 0);
-    }
-}
-protoop_arg_t get_pkt(picoquic_packet_t *pkt, access_key_t ak) {
-    cc_pkt_t *p = (cc_pkt_t *)pkt;
-    if (ak == AK_PKT_NEXT_PACKET) return p + 1 < g_cc_pkts + g_cc_n ? (protoop_arg_t)(p + 1) : 0;
-    if (ak == AK_PKT_SEQUENCE_NUMBER) return p->pn;
-    if (ak == AK_PKT_IS_PURE_ACK) return (protoop_arg_t)p->pure_ack;
-    return 0;
-}
-
+/* The transport protoops the pluglet calls.  Event 5 (the pluglet's set_pkt_ctx of the latest CC
+ * notification time, which getset.c performs without telling anyone) is logged from the field itself
+ * right before the notification it always precedes (fec_protoops.h:171-174: set, then notify, in
+ * one branch and nowhere else). */
 static protoop_arg_t cc_protoop(const char *pid, protoop_params_t *pp) {
     if (strcmp(pid, PROTOOPID_NOPARAM_RETRANSMIT_NEEDED_BY_PACKET) == 0) {
-        cc_pkt_t *p = (cc_pkt_t *)pp->inputv[0];
-        cc_log(1, p->pn, pp->inputv[1], pp->inputv[2]);
+        picoquic_packet_t *p = (picoquic_packet_t *)pp->inputv[0];
+        cc_log(1, p->sequence_number, pp->inputv[1], pp->inputv[2]);
         if (pp->outputv) { pp->outputv[0] = 0; pp->outputv[1] = 0; pp->outputv[2] = 0; }
-        return (protoop_arg_t)p->needed;
+        return (protoop_arg_t)g_cc_needed[p - g_cc_pkts];
     }
     if (strcmp(pid, PROTOOPID_NOPARAM_PACKET_WAS_LOST) == 0) {
-        cc_log(2, ((cc_pkt_t *)pp->inputv[0])->pn, pp->inputv[1] == (protoop_arg_t)&g_cc_path, 0);
+        cc_log(2, ((picoquic_packet_t *)pp->inputv[0])->sequence_number, pp->inputv[1] == (protoop_arg_t)&g_cc_path, 0);
         return 0;
     }
     if (strcmp(pid, PROTOOPID_NOPARAM_DEQUEUE_RETRANSMIT_PACKET) == 0) {
-        cc_log(3, ((cc_pkt_t *)pp->inputv[0])->pn, pp->inputv[1], 0);
+        cc_log(3, ((picoquic_packet_t *)pp->inputv[0])->sequence_number, pp->inputv[1], 0);
         return 0;
     }
     if (strcmp(pid, PROTOOPID_NOPARAM_CONGESTION_ALGORITHM_NOTIFY) == 0) {
+        cc_log(5, cc_ctx()->latest_retransmit_cc_notification_time, 0, 0);
         cc_log(4, pp->inputv[1], pp->inputv[4], pp->inputv[5]);
         return 0;
     }
@@ -640,9 +640,21 @@ protoop_arg_t ref_prepare_packet_ready(picoquic_cnx_t *cnx);
 int ref_cc_scenario(int n, const uint64_t *pns, const uint8_t *pure, const uint8_t *needed, uint64_t srtt,
                     uint64_t latest, uint64_t now, uint32_t *buf_start, uint32_t *buf_size, uint64_t *buf_pns,
                     uint64_t *events, int maxev, uint64_t *latest_out) {
-    cc_pkt_t *pk = calloc((size_t)(n ? n : 1), sizeof *pk);
-    for (int i = 0; i < n; i++) { pk[i].pn = pns[i]; pk[i].pure_ack = pure[i]; pk[i].needed = needed[i]; }
-    g_cc_pkts = pk; g_cc_n = n; g_cc_srtt = srtt; g_cc_latest = latest;
+    picoquic_packet_t *pk = calloc((size_t)(n ? n : 1), sizeof *pk);
+    uint8_t *nd = calloc((size_t)(n ? n : 1), 1);
+    for (int i = 0; i < n; i++) {
+        pk[i].sequence_number = pns[i];
+        pk[i].is_pure_ack = pure[i] ? 1 : 0;
+        pk[i].next_packet = i + 1 < n ? &pk[i + 1] : NULL;
+        pk[i].previous_packet = i ? &pk[i - 1] : NULL;
+        nd[i] = needed[i];
+    }
+    memset(&g_cc_path, 0, sizeof g_cc_path);
+    g_cc_path.smoothed_rtt = srtt;
+    cc_ctx()->retransmit_oldest = n ? &pk[0] : NULL;
+    cc_ctx()->retransmit_newest = n ? &pk[n - 1] : NULL;
+    cc_ctx()->latest_retransmit_cc_notification_time = latest;
+    g_cc_pkts = pk; g_cc_needed = nd; g_cc_n = n;
     g_cc_ev = events; g_cc_nev = 0; g_cc_maxev = maxev;
     memset(&g_state, 0, sizeof g_state);
     g_state.recovered_packets.start = *buf_start;
@@ -651,13 +663,14 @@ int ref_cc_scenario(int n, const uint64_t *pns, const uint8_t *pure, const uint8
     memset(g_in, 0, sizeof g_in);
     g_in[2] = now;
     g_cc_active = 1;
-    ref_prepare_packet_ready(NULL);
+    ref_prepare_packet_ready(call_cnx());
     g_cc_active = 0;
     *buf_start = g_state.recovered_packets.start;
     *buf_size = g_state.recovered_packets.size;
     memcpy(buf_pns, g_state.recovered_packets.packet_numbers, sizeof g_state.recovered_packets.packet_numbers);
-    *latest_out = g_cc_latest;
+    *latest_out = cc_ctx()->latest_retransmit_cc_notification_time;
     free(pk);
+    free(nd);
     return g_cc_nev;
 }
 
@@ -676,7 +689,7 @@ void ref_process_recovered(const uint64_t *pns, int n, uint32_t *buf_start, uint
     memcpy(g_state.recovered_packets.packet_numbers, buf_pns, sizeof g_state.recovered_packets.packet_numbers);
     memset(g_in, 0, sizeof g_in);
     g_in[0] = (protoop_arg_t)sp;
-    ref_process_recovered_frame(NULL);
+    ref_process_recovered_frame(call_cnx());
     *buf_start = g_state.recovered_packets.start;
     *buf_size = g_state.recovered_packets.size;
     memcpy(buf_pns, g_state.recovered_packets.packet_numbers, sizeof g_state.recovered_packets.packet_numbers);

@@ -45,7 +45,7 @@
 
 enum { OP_GENERATE = 0, OP_RECOVER = 1, OP_WINDOW = 2 /* generate, window blocks */ };
 #define GENERATES(op) ((op) != OP_RECOVER)
-enum { MAX_OPEN = 32, MAX_STAGERS = 16, MAX_ENGINES = 4, STAGE_CHUNK = 256 /* blocks per staging work item */, MAX_HEAPS = 64 };
+enum { MAX_OPEN = 32, MAX_STAGERS = 16, MAX_ENGINES = 4, STAGE_CHUNK = 256 /* blocks per staging work item */ };
 
 typedef struct {
     uintptr_t base;
@@ -80,7 +80,12 @@ typedef struct job {
     int post;                      /* 1 once the engine ran: work items copy repairs out */
     uint32_t next_chunk, chunks_done;  /* staging work items claimed / finished (under the batcher lock) */
     int gather;                    /* generate with row tables (fecgpu_rlc_encode_rows) */
-    uint64_t *srow, *rrow;         /* pinned: [cap][k] source / [cap][r] repair row device addresses */
+    uint64_t *srow, *rrow;         /* pinned: [cap][k] source / [cap][r] repair row device addresses (recover:
+                                    * a missing source's entry is the row its recovered bytes go to) */
+    pquic_source_symbol_t **pre;   /* recover gather: [cap][k] symbols allocated at submission for the missing
+                                    * sources (written in place by the kernel), NULL where none */
+    size_t pre_cap;
+    uint64_t seq;                  /* flush order: completions are handed out in it */
     size_t srow_cap, rrow_cap;
     uint64_t src_dev, rep_dev;     /* device addresses of the staging rows */
     uint8_t *copy;                 /* gather: block needs its repairs copied out of the staging rows */
@@ -111,33 +116,90 @@ struct pquic_fec_batcher {
     job_t *completing;             /* finished job whose completions a bounded poll left part-done */
     uint32_t completing_i;         /* its next entry */
     pquic_fec_batch_stats_t stats;
-    heap_t heaps[MAX_HEAPS];
-    int nheaps;
+    uint64_t next_seq;             /* caller thread: sequence number of the next flushed job */
+    uint64_t collect_seq;          /* caller thread: the job whose completions come next */
+    /* registered arenas, sorted by base and disjoint; stagers look rows up under the read lock (one
+     * lock per work item), registration takes the write lock, so connections may come and go while
+     * batches run */
+    heap_t *heaps;
+    int nheaps, heaps_cap;
+    pthread_rwlock_t heaps_mu;
 };
 
-/* device address of [p, p + n) when it lies in a registered heap, else 0 */
-static uint64_t heap_dev(const pquic_fec_batcher_t *b, const void *p, size_t n) {
-    const uintptr_t a = (uintptr_t)p;
-    for (int i = 0; i < b->nheaps; i++) {
-        const heap_t *h = &b->heaps[i];
-        if (a - h->base < h->size && n <= h->size - (a - h->base) && (a & 3) == 0) return h->dev + (a - h->base);
+/* Index of the last registered heap whose base is <= a, or -1 (caller holds heaps_mu). */
+static int heap_floor(const pquic_fec_batcher_t *b, uintptr_t a) {
+    int lo = 0, hi = b->nheaps - 1, f = -1;
+    while (lo <= hi) {
+        const int m = (lo + hi) >> 1;
+        if (b->heaps[m].base <= a) {
+            f = m;
+            lo = m + 1;
+        } else {
+            hi = m - 1;
+        }
     }
-    return 0;
+    return f;
+}
+
+/* Device address of [p, p + n) when it lies in one registered heap, else 0 (caller holds heaps_mu for
+ * reading).  *hint: the heap the previous row was found in -- a block's rows, and a connection's
+ * blocks, come from one arena -- tried before the binary search. */
+static uint64_t heap_dev(const pquic_fec_batcher_t *b, const void *p, size_t n, int *hint) {
+    const uintptr_t a = (uintptr_t)p;
+    if ((a & 3) || !b->nheaps) return 0;
+    int i = *hint;
+    if (i < 0 || i >= b->nheaps || a - b->heaps[i].base >= b->heaps[i].size) i = heap_floor(b, a);
+    if (i < 0) return 0;
+    const heap_t *h = &b->heaps[i];
+    if (a - h->base >= h->size || n > h->size - (a - h->base)) return 0;
+    *hint = i;
+    return h->dev + (a - h->base);
 }
 
 int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t bytes) {
-    if (!b || !base || !bytes || b->nheaps >= MAX_HEAPS) return -1;
-    if (fecgpu_host_register(base, bytes) != FECGPU_OK) return -1;
-    uint64_t dev = 0;
-    if (fecgpu_host_device_address(base, bytes, &dev) != FECGPU_OK) {
-        fecgpu_host_unregister(base);
-        return -1;
+    if (!b || !base || !bytes) return -1;
+    const uintptr_t a = (uintptr_t)base;
+    pthread_rwlock_wrlock(&b->heaps_mu);
+    const int f = heap_floor(b, a);
+    const int overlap = (f >= 0 && a - b->heaps[f].base < b->heaps[f].size) ||
+                        (f + 1 < b->nheaps && b->heaps[f + 1].base - a < bytes);
+    int rc = -1;
+    if (!overlap) {
+        if (b->nheaps == b->heaps_cap) {
+            const int nc = b->heaps_cap ? 2 * b->heaps_cap : 64;
+            heap_t *nh = realloc(b->heaps, sizeof *nh * (size_t)nc);
+            if (!nh) goto out;
+            b->heaps = nh;
+            b->heaps_cap = nc;
+        }
+        if (fecgpu_host_register(base, bytes) != FECGPU_OK) goto out;
+        uint64_t dev = 0;
+        if (fecgpu_host_device_address(base, bytes, &dev) != FECGPU_OK) {
+            fecgpu_host_unregister(base);
+            goto out;
+        }
+        memmove(&b->heaps[f + 2], &b->heaps[f + 1], sizeof *b->heaps * (size_t)(b->nheaps - f - 1));
+        b->heaps[f + 1] = (heap_t){a, bytes, dev};
+        b->nheaps++;
+        rc = 0;
     }
-    pthread_mutex_lock(&b->mu);  /* stagers read the list while holding no lock: register before traffic */
-    b->heaps[b->nheaps] = (heap_t){(uintptr_t)base, bytes, dev};
-    b->nheaps++;
-    pthread_mutex_unlock(&b->mu);
-    return 0;
+out:
+    pthread_rwlock_unlock(&b->heaps_mu);
+    return rc;
+}
+
+int pquic_fec_batch_unregister_heap(pquic_fec_batcher_t *b, void *base) {
+    if (!b || !base) return -1;
+    pthread_rwlock_wrlock(&b->heaps_mu);  /* no stager is between a lookup and its use of the heap */
+    const int f = heap_floor(b, (uintptr_t)base);
+    int rc = -1;
+    if (f >= 0 && b->heaps[f].base == (uintptr_t)base) {
+        memmove(&b->heaps[f], &b->heaps[f + 1], sizeof *b->heaps * (size_t)(b->nheaps - f - 1));
+        b->nheaps--;
+        rc = fecgpu_host_unregister(base) == FECGPU_OK ? 0 : -1;
+    }
+    pthread_rwlock_unlock(&b->heaps_mu);
+    return rc;
 }
 
 static void job_free(job_t *j) {
@@ -147,6 +209,7 @@ static void job_free(job_t *j) {
     free(j->order);
     fecgpu_host_free(j->srow);
     fecgpu_host_free(j->rrow);
+    free(j->pre);
     free(j->copy);
     fecgpu_host_free(j->src);
     fecgpu_host_free(j->rep);
@@ -199,8 +262,13 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         }
         j->seed_bytes = eb;
     }
-    /* gather tables (RLC generate with a registered heap): grown on reuse like the repair table */
-    j->gather = op == OP_GENERATE && !xor_scheme && b->nheaps > 0;
+    /* gather tables (RLC generate or recover with a registered heap): grown on reuse like the repair table */
+    j->gather = (op == OP_GENERATE || op == OP_RECOVER) && !xor_scheme && __atomic_load_n(&b->nheaps, __ATOMIC_RELAXED) > 0;
+    if (j->gather && op == OP_RECOVER && j->pre_cap < (size_t)cap * k) {
+        free(j->pre);
+        j->pre_cap = (j->pre = calloc((size_t)cap * k, sizeof *j->pre)) ? (size_t)cap * k : 0;
+        if (!j->pre) j->gather = 0;
+    }
     if (j->gather && (j->srow_cap < (size_t)cap * k || j->rrow_cap < (size_t)cap * r || !j->copy)) {
         if (j->srow_cap < (size_t)cap * k) {
             fecgpu_host_free(j->srow);
@@ -264,6 +332,9 @@ static void run_engine(fecgpu_host_ctx_t *c, job_t *j) {
     const uint32_t S = j->stride;
     if (j->op == OP_WINDOW)
         j->rc = fecgpu_rlc_window_encode_host(c, j->src, j->nrows, j->wrow, j->n, j->k, j->r, S, j->rep);
+    else if (j->gather && j->op == OP_RECOVER)
+        j->rc = fecgpu_rlc_decode_rows_host(c, j->srow, j->rrow, j->n, j->k, j->r, S, j->seeds, j->sp, j->rp, j->st,
+                                            j->rec);
     else if (j->gather)
         j->rc = fecgpu_rlc_encode_rows_host(c, j->srow, j->rrow, j->n, j->k, j->r, S, j->fbn);
     else if (j->op == OP_GENERATE)
@@ -280,38 +351,122 @@ static void run_engine(fecgpu_host_ctx_t *c, job_t *j) {
  * registered heap and is as long as the block (shorter ones are zero-padded, :41-55, so they are
  * staged); a repair row is written in place when its symbol is in a heap and as long as the stride
  * (the kernel writes `stride` bytes), else into the staging rows and copied out after the engine. */
-static void gather_blocks(const pquic_fec_batcher_t *b, job_t *j, uint32_t i0, uint32_t i1) {
+static void gather_recover_blocks(pquic_fec_batcher_t *b, job_t *j, uint32_t i0, uint32_t i1);
+
+static void gather_blocks(pquic_fec_batcher_t *b, job_t *j, uint32_t i0, uint32_t i1) {
+    if (j->op == OP_RECOVER) {
+        gather_recover_blocks(b, j, i0, i1);
+        return;
+    }
     const uint32_t S = j->stride, k = j->k, r = j->r;
     uint32_t ncopy = 0;
+    uint64_t inplace = 0, staged = 0;
+    int hint = -1;
+    pthread_rwlock_rdlock(&b->heaps_mu);
     for (uint32_t i = i0; i < i1; i++) {
         const entry_t *e = &j->ent[i];
         const pquic_fec_block_t *fb = e->fb;
         for (uint32_t x = 0; x < k; x++) {
             const pquic_source_symbol_t *ss = fb->source_symbols[x];
             const size_t o = ((size_t)i * k + x) * S;
-            uint64_t d = ss && ss->data_length == e->maxl ? heap_dev(b, ss->data, S) : 0;
+            uint64_t d = ss && ss->data_length == e->maxl ? heap_dev(b, ss->data, S, &hint) : 0;
             if (!d) {  /* staged, zero-padded to the stride */
                 const uint16_t n = ss ? ss->data_length : 0;
                 if (n) memcpy(j->src + o, ss->data, n);
                 memset(j->src + o + n, 0, S - n);
                 d = j->src_dev + o;
+                staged++;
+            } else {
+                inplace++;
             }
             j->srow[(size_t)i * k + x] = d;
         }
         uint8_t cp = 0;
         for (uint32_t x = 0; x < r; x++) {
             pquic_repair_symbol_t *rs = (int)x < e->nalloc ? j->reps[(size_t)i * r + x] : NULL;
-            uint64_t d = rs && e->maxl == S ? heap_dev(b, rs->data, S) : 0;
+            uint64_t d = rs && e->maxl == S ? heap_dev(b, rs->data, S, &hint) : 0;
             if (!d) {
                 d = j->rep_dev + ((size_t)i * r + x) * S;
                 cp |= rs != NULL;
+                staged += rs != NULL;
+            } else {
+                inplace++;
             }
             j->rrow[(size_t)i * r + x] = d;
         }
         j->copy[i] = cp;
         ncopy += cp;
     }
+    pthread_rwlock_unlock(&b->heaps_mu);
     if (ncopy) __atomic_fetch_add(&j->ncopy, ncopy, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&b->stats.rows_in_place, inplace, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&b->stats.rows_staged, staged, __ATOMIC_RELAXED);
+}
+
+/* Recover gather: the tables of blocks [i0, i1).  A block is read in place only when its length (the
+ * first present repair's, rlc_fec_scheme_gf256.c:186) is the stride -- the kernel reads and writes
+ * `stride` bytes per row and its zero rule looks at all of them (:98-101), so no byte past max_length may
+ * reach it -- and then a received source or repair row is read where it lies when it is in a registered
+ * heap and at least that long (longer ones are read up to max_length, the reference's truncation, :205);
+ * a missing source's row is the symbol allocated for it at submission.  Everything else is staged as
+ * fec_recover_stage stages it (truncated, zero-padded), recovered bytes into the staging row. */
+static void gather_recover_blocks(pquic_fec_batcher_t *b, job_t *j, uint32_t i0, uint32_t i1) {
+    const uint32_t S = j->stride, k = j->k, r = j->r;
+    uint64_t inplace = 0, staged = 0;
+    int hint = -1;
+    pthread_rwlock_rdlock(&b->heaps_mu);
+    for (uint32_t i = i0; i < i1; i++) {
+        const entry_t *e = &j->ent[i];
+        const pquic_fec_block_t *fb = e->fb;
+        const int whole = e->maxl == S;
+        uint64_t *sp = j->sp + 2 * (size_t)i, *rp = j->rp + 2 * (size_t)i;
+        sp[0] = sp[1] = rp[0] = rp[1] = 0;
+        for (uint32_t x = 0; x < k; x++) {
+            const pquic_source_symbol_t *ss = fb->source_symbols[x];
+            const size_t o = ((size_t)i * k + x) * S;
+            uint64_t d = 0;
+            if (ss) {
+                sp[x >> 6] |= 1ull << (x & 63);
+                d = whole && ss->data_length >= S ? heap_dev(b, ss->data, S, &hint) : 0;
+                if (!d) {
+                    const uint16_t n = ss->data_length < e->maxl ? ss->data_length : e->maxl;
+                    memcpy(j->src + o, ss->data, n);
+                    memset(j->src + o + n, 0, S - n);
+                    staged++;
+                } else {
+                    inplace++;
+                }
+            } else {
+                const pquic_source_symbol_t *pre = j->pre[(size_t)i * k + x];
+                d = whole && pre ? heap_dev(b, pre->data, S, &hint) : 0;
+                inplace += d != 0;
+            }
+            j->srow[(size_t)i * k + x] = d ? d : j->src_dev + o;
+        }
+        for (uint32_t x = 0; x < r; x++) {
+            const pquic_repair_symbol_t *rs = fb->repair_symbols[x];
+            const size_t o = ((size_t)i * r + x) * S;
+            uint64_t d = 0;
+            if (rs) {
+                rp[x >> 6] |= 1ull << (x & 63);
+                d = whole && rs->data_length >= S ? heap_dev(b, rs->data, S, &hint) : 0;
+                if (!d) {
+                    const uint16_t n = rs->data_length < e->maxl ? rs->data_length : e->maxl;
+                    memcpy(j->rep + o, rs->data, n);
+                    memset(j->rep + o + n, 0, S - n);
+                    staged++;
+                } else {
+                    inplace++;
+                }
+            }
+            j->rrow[(size_t)i * r + x] = d ? d : j->rep_dev + o;  /* absent repairs: never read */
+            /* every equation is seeded by its repair's own FPID (rlc_fec_scheme_gf256.c:200) */
+            j->seeds[(size_t)i * r + x] = rs ? rs->fpid.f.source_fpid.raw : 0;
+        }
+    }
+    pthread_rwlock_unlock(&b->heaps_mu);
+    __atomic_fetch_add(&b->stats.rows_in_place, inplace, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&b->stats.rows_staged, staged, __ATOMIC_RELAXED);
 }
 
 /* Copies blocks [i0, i1) of a job into its page-locked rows (the stage halves of fec_core.c). */
@@ -380,9 +535,14 @@ static void copy_out_blocks(job_t *j, uint32_t i0, uint32_t i1) {
     const uint32_t S = j->stride, r = j->r;
     for (uint32_t i = i0; i < i1; i++) {
         const entry_t *e = &j->ent[i];
-        if (j->gather && !j->copy[i]) continue;  /* written in place by the kernel */
-        for (int x = 0; x < e->nalloc; x++)
-            memcpy(j->reps[(size_t)i * r + x]->data, j->rep + ((size_t)i * r + x) * S, e->maxl);
+        if (j->gather && !j->copy[i]) continue;  /* every row written in place by the kernel */
+        for (int x = 0; x < e->nalloc; x++) {
+            const size_t q = (size_t)i * r + x;
+            /* a block's repairs may be split between the arena and other memory (an arena filled part
+             * way through the block): only the rows the kernel wrote into the staging area are copied */
+            if (j->gather && j->rrow[q] != j->rep_dev + q * S) continue;
+            memcpy(j->reps[q]->data, j->rep + q * S, e->maxl);
+        }
     }
 }
 
@@ -396,6 +556,20 @@ static void push(job_t **head, job_t **tail, job_t *j) {
     j->next = NULL;
     if (*tail) (*tail)->next = j; else *head = j;
     *tail = j;
+}
+
+/* Finished jobs wait in flush order (two engine threads, and generate jobs that take a copy-out pass,
+ * can finish out of it), so completions reach the caller in the order its blocks were submitted, across
+ * batches too, as the synchronous operations complete (caller holds b->mu). */
+static void push_done(pquic_fec_batcher_t *b, job_t *j) {
+    if (!b->done_tail || b->done_tail->seq < j->seq) {
+        push(&b->done_head, &b->done_tail, j);
+        return;
+    }
+    job_t **pp = &b->done_head;
+    while (*pp && (*pp)->seq < j->seq) pp = &(*pp)->next;
+    j->next = *pp;
+    *pp = j;
 }
 
 /* Stager threads split every job into work items of STAGE_CHUNK blocks, so several threads copy
@@ -430,7 +604,7 @@ static void *stager_main(void *arg) {
         b->stats.stage_us += dt;
         if (++j->chunks_done == nchunks) {
             if (j->post) {
-                push(&b->done_head, &b->done_tail, j);
+                push_done(b, j);
                 b->inflight--;
                 pthread_cond_broadcast(&b->cv_done);
             } else {
@@ -510,7 +684,7 @@ static void *worker_main(void *arg) {
             push(&b->post_head, &b->post_tail, j);
             pthread_cond_broadcast(&b->cv_todo);
         } else {
-            push(&b->done_head, &b->done_tail, j);
+            push_done(b, j);
             b->inflight--;
             pthread_cond_broadcast(&b->cv_done);
         }
@@ -539,6 +713,7 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
         }
     }
     pthread_mutex_init(&b->mu, NULL);
+    pthread_rwlock_init(&b->heaps_mu, NULL);
     pthread_cond_init(&b->cv_todo, NULL);
     pthread_cond_init(&b->cv_staged, NULL);
     pthread_cond_init(&b->cv_done, NULL);
@@ -575,6 +750,7 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
         pthread_cond_destroy(&b->cv_staged);
         pthread_cond_destroy(&b->cv_done);
         pthread_mutex_destroy(&b->mu);
+        pthread_rwlock_destroy(&b->heaps_mu);
         for (int e = 0; e < b->nengines; e++) fecgpu_host_ctx_destroy(b->ctx[e]);
         free(b);
         return NULL;
@@ -593,6 +769,7 @@ static void flush_job(pquic_fec_batcher_t *b, int slot, uint64_t *counter) {
     }
     (*counter)++;
     b->stats.batches++;
+    j->seq = b->next_seq++;
     pthread_mutex_lock(&b->mu);
     j->next = NULL;
     if (b->todo_tail) b->todo_tail->next = j; else b->todo_head = j;
@@ -671,6 +848,8 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
     j->ent[i] = (entry_t){cnx, fb, done, user, maxl, -1};
     if (GENERATES(op))  /* the protocol operation's allocations, in its order, on this thread */
         j->ent[i].nalloc = (int16_t)fec_generate_alloc(cnx, fb, maxl, j->reps + (size_t)i * r);
+    else if (j->gather)  /* the recovered symbols, so the kernel writes them where they will stay */
+        fec_recover_alloc(cnx, fb, maxl, j->pre + (size_t)i * k);
     if (!i) j->t_first = now_us;
     j->n = i + 1;
     b->stats.submitted++;
@@ -705,8 +884,17 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     job_t *j = b->completing;
     if (!j || __atomic_load_n(&b->done_head, __ATOMIC_RELAXED)) {  /* and the finished jobs behind it */
         pthread_mutex_lock(&b->mu);
-        job_t *more = b->done_head;
-        b->done_head = b->done_tail = NULL;
+        /* the finished jobs that continue the flush order; a later job waits for the ones before it */
+        job_t *more = NULL, **tail = &more;
+        while (b->done_head && b->done_head->seq == b->collect_seq) {
+            job_t *x = b->done_head;
+            b->done_head = x->next;
+            x->next = NULL;
+            *tail = x;
+            tail = &x->next;
+            b->collect_seq++;
+        }
+        if (!b->done_head) b->done_tail = NULL;
         pthread_mutex_unlock(&b->mu);
         if (!j) {
             j = more;
@@ -732,6 +920,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
             if (i + 4 < j->n) __builtin_prefetch(j->ent[i + 4].fb, 1);  /* the blocks were last touched at submission */
             protoop_arg_t ret;
             pquic_repair_symbol_t **reps = GENERATES(j->op) ? j->reps + (size_t)i * j->r : NULL;
+            pquic_source_symbol_t **pre = j->op == OP_RECOVER && j->gather ? j->pre + (size_t)i * j->k : NULL;
             if (j->rc) {
                 FEC_STAT_ADD(errors, 1);
                 ret = PQUIC_FEC_ERR_UNBOUND;
@@ -739,8 +928,22 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
                     g_fec_api.my_free(e->cnx, reps[x]->data);
                     g_fec_api.my_free(e->cnx, reps[x]);
                 }
+                for (uint32_t x = 0; pre && x < j->k; x++)
+                    if (pre[x]) {
+                        g_fec_api.my_free(e->cnx, pre[x]->data);
+                        g_fec_api.my_free(e->cnx, pre[x]);
+                        pre[x] = NULL;
+                    }
             } else if (GENERATES(j->op)) {
                 ret = fec_generate_attach(e->fb, reps, e->nalloc);
+            } else if (pre) {
+                /* rows the kernel wrote into the staging area (no in-place row for them) are copied */
+                uint64_t copy[2] = {0, 0};
+                const uint64_t s0 = j->src_dev + (uint64_t)i * j->k * S;
+                for (uint32_t x = 0; x < j->k; x++)
+                    if (j->srow[(size_t)i * j->k + x] == s0 + (uint64_t)x * S) copy[x >> 6] |= 1ull << (x & 63);
+                ret = fec_recover_finish_pre(e->cnx, e->fb, j->st[i], j->rec + 2 * (size_t)i, pre, copy,
+                                             j->src + (size_t)i * j->k * S, S, e->maxl);
             } else {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);
@@ -813,6 +1016,8 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
         job_free(j);
     }
     for (int i = 0; i < b->nheaps; i++) fecgpu_host_unregister((void *)b->heaps[i].base);
+    free(b->heaps);
+    pthread_rwlock_destroy(&b->heaps_mu);
     for (int e = 0; e < b->nengines; e++) fecgpu_host_ctx_destroy(b->ctx[e]);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->cv_todo);

@@ -174,3 +174,44 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
     }
     return ret;
 }
+
+int fec_recover_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t maxl, pquic_source_symbol_t **pre) {
+    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+    int n = 0;
+    for (int j = 0; j < fb->total_source_symbols; j++) {
+        pre[j] = NULL;
+        if (fb->source_symbols[j]) continue;
+        if ((pre[j] = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) n++;
+    }
+    return n;
+}
+
+protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, uint8_t status, const uint64_t rec[2],
+                                     pquic_source_symbol_t **pre, const uint64_t copy[2], const uint8_t *src_rows,
+                                     uint32_t stride, uint16_t maxl) {
+    const int k = fb->total_source_symbols;
+    const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+    if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
+    for (int j = 0; j < k; j++) {  /* :218-236, in source order as the reference inserts them */
+        const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
+        pquic_source_symbol_t *ss = pre[j];
+        pre[j] = NULL;
+        if (!got) {
+            if (ss) {  /* allocated for a source the reference leaves unrecovered */
+                g_fec_api.my_free(cnx, ss->data);
+                g_fec_api.my_free(cnx, ss);
+            }
+            continue;
+        }
+        if (!ss) {
+            if (!(ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) continue;
+            memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
+        } else if ((copy[j >> 6] >> (j & 63)) & 1) {
+            memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
+        }
+        fb->source_symbols[j] = ss;
+        fb->current_source_symbols++;
+        FEC_STAT_ADD(recovered_symbols, 1);
+    }
+    return 0;
+}

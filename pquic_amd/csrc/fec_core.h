@@ -70,6 +70,20 @@ void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t max
 protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme, uint8_t status,
                                  const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl);
 
+/* RLC recover with the recovered symbols allocated before the engine (the batching adapter's gather
+ * path, batch.c): fec_recover_alloc allocates one source symbol of maxl bytes, FPID (fbn << 8) + j, for
+ * every missing source j into pre[j] (pre[j] = NULL for received sources and failed allocations) and
+ * returns how many it got; the engine then writes the recovered bytes into their data.  After it,
+ * fec_recover_finish_pre inserts pre[j] for every recovered source (first copying maxl bytes from
+ * src_rows row j when bit j of `copy` is set: the engine wrote that row into the staging rows), allocates
+ * anew for a recovered source without a pre-allocated symbol (skipped when that fails, :222-226), and
+ * frees the pre-allocated symbols of sources left unrecovered -- the block ends as fec_recover_finish
+ * leaves it.  Returns 0 (rlc_fec_scheme_gf256.c:250). */
+int fec_recover_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t maxl, pquic_source_symbol_t **pre);
+protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, uint8_t status, const uint64_t rec[2],
+                                     pquic_source_symbol_t **pre, const uint64_t copy[2], const uint8_t *src_rows,
+                                     uint32_t stride, uint16_t maxl);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus

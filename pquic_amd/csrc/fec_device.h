@@ -3,11 +3,12 @@
 //   * TinyMT32 coefficient streams, bit-exact with plugins/fec/prng/tinymt32.c:60-161,301-315
 //     and get_coefs (rlc_fec_scheme_generate_gf256.c:9-17).
 //   * GF(2^8)/0x11D scalar arithmetic (gf256/swif_symbol.c:16-29) for the elimination.
-//   * The packed GF multiply-accumulate used on the data path: a byte-wise product by a
-//     constant c is split over the bit fields x = x[2:0] | x[5:3] << 3 | x[7:6] << 6, and
-//     each field is looked up with one v_perm_b32 in an 8-entry product table held in a
-//     pair of 32-bit registers (c*x[2:0], c*(x[5:3] << 3), c*(x[7:6] << 6)); the three
-//     partial products are XOR-ed in with v_bitop3_b32.  Four bytes per lane per v_perm.
+//   * The packed GF multiply-accumulate of the one-block kernels (k_rlc_encode_lds,
+//     k_rlc_decode_lds, k_block_svc; the batched data path is bit-sliced, bitslice_gen.h): a
+//     byte-wise product by a constant c is split over the bit fields
+//     x = x[2:0] | x[5:3] << 3 | x[7:6] << 6, and each field is looked up with one v_perm_b32 in
+//     an 8-entry product table held in a pair of 32-bit registers (c*x[2:0], c*(x[5:3] << 3),
+//     c*(x[7:6] << 6)); the three partial products are XOR-ed in with v_bitop3_b32.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

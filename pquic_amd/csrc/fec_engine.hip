@@ -1,24 +1,31 @@
 // pquic_amd/csrc/fec_engine.hip -- MI355X (gfx950) FEC engine: kernels + C ABI (include/fecgpu.h).
 //
-// Data path (HBM-bound byte arithmetic, no MFMA):
-//   k_rlc_encode   one wavefront per (FEC block, column chunk).  Lanes own 4-byte words
-//                  of the symbol row; every source word is loaded once (coalesced 256-B
-//                  rows per load instruction) and multiply-accumulated into R_TILE repair
-//                  accumulators held in VGPRs.  Coefficients come from TinyMT32 run in
-//                  lanes 0..R_TILE-1 (seed (fbn << 8) | i), their v_perm product tables
-//                  are staged in LDS and read as wave-uniform broadcasts.
-//   k_rlc_plan     one wavefront per block: replays the reference's fec_recover on the
-//                  coefficients only (repair selection, sort_system, elimination without
-//                  re-pivoting, back substitution) and emits the e x k matrix that maps the
-//                  k received symbols to the e unknowns, plus the dependency pattern used by
-//                  the data-dependent "all-zero unknown" rule.
-//   k_rlc_recover  same shape as encode: e outputs from k gathered inputs, in place.
-//   k_rlc_finalize per block: applies the reference's zero/undetermined propagation.
+// Data path (HBM-bound byte arithmetic over GF(2^8), no MFMA):
+//   k_rlc_encode_bs / _bs2 / _rows   a wave streams a group of blocks (one column chunk of <= 2 KiB
+//                  at a time, a lane owning 32 B of a row).  Each source row is loaded once and
+//                  bit-sliced in registers (three shift-exchange rounds -> 8 bit planes), its
+//                  Four-Russians XOR combinations are built once, and every coefficient then costs
+//                  one 3-input XOR per output plane, dispatched by the wave-uniform coefficient
+//                  through a chain of generated case blocks (bitslice_gen.h, from gen_bitslice.py).
+//                  Coefficients come from TinyMT32 run per (block, repair) in the group setup (seed
+//                  (fbn << 8) | i) and wait in LDS as 16-bit case offsets.  Sources wait in VGPRs
+//                  (register prefetch, tiles of 1-8 repairs) or in a per-wave LDS ring fed by LDS-DMA
+//                  (16-repair tiles).
+//   k_rlc_plan*    the decode plan: replays the reference's fec_recover on the coefficients only
+//                  (repair selection, sort_system, elimination without re-pivoting, back
+//                  substitution) and emits the e x k matrix that maps the k received symbols to the e
+//                  unknowns, plus the dependency pattern of the "all-zero unknown" rule.
+//   k_rlc_recover_bs / _bs2   the data pass of decode: the encode's bodies with the plan's rows as
+//                  coefficients and the inputs gathered by the plan's slot map (or row tables); the
+//                  zero/undetermined rule fused for e <= 16, k_rlc_finalize beyond.
+//   k_rlc_encode_lds / k_rlc_decode_lds / k_block_svc   one block per workgroup (the synchronous hooks):
+//                  rows staged in LDS, a packed v_perm multiply (fec_device.h gf_mac) per dword.
 //   k_xor_*        XOR scheme, streaming 16-B lanes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 #include <atomic>
 #include <mutex>
 #include <stdlib.h>
@@ -1464,7 +1471,9 @@ __device__ __forceinline__ uint64_t rec_row(uint64_t b, int k, int j, int dst_ro
 }
 
 // One group of the recover data pass (group q of NG, blocks b0, b0 + bstep, ...); every lane of the
-// wave calls it.  k_rlc_recover_bs runs it over a grid-stride loop; k_rlc_decode_small after the
+// wave calls it.  dst_rows < 0: row tables (fecgpu_rlc_decode_rows) -- src and rep are the [block][k]
+// source-row and [block][r] repair-row device-address tables, and a missing source's entry is the row
+// its recovered bytes go to.  k_rlc_recover_bs runs it over a grid-stride loop; k_rlc_decode_small after the
 // wave plan of the group's block.
 template <int RT, int VEC>
 __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_t *__restrict__ src,
@@ -1541,9 +1550,14 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
         row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD(h[WL.off_D + (r0 + u) * k + j], u) : (uint16_t)0;
       const uint32_t sl = h[WL.off_slot + j];
 #endif
-      const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
-                                     : src + (b * (uint64_t)k + sl) * (uint64_t)L;
-      S.intab[x] = (uint64_t)(uintptr_t)p;
+      if (dst_rows < 0) {  // row tables: src / rep hold the rows' device addresses ([block][k] / [block][r])
+        S.intab[x] = (sl & 0x80) ? reinterpret_cast<const uint64_t *>(rep)[b * (uint64_t)r + (sl & 0x7f)]
+                                 : reinterpret_cast<const uint64_t *>(src)[b * (uint64_t)k + sl];
+      } else {
+        const uint8_t *p = (sl & 0x80) ? rep + (b * (uint64_t)r + (sl & 0x7f)) * (uint64_t)L
+                                       : src + (b * (uint64_t)k + sl) * (uint64_t)L;
+        S.intab[x] = (uint64_t)(uintptr_t)p;
+      }
     }
     // records: output addresses, rt, flags; for the fused finalize the dependency masks
     for (int x = lane; x < nact * 16; x += 64) {
@@ -1559,7 +1573,9 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
 #else
         const int j = h[WL.off_unk + r0 + u];
 #endif
-        reinterpret_cast<uint64_t *>(rc)[u] = (uint64_t)(uintptr_t)(dst + rec_row(b, k, j, dst_rows, r0 + u) * (uint64_t)L);
+        reinterpret_cast<uint64_t *>(rc)[u] =
+            dst_rows < 0 ? reinterpret_cast<const uint64_t *>(src)[b * (uint64_t)k + j]  // the missing source's row
+                         : (uint64_t)(uintptr_t)(dst + rec_row(b, k, j, dst_rows, r0 + u) * (uint64_t)L);
         if (status) {
           uint32_t m = 0;
 #ifndef FEC_PROBE_NOWS
@@ -3311,6 +3327,38 @@ int fecgpu_rlc_decode_apply_packed(const void *src, const void *rep, void *dst, 
                            workspace_bytes, (hipStream_t)stream, em ? (int)em : 1);
 }
 
+int fecgpu_rlc_decode_rows(const uint64_t *src_rows, const uint64_t *rep_rows, uint64_t nblocks, uint32_t k,
+                           uint32_t r, uint32_t symbol_size, const uint32_t *rep_seed, const uint64_t *src_present,
+                           const uint64_t *rep_present, uint8_t *status, uint64_t *recovered, void *workspace,
+                           size_t workspace_bytes, void *stream) {
+  int rc = decode_args(src_rows, rep_rows, nblocks, k, r, symbol_size, src_present, rep_present, status, recovered,
+                       workspace, workspace_bytes);
+  if (rc || nblocks == 0) return rc;
+  if (r && !rep_seed) return set_err(FECGPU_ERR_INVALID, "%s", "NULL rep_seed");
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = decode_plan_impl(nblocks, k, r, 0, nullptr, rep_seed, src_present, rep_present, workspace,
+                             workspace_bytes, s)))
+    return rc;
+  g_stats[2]++;
+  g_stats[3] += nblocks;
+  uint8_t *ws = (uint8_t *)workspace;
+  const WsLayout WL = ws_layout(k, r);
+  if (r == 0) return launch_finalize(nblocks, k, r, status, recovered, ws, s);
+  if (int rc2 = bs_table_check()) return rc2;
+  const int rt = WL.em <= 1 ? 1 : WL.em <= 2 ? 2 : WL.em <= 4 ? 4 : WL.em <= 8 ? 8 : 16;
+  const BsCfg cfg = pick_bs_cfg((int)symbol_size);
+  const bool fused = (int)WL.em <= rt;
+  // the register-prefetch recover pass for every tile size (the LDS-ring pass computes its row
+  // addresses from packed buffers); dst_rows = -1 selects the row tables
+  for (int r0 = 0; r0 < (int)WL.em; r0 += rt) {
+    FEC_BS_DISPATCH(launch_recover_bs, (uint8_t *)src_rows, (const uint8_t *)rep_rows, nblocks, (int)k, (int)r,
+                    (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
+                    (uint8_t *)nullptr, -1)
+  }
+  HIPCHK(hipGetLastError());
+  return fused ? FECGPU_OK : launch_finalize(nblocks, k, r, status, recovered, ws, s);
+}
+
 extern "C++" {
 template <int RT, int VEC>
 static void launch_decode_small(uint8_t *src, const uint8_t *rep, uint64_t nb, int k, int r, int L, const BsCfg &c,
@@ -3495,8 +3543,20 @@ struct fecgpu_block_svc {
   BlockSvcMailbox *mb_dev = nullptr;
   uint64_t seq = 0;
   bool launched = false;
+  uint64_t deadline_us = 2000;      // a request not served by then is withdrawn (svc_withdraw)
+  uint64_t backoff_until = 0;       // after a withdrawal the calls take the launch path until then (us)
+  uint64_t misses = 0;              // requests withdrawn at the deadline
   std::mutex mu;
 };
+
+static uint64_t svc_now_us() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+// after a withdrawn request the hooks use the launch path for this long: a worker that was not
+// scheduled within the deadline is most likely queued behind a long kernel, and so would the next be
+constexpr uint64_t kSvcBackoffUs = 50000;
 
 // worker lifetime: ends after 20 ms without a request (the next call relaunches it) and after 2 s
 // in all, so no launch outlives its caller by more than that (s_memrealtime: 100 MHz)
@@ -3545,6 +3605,7 @@ void fecgpu_block_svc_destroy(fecgpu_block_svc_t *v) {
 static int svc_ensure(fecgpu_block_svc_t *v) {
   if (v->launched && hipEventQuery(v->ev) == hipErrorNotReady) return FECGPU_OK;
   (void)hipGetLastError();
+  __atomic_store_n(&v->mb->quit, 0ull, __ATOMIC_RELEASE);  // a withdrawal ended the last worker with it
   hipLaunchKernelGGL(k_block_svc, dim3(1), dim3(kLdsThreads), kSvcLds, v->stream, v->mb_dev, kSvcIdleTicks,
                      kSvcLifeTicks);
   HIPCHK(hipGetLastError());
@@ -3553,21 +3614,57 @@ static int svc_ensure(fecgpu_block_svc_t *v) {
   return FECGPU_OK;
 }
 
-// Posts the request already written into the mailbox and waits for its completion.
+// Takes back request `seq` (posted, not served): no worker may serve it later, when its rows are
+// the caller's again.  The request number goes back to the last one served, so a worker started
+// later sees nothing pending.
+static void svc_unpost(fecgpu_block_svc_t *v, uint64_t seq) {
+  __atomic_store_n(&v->mb->req.seq, seq - 1, __ATOMIC_RELEASE);
+  v->seq = seq - 1;
+}
+
+// The deadline passed with request `seq` unserved: the worker is told to end and is waited for (a
+// worker serves a posted request before it looks at the quit flag, so once it has ended the request
+// is either done or was never seen), then the request is taken back if nobody served it.  Returns OK
+// when it was served after all, else FECGPU_ERR_INVALID: the caller runs the block through the launch
+// path, as for a block the service does not take.  The next calls skip the service for a while.
+static int svc_withdraw(fecgpu_block_svc_t *v, uint64_t seq) {
+  __atomic_store_n(&v->mb->quit, 1ull, __ATOMIC_RELEASE);
+  const hipError_t e = hipEventSynchronize(v->ev);
+  v->misses++;
+  v->backoff_until = svc_now_us() + kSvcBackoffUs;
+  if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+  svc_unpost(v, seq);
+  if (e != hipSuccess) return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(e));
+  return set_err(FECGPU_ERR_INVALID, "%s", "block service: deadline passed, request withdrawn");
+}
+
+// Posts the request already written into the mailbox and waits for its completion, at most
+// v->deadline_us before it is withdrawn (svc_withdraw).  The request number is posted only once a
+// worker is running or launched, and taken back on every error return.
 static int svc_run(fecgpu_block_svc_t *v) {
-  const uint64_t seq = ++v->seq;
-  __atomic_store_n(&v->mb->req.seq, seq, __ATOMIC_RELEASE);
+  const uint64_t t0 = svc_now_us();
+  if (t0 < v->backoff_until) return FECGPU_ERR_INVALID;  // a recent withdrawal: the launch path for now
   if (int rc = svc_ensure(v)) return rc;
+  const uint64_t seq = v->seq + 1;
+  v->seq = seq;
+  __atomic_store_n(&v->mb->req.seq, seq, __ATOMIC_RELEASE);
   for (uint64_t spin = 1;; spin++) {
     if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
     __builtin_ia32_pause();
+    if ((spin & 255) == 0 && svc_now_us() - t0 > v->deadline_us) return svc_withdraw(v, seq);
     if ((spin & 1023) == 0) {
       const hipError_t q = hipEventQuery(v->ev);
       if (q == hipErrorNotReady) continue;
-      if (q != hipSuccess) return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(q));
+      if (q != hipSuccess) {
+        svc_unpost(v, seq);
+        return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(q));
+      }
       // the worker ended (idle limit reached as the request was posted): the next one serves it
       if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
-      if (int rc = svc_ensure(v)) return rc;
+      if (int rc = svc_ensure(v)) {
+        svc_unpost(v, seq);
+        return rc;
+      }
     }
   }
 }
@@ -3643,6 +3740,20 @@ int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *v, const void *src, c
 
 uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *v) {
   return v && v->mb ? __atomic_load_n(&v->mb->launches, __ATOMIC_ACQUIRE) : 0;
+}
+
+int fecgpu_block_svc_set_deadline(fecgpu_block_svc_t *v, uint64_t deadline_us) {
+  if (!v) return FECGPU_ERR_INVALID;
+  std::lock_guard<std::mutex> g(v->mu);
+  v->deadline_us = deadline_us;
+  v->backoff_until = 0;
+  return FECGPU_OK;
+}
+
+uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *v) {
+  if (!v) return 0;
+  std::lock_guard<std::mutex> g(v->mu);
+  return v->misses;
 }
 
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream) {

@@ -424,6 +424,55 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *c, void *src, const void *r
   return decode_host(c, false, src, rep, nblocks, k, r, L, 0, nullptr, rep_seed, sp, rp, status, recovered);
 }
 
+int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, const uint64_t *rep_rows,
+                                uint64_t nblocks, uint32_t k, uint32_t r, uint32_t L, const uint32_t *seeds,
+                                const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
+  if (!c || !src_rows || !rep_rows || !sp || !rp || !status || !recovered || (r && !seeds)) return FECGPU_ERR_INVALID;
+  if (!nblocks) return FECGPU_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HCHK(hipSetDevice(c->device));
+  Slot &s = c->slot[0];
+  const uint32_t nseed = r ? r : 1;
+  // every array page-locked (the batching adapter's job tables): the kernels use them in place
+  const uint64_t *ds = (const uint64_t *)mapped_host(src_rows, nblocks * k * 8);
+  const uint64_t *dr = ds ? (const uint64_t *)mapped_host(rep_rows, nblocks * nseed * 8) : nullptr;
+  const uint32_t *dseed = dr ? (const uint32_t *)mapped_host(seeds, nblocks * nseed * 4) : nullptr;
+  const uint64_t *dsp = dseed ? (const uint64_t *)mapped_host(sp, nblocks * 16) : nullptr;
+  const uint64_t *drp = dsp ? (const uint64_t *)mapped_host(rp, nblocks * 16) : nullptr;
+  uint8_t *dst = drp ? mapped_host(status, nblocks) : nullptr;
+  uint64_t *drec = dst ? (uint64_t *)mapped_host(recovered, nblocks * 16) : nullptr;
+  int rc = FECGPU_OK;
+  do {
+    const size_t wsb = fecgpu_rlc_decode_workspace(nblocks, k, r);
+    LCHK(grow(&s.d_ws, &s.cap_ws, wsb));
+    if (!drec) {  // pageable: one device copy of the tables and masks, status and masks copied back
+      const size_t tb = nblocks * (k + nseed) * 8, sdb = (nblocks * nseed * 4 + 15) & ~(size_t)15;
+      LCHK(grow(&s.d_aux, &s.cap_aux, tb + sdb + nblocks * 48 + nblocks));
+      uint8_t *a = (uint8_t *)s.d_aux;
+      ds = (const uint64_t *)a;
+      dr = (const uint64_t *)(a + nblocks * k * 8);
+      dseed = (const uint32_t *)(a + tb);
+      uint64_t *m = (uint64_t *)(a + tb + sdb);
+      dsp = m;
+      drp = m + 2 * nblocks;
+      drec = m + 4 * nblocks;
+      dst = (uint8_t *)(m + 6 * nblocks);
+      LCHK(hipMemcpyAsync((void *)ds, src_rows, nblocks * k * 8, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync((void *)dr, rep_rows, nblocks * nseed * 8, hipMemcpyHostToDevice, s.st));
+      if (r) LCHK(hipMemcpyAsync((void *)dseed, seeds, nblocks * r * 4, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync((void *)dsp, sp, nblocks * 16, hipMemcpyHostToDevice, s.st));
+      LCHK(hipMemcpyAsync((void *)drp, rp, nblocks * 16, hipMemcpyHostToDevice, s.st));
+      if ((rc = fecgpu_rlc_decode_rows(ds, dr, nblocks, k, r, L, dseed, dsp, drp, dst, drec, s.d_ws, s.cap_ws, s.st)))
+        break;
+      LCHK(hipMemcpyAsync(status, dst, nblocks, hipMemcpyDeviceToHost, s.st));
+      LCHK(hipMemcpyAsync(recovered, drec, nblocks * 16, hipMemcpyDeviceToHost, s.st));
+      break;
+    }
+    rc = fecgpu_rlc_decode_rows(ds, dr, nblocks, k, r, L, dseed, dsp, drp, dst, drec, s.d_ws, s.cap_ws, s.st);
+  } while (0);
+  return finish(c, rc);
+}
+
 int fecgpu_xor_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uint64_t nblocks, uint32_t k,
                            uint32_t L, const uint64_t *sp, const uint64_t *rp, uint8_t *status,
                            uint64_t *recovered) {

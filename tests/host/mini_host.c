@@ -21,10 +21,13 @@
 
 #include "pquic_fec_protoops.h"
 
+struct mh_arena;
+
 struct st_picoquic_cnx_t {
     protoop_arg_t inputv[16];
     protoop_arg_t outputv[16];
     int inputc, outputc;
+    struct mh_arena *arena;  /* the connection's plugin memory (NULL: the default arena, if any) */
 };
 
 static long g_live;
@@ -46,45 +49,84 @@ static long g_fail_after = -1;  /* allocation-failure injection: the n-th alloca
 
 void mh_fail_alloc_after(long n) { g_fail_after = n; }
 
-/* Optional plugin-style memory arena (picoquic_internal.h:576 memory[PLUGIN_MEMORY], carved into
- * 2100-B slots, picoquic/memory.c:181-191): allocations up to 2092 B come from it, so the batching
- * adapter can be given the arena (mh_batch_register_arena) and gather rows in place. */
+/* Plugin-style memory arenas (picoquic_internal.h:576 memory[PLUGIN_MEMORY], carved into 2100-B
+ * slots, picoquic/memory.c:181-191): allocations up to 2092 B come from the arena of the connection
+ * that asks (every connection owns its plugin instances and their memory, plugin.c:835, 946-950), or
+ * from the default arena (mh_arena_enable) for connections without one; a full arena falls back to the
+ * heap, as a plugin with dynamic_memory would (plugin.c:409-424).  The batching adapter can be given
+ * the arenas (pquic_fec_batch_register_heap) and gather rows in place. */
 enum { MH_SLOT = 2112 };
-static uint8_t *g_arena;
-static size_t g_arena_size, g_arena_used;
-static void *g_arena_free;
+typedef struct mh_arena {
+    uint8_t *base;
+    size_t size, used;
+    void *free_list;
+    long live;
+} mh_arena_t;
+static mh_arena_t **g_arenas;  /* every arena made, for frees (a symbol outlives nothing but its arena) */
+static int g_narenas, g_arenas_cap;
+static mh_arena_t *g_default_arena;
 
-int mh_arena_enable(size_t bytes) {
-    if (g_arena) return 0;
-    g_arena_size = (bytes + 4095) & ~(size_t)4095;
-    void *p = mmap(NULL, g_arena_size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (p == MAP_FAILED) return -1;
-    g_arena = p;
-    g_arena_used = 0;
-    g_arena_free = NULL;
-    return 0;
+static mh_arena_t *arena_new(size_t bytes) {
+    mh_arena_t *a = calloc(1, sizeof *a);
+    if (!a) return NULL;
+    a->size = (bytes + 4095) & ~(size_t)4095;
+    void *p = mmap(NULL, a->size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) {
+        free(a);
+        return NULL;
+    }
+    a->base = p;
+    if (g_narenas == g_arenas_cap) {
+        g_arenas_cap = g_arenas_cap ? 2 * g_arenas_cap : 64;
+        g_arenas = realloc(g_arenas, sizeof *g_arenas * (size_t)g_arenas_cap);
+    }
+    g_arenas[g_narenas++] = a;
+    return a;
 }
 
-static int in_arena(const void *p) {
-    return g_arena && (uintptr_t)p - (uintptr_t)g_arena < g_arena_size;
+static void arena_drop(mh_arena_t *a) {  /* an arena nothing lives in any more */
+    for (int i = 0; i < g_narenas; i++)
+        if (g_arenas[i] == a) {
+            g_arenas[i] = g_arenas[--g_narenas];
+            break;
+        }
+    munmap(a->base, a->size);
+    free(a);
+}
+
+/* A fresh default arena of `bytes` (the previous one is dropped once nothing lives in it). */
+int mh_arena_enable(size_t bytes) {
+    mh_arena_t *old = g_default_arena;
+    g_default_arena = arena_new(bytes);
+    if (old && !old->live) arena_drop(old);
+    return g_default_arena ? 0 : -1;
+}
+
+static mh_arena_t *arena_of(picoquic_cnx_t *cnx, const void *p) {
+    const uintptr_t a = (uintptr_t)p;
+    if (cnx && cnx->arena && a - (uintptr_t)cnx->arena->base < cnx->arena->size) return cnx->arena;
+    for (int i = 0; i < g_narenas; i++)
+        if (a - (uintptr_t)g_arenas[i]->base < g_arenas[i]->size) return g_arenas[i];
+    return NULL;
 }
 
 static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
-    (void)cnx;
     if (g_fail_after == 0) {
         g_fail_after = -1;
         return NULL;
     }
     if (g_fail_after > 0) g_fail_after--;
     void *p = NULL;
-    if (g_arena && size <= 2092) {
-        if (g_arena_free) {
-            p = g_arena_free;
-            g_arena_free = *(void **)p;
-        } else if (g_arena_used + MH_SLOT <= g_arena_size) {
-            p = g_arena + g_arena_used;
-            g_arena_used += MH_SLOT;
+    mh_arena_t *ar = cnx && cnx->arena ? cnx->arena : g_default_arena;
+    if (ar && size <= 2092) {
+        if (ar->free_list) {
+            p = ar->free_list;
+            ar->free_list = *(void **)p;
+        } else if (ar->used + MH_SLOT <= ar->size) {
+            p = ar->base + ar->used;
+            ar->used += MH_SLOT;
         }
+        if (p) ar->live++;
     }
     if (!p) p = malloc(size <= 2092 ? 2100 : size);
     if (p) g_live++;
@@ -92,12 +134,13 @@ static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
 }
 
 static void mh_free(picoquic_cnx_t *cnx, void *p) {
-    (void)cnx;
     if (!p) return;
     g_live--;
-    if (in_arena(p)) {
-        *(void **)p = g_arena_free;
-        g_arena_free = p;
+    mh_arena_t *ar = arena_of(cnx, p);
+    if (ar) {
+        *(void **)p = ar->free_list;
+        ar->free_list = p;
+        ar->live--;
     } else {
         free(p);
     }
@@ -154,19 +197,23 @@ static op_t op_create(int xor_scheme) {
     return xor_scheme ? pquic_fec_xor_create_fec_schemes : pquic_fec_rlc_create_fec_schemes;
 }
 
-static pquic_source_symbol_t *mk_source(uint32_t fbn, int j, const uint8_t *data, uint16_t len) {
-    picoquic_cnx_t c;
-    pquic_source_symbol_t *s = mh_malloc(&c, sizeof *s);
+static pquic_source_symbol_t *mk_source_in(picoquic_cnx_t *c, uint32_t fbn, int j, const uint8_t *data, uint16_t len) {
+    pquic_source_symbol_t *s = mh_malloc(c, sizeof *s);
     memset(s, 0, sizeof *s);
     s->fpid.raw = (fbn << 8) | (uint32_t)j;
-    s->data = mh_malloc(&c, len);
+    s->data = mh_malloc(c, len);
     memcpy(s->data, data, len);
     s->data_length = len;
     return s;
 }
 
+static pquic_source_symbol_t *mk_source(uint32_t fbn, int j, const uint8_t *data, uint16_t len) {
+    picoquic_cnx_t c = {0};
+    return mk_source_in(&c, fbn, j, data, len);
+}
+
 static void free_block(pquic_fec_block_t *fb) {
-    picoquic_cnx_t c;
+    picoquic_cnx_t c = {0};
     for (int j = 0; j < PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK; j++) {
         if (fb->source_symbols[j]) { mh_free(&c, fb->source_symbols[j]->data); mh_free(&c, fb->source_symbols[j]); }
         if (fb->repair_symbols[j]) { mh_free(&c, fb->repair_symbols[j]->data); mh_free(&c, fb->repair_symbols[j]); }
@@ -320,6 +367,7 @@ typedef struct {
     pquic_fec_block_t *fb;
     pquic_source_symbol_t *before[PQUIC_FEC_MAX_SYMBOLS_PER_BLOCK];
     long ret;
+    long order;  /* position among all completions */
     int done, calls, k, r;
     int shared;  /* window block: its source symbols belong to a stream */
 } ticket_t;
@@ -328,6 +376,36 @@ static pquic_fec_batcher_t *g_batcher;
 static ticket_t *g_tickets;
 static long g_nt, g_capt;
 static picoquic_cnx_t g_bcnx;
+static long g_ndone;
+/* connections with arenas of their own (mh_batch_connections); mh_batch_use_connection picks the one
+ * the next blocks are built and submitted on (-1: g_bcnx, the default arena) */
+static picoquic_cnx_t *g_cnxs;
+static int g_ncnx;
+static picoquic_cnx_t *g_cur = &g_bcnx;
+
+/* n connections, each with an arena of `bytes` registered with the open batcher */
+int mh_batch_connections(int n, size_t bytes) {
+    g_cnxs = calloc((size_t)n, sizeof *g_cnxs);
+    if (!g_cnxs) return -1;
+    for (int i = 0; i < n; i++) {
+        if (!(g_cnxs[i].arena = arena_new(bytes))) return -1;
+        g_ncnx = i + 1;
+        if (pquic_fec_batch_register_heap(g_batcher, g_cnxs[i].arena->base, g_cnxs[i].arena->size)) return -1;
+    }
+    return 0;
+}
+
+int mh_batch_use_connection(int i) {
+    if (i >= g_ncnx) return -1;
+    g_cur = i < 0 ? &g_bcnx : &g_cnxs[i];
+    return 0;
+}
+
+/* arena slots in use of connection i (-1: the default arena) */
+long mh_arena_live(int i) {
+    const mh_arena_t *a = i < 0 ? g_default_arena : (i < g_ncnx ? g_cnxs[i].arena : NULL);
+    return a ? a->live : -1;
+}
 
 static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     ticket_t *t = &g_tickets[(long)(intptr_t)user];
@@ -335,7 +413,11 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     t->ret = (long)ret;
     t->done = 1;
     t->calls++;
+    t->order = g_ndone++;
 }
+
+/* completion position of ticket t (-1 before its completion) */
+long mh_batch_order(long t) { return g_tickets[t].done ? g_tickets[t].order : -1; }
 
 int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsigned max_symbol, int nstreams,
                   unsigned poll_blocks) {
@@ -344,9 +426,9 @@ int mh_batch_open(int device, unsigned batch_blocks, unsigned max_delay_us, unsi
     return g_batcher ? 0 : -1;
 }
 
-/* registers the arena (mh_arena_enable) with the open batcher */
+/* registers the default arena (mh_arena_enable) with the open batcher */
 int mh_batch_register_arena(void) {
-    return g_arena ? pquic_fec_batch_register_heap(g_batcher, g_arena, g_arena_size) : -1;
+    return g_default_arena ? pquic_fec_batch_register_heap(g_batcher, g_default_arena->base, g_default_arena->size) : -1;
 }
 
 static long new_ticket(pquic_fec_block_t *fb, int k, int r) {
@@ -367,14 +449,14 @@ long mh_batch_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t
                        int src_stride, uint64_t now_us) {
     pquic_fec_block_t *fb = calloc(1, sizeof *fb);
     fb->fec_block_number = fbn;
-    for (int j = 0; j < k; j++) fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+    for (int j = 0; j < k; j++) fb->source_symbols[j] = mk_source_in(g_cur, fbn, j, src + (size_t)j * src_stride, src_len[j]);
     fb->current_source_symbols = (uint8_t)k;
     fb->total_source_symbols = (uint8_t)k;
     fb->total_repair_symbols = (uint8_t)r;
     long t = new_ticket(fb, k, r);
     g_fail_after = g_fail_next_op;  /* armed from here on: the caller disarms after the completion */
     g_fail_next_op = -1;
-    if (pquic_fec_batch_generate(g_batcher, &g_bcnx, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
+    if (pquic_fec_batch_generate(g_batcher, g_cur, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
         free_block(fb);
         g_nt--;
         return -1;
@@ -385,22 +467,22 @@ long mh_batch_generate(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t
 long mh_batch_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t *src, const uint16_t *src_len,
                       const uint8_t *src_present, int src_stride, const uint8_t *rep, const uint16_t *rep_len,
                       const uint8_t *rep_present, const uint64_t *rep_fpid, int rep_stride, uint64_t now_us) {
-    picoquic_cnx_t c;
+    picoquic_cnx_t *c = g_cur;
     pquic_fec_block_t *fb = calloc(1, sizeof *fb);
     fb->fec_block_number = fbn;
     fb->total_source_symbols = (uint8_t)k;
     fb->total_repair_symbols = (uint8_t)r;
     for (int j = 0; j < k; j++)
         if (src_present[j]) {
-            fb->source_symbols[j] = mk_source(fbn, j, src + (size_t)j * src_stride, src_len[j]);
+            fb->source_symbols[j] = mk_source_in(c, fbn, j, src + (size_t)j * src_stride, src_len[j]);
             fb->current_source_symbols++;
         }
     for (int i = 0; i < r; i++)
         if (rep_present[i]) {
-            pquic_repair_symbol_t *rs = mh_malloc(&c, sizeof *rs);
+            pquic_repair_symbol_t *rs = mh_malloc(c, sizeof *rs);
             memset(rs, 0, sizeof *rs);
             rs->fpid.raw = rep_fpid[i];
-            rs->data = mh_malloc(&c, rep_len[i]);
+            rs->data = mh_malloc(c, rep_len[i]);
             memcpy(rs->data, rep + (size_t)i * rep_stride, rep_len[i]);
             rs->data_length = rep_len[i];
             fb->repair_symbols[i] = rs;
@@ -408,7 +490,7 @@ long mh_batch_recover(int xor_scheme, uint32_t fbn, int k, int r, const uint8_t 
         }
     long t = new_ticket(fb, k, r);
     memcpy(g_tickets[t].before, fb->source_symbols, sizeof g_tickets[t].before);
-    if (pquic_fec_batch_recover(g_batcher, &g_bcnx, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
+    if (pquic_fec_batch_recover(g_batcher, c, fb, xor_scheme, now_us, on_done, (void *)(intptr_t)t)) {
         free_block(fb);
         g_nt--;
         return -1;
@@ -491,12 +573,12 @@ void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recove
     *cur_ss = tk->fb->current_source_symbols;
 }
 
-void mh_batch_get_stats(uint64_t out[10]) {
+void mh_batch_get_stats(uint64_t out[12]) {
     pquic_fec_batch_stats_t s;
     pquic_fec_batch_get_stats(g_batcher, &s);
     out[0] = s.submitted; out[1] = s.completed; out[2] = s.batches; out[3] = s.flushed_full;
     out[4] = s.flushed_deadline; out[5] = s.flushed_drain; out[6] = s.immediate; out[7] = s.engine_errors;
-    out[8] = s.windows; out[9] = s.window_rows;
+    out[8] = s.windows; out[9] = s.window_rows; out[10] = s.rows_in_place; out[11] = s.rows_staged;
 }
 
 /* frees every ticket's block and the batcher */
@@ -507,7 +589,7 @@ void mh_batch_close(void) {
         if (g_tickets[t].shared) memset(g_tickets[t].fb->source_symbols, 0, sizeof g_tickets[t].fb->source_symbols);
         free_block(g_tickets[t].fb);
     }
-    picoquic_cnx_t c;
+    picoquic_cnx_t c = {0};
     for (int i = 0; i < g_nstreams; i++) {
         for (int x = 0; x < g_stream_len[i]; x++) { mh_free(&c, g_stream[i][x]->data); mh_free(&c, g_stream[i][x]); }
         free(g_stream[i]);
@@ -517,6 +599,13 @@ void mh_batch_close(void) {
     free(g_tickets);
     g_tickets = NULL;
     g_nt = g_capt = 0;
+    g_ndone = 0;
+    for (int i = 0; i < g_ncnx; i++)  /* the batcher unregistered them; nothing lives in them any more */
+        if (g_cnxs[i].arena && !g_cnxs[i].arena->live) arena_drop(g_cnxs[i].arena);
+    free(g_cnxs);
+    g_cnxs = NULL;
+    g_ncnx = 0;
+    g_cur = &g_bcnx;
 }
 
 /* ------------------------------------------------------------------------------------------

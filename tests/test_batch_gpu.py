@@ -24,7 +24,8 @@ def _p(a, t=C.c_uint8):
 
 
 class Batch:
-    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2, arena=False, poll_blocks=0):
+    def __init__(self, batch_blocks, max_delay_us=1000, max_symbol=9000, nstreams=2, arena=False, poll_blocks=0,
+                 arena_bytes=256 << 20, connections=0, conn_bytes=1 << 20):
         L = C.CDLL(MINIHOST)
         L.mh_arena_enable.argtypes = [C.c_size_t]
         for f in ("mh_batch_generate", "mh_batch_recover", "mh_batch_status", "mh_live_allocations"):
@@ -41,16 +42,27 @@ class Batch:
         L.mh_stream_open.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
         L.mh_batch_generate_window.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
         L.mh_batch_generate_window.restype = C.c_long
+        L.mh_batch_connections.argtypes = [C.c_int, C.c_size_t]
+        L.mh_batch_order.argtypes = [C.c_long]
+        L.mh_batch_order.restype = C.c_long
+        L.mh_arena_live.argtypes = [C.c_int]
+        L.mh_arena_live.restype = C.c_long
         self.L = L
         self.stream_stride = {}
         assert L.mh_bind(0) == 0
         self.base = L.mh_live_allocations()
         if arena:  # symbols in a plugin-style arena the batcher gathers rows from (registered heap)
-            assert L.mh_arena_enable(256 << 20) == 0
+            assert L.mh_arena_enable(arena_bytes) == 0
         assert L.mh_batch_open(0, batch_blocks, max_delay_us, max_symbol, nstreams, poll_blocks) == 0
         if arena:
             assert L.mh_batch_register_arena() == 0
+        if connections:  # connections with arenas of their own, each registered (one per plugin instance)
+            assert L.mh_batch_connections(connections, conn_bytes) == 0
         self.meta = {}
+
+    def use(self, conn):
+        """Build and submit the next blocks on connection `conn` (-1: the default one)."""
+        assert self.L.mh_batch_use_connection(conn) == 0
 
     def generate(self, xor, fbn, srcs, r, now=0):
         k = len(srcs)
@@ -136,10 +148,10 @@ class Batch:
         return {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}, cur.value
 
     def stats(self):
-        s = (C.c_uint64 * 10)()
+        s = (C.c_uint64 * 12)()
         self.L.mh_batch_get_stats(s)
         keys = ["submitted", "completed", "batches", "flushed_full", "flushed_deadline", "flushed_drain",
-                "immediate", "engine_errors", "windows", "window_rows"]
+                "immediate", "engine_errors", "windows", "window_rows", "rows_in_place", "rows_staged"]
         return dict(zip(keys, list(s)))
 
     def close(self):
@@ -518,4 +530,141 @@ def test_batch_window_generate_fixtures():
         rec, _ = bt.recovered(t)
         assert {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())} == case["recovered"], case["tag"]
     assert bt.stats()["windows"] == len(jobs)
+    bt.close()
+
+
+def test_batch_generate_arena_full_part_way_through_a_block():
+    """A block whose repair symbols are split between the registered arena and other memory (the
+    arena fills up part way through the block's allocations): the repairs written in place keep
+    their bytes and the staged ones are copied out (advisor finding, round 3: the copy-out used to
+    overwrite the in-place rows with stale staging bytes)."""
+    # 13 slots: the first block's 4 sources (8 slots), repairs 0-1 (4 slots) and repair 2's struct;
+    # repair 2's data and repair 3 come from the heap, as do the later blocks
+    bt = Batch(4, max_symbol=1200, arena=True, arena_bytes=13 * 2112)
+    rng = np.random.default_rng(11)
+    o = Oracle()
+    jobs = []
+    for b in range(3):
+        srcs = [rng.integers(0, 256, 1200, dtype=np.uint8) for _ in range(4)]
+        fbn = int(rng.integers(0, 1 << 24))
+        rep = o.rlc_encode_batch(np.stack(srcs)[None], 4, fbn)[0]
+        jobs.append((False, fbn, srcs, 4, ("hex", [x.tobytes().hex() for x in rep]),
+                     [(fbn << 8) | i for i in range(4)], 0))
+    tickets = [bt.generate(*j[:4], now=i) for i, j in enumerate(jobs)]
+    bt.L.mh_batch_drain()
+    for t, j in zip(tickets, jobs):
+        _check_generate(bt, t, j)
+    st = bt.stats()
+    assert st["engine_errors"] == 0
+    assert st["rows_in_place"] == 4 + 2 and st["rows_staged"] > 0
+    bt.close()
+
+
+def _random_recover_jobs(rng, n, L, kmax=32, rmax=8):
+    """RLC blocks of L-byte symbols with up to r random erasures, all repairs present, with the
+    oracle's expected recovery (status, {j: bytes})."""
+    o = Oracle()
+    jobs = []
+    for _ in range(n):
+        k, r = int(rng.integers(2, kmax + 1)), int(rng.integers(1, rmax + 1))
+        fbn = int(rng.integers(0, 1 << 24))
+        full = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        reps = o.rlc_encode_block(fbn, full, r)[1]
+        e = int(rng.integers(1, min(k, r) + 1))
+        miss = set(int(x) for x in rng.choice(k, e, replace=False))
+        srcs = [None if j in miss else full[j] for j in range(k)]
+        st, rec = o.rlc_decode_block(fbn, srcs, list(reps))
+        jobs.append((fbn, srcs, list(reps), [(fbn << 8) | i for i in range(r)], st, rec))
+    return jobs
+
+
+@pytest.mark.parametrize("batch_blocks", [3, 64])
+def test_batch_recover_gathers_from_connection_arenas(batch_blocks):
+    """RLC recover batches read the received symbols where they lie in the connections' registered
+    arenas (one per connection, as each plugin instance owns its memory) and the kernel writes each
+    recovered source into the symbol allocated for it at submission.  Blocks whose length is not the
+    stride, rows outside an arena and XOR blocks are staged.  Everything against the reference
+    fixtures and the oracle; every symbol freed (pre-allocated symbols of unrecovered sources too)."""
+    ncon = 5
+    bt = Batch(batch_blocks, max_symbol=1200, connections=ncon, conn_bytes=8 << 20)
+    fx = [j for j in _decode_jobs() if max([len(x) for x in j[1] + j[2] if x is not None] + [1]) <= 1200]
+    rng = np.random.default_rng(batch_blocks)
+    rnd = _random_recover_jobs(rng, 120, 1200)
+    tickets = []
+    for i, (case, srcs, reps, fp) in enumerate(fx):
+        bt.use(i % ncon)
+        tickets.append(bt.recover(case["scheme"] == "xor", case["fbn"], srcs, reps, fp, now=i))
+    for i, (fbn, srcs, reps, fp, _, _) in enumerate(rnd):
+        bt.use((i * 3) % ncon)
+        tickets.append(bt.recover(False, fbn, srcs, reps, fp, now=len(fx) + i))
+    bt.L.mh_batch_drain()
+    for t, (case, srcs, _, _) in zip(tickets, fx):
+        ret, calls = bt.status(t)
+        assert calls == 1, case["tag"]
+        rec, cur = bt.recovered(t)
+        if case["crashed"]:
+            assert ret == 0 and rec == {}
+            continue
+        assert ret == case["ret"], case["tag"]
+        assert {str(j): sha(v.tobytes()) for j, v in sorted(rec.items())} == case["recovered"], case["tag"]
+        assert {str(j): len(v) for j, v in rec.items()} == case["recovered_len"]
+        present = sum(s is not None for s in srcs)
+        assert cur == (present + len(rec) if case["scheme"] == "rlc" else present)
+    n_rec = 0
+    for t, (fbn, srcs, _, _, st, want) in zip(tickets[len(fx):], rnd):
+        ret, calls = bt.status(t)
+        assert calls == 1 and ret == 0
+        rec, cur = bt.recovered(t)
+        assert sorted(rec) == sorted(want), fbn
+        for j in rec:
+            assert rec[j].tobytes() == want[j].tobytes(), (fbn, j)
+            assert bt.last_fpids[j] == ((fbn << 8) + j) & 0xFFFFFFFF
+        assert cur == sum(s is not None for s in srcs) + len(rec)
+        n_rec += len(rec)
+    assert n_rec > 100
+    st = bt.stats()
+    assert st["engine_errors"] == 0
+    assert st["rows_in_place"] > 1000, st
+    bt.close()
+
+
+def test_batch_many_connection_arenas():
+    """More than a thousand registered arenas (one per connection): every block's rows are found in
+    its connection's arena (sorted registry, binary search) and coded in place."""
+    ncon = 1100
+    bt = Batch(512, max_symbol=1200, connections=ncon, conn_bytes=64 << 10)
+    rng = np.random.default_rng(5)
+    o = Oracle()
+    jobs = []
+    for c in range(ncon):
+        srcs = [rng.integers(0, 256, 1200, dtype=np.uint8) for _ in range(4)]
+        fbn = int(rng.integers(0, 1 << 24))
+        rep = o.rlc_encode_batch(np.stack(srcs)[None], 2, fbn)[0]
+        jobs.append((False, fbn, srcs, 2, ("hex", [x.tobytes().hex() for x in rep]),
+                     [(fbn << 8) | i for i in range(2)], 0))
+    tickets = []
+    for c, j in enumerate(jobs):
+        bt.use(c)
+        tickets.append(bt.generate(*j[:4], now=c))
+    bt.L.mh_batch_drain()
+    for t, j in zip(tickets, jobs):
+        _check_generate(bt, t, j)
+    st = bt.stats()
+    assert st["engine_errors"] == 0
+    assert st["rows_in_place"] == ncon * (4 + 2) and st["rows_staged"] == 0, st
+    bt.close()
+
+
+def test_batch_completions_follow_submission_order():
+    """Blocks of one queue complete in submission order across batches, although two engine threads
+    (and copy-out passes) can finish batches out of order."""
+    bt = Batch(3, max_symbol=1200)
+    rng = np.random.default_rng(3)
+    tickets = []
+    for i in range(60):
+        srcs = [rng.integers(0, 256, 1200, dtype=np.uint8) for _ in range(8)]
+        tickets.append(bt.generate(False, i, srcs, 4, now=i))
+    bt.L.mh_batch_drain()
+    order = [bt.L.mh_batch_order(t) for t in tickets]
+    assert order == sorted(order) and min(order) >= 0
     bt.close()

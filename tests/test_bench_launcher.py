@@ -70,3 +70,29 @@ def test_single_gpu_dry_run_line():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _line(p.stdout)
     assert d["n_gpus"] == 1 and d["cpu_baseline"] is None
+
+
+def test_launcher_never_opens_the_gpu():
+    """The launcher counts GPUs in a throw-away child process and checks, before it starts the ranks,
+    that it holds no GPU device file (/dev/kfd, /dev/dri/*) itself; without enough GPUs (none here) it
+    exits with code 2 and says how many it saw."""
+    sys.path.insert(0, ROOT)
+    import bench
+    before = bench.gpu_device_fds()
+    n = bench.visible_gpu_count()
+    assert n >= 0
+    assert bench.gpu_device_fds() == before == [], "counting GPUs opened a device file in this process"
+    if n >= 2:
+        pytest.skip("enough GPUs visible for two ranks")
+    p = _run(["--gpus", "2", "--no-cpu"], {"PQUIC_BENCH_SHARE_GPU": "0"})
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert f"--gpus 2 but {n} GPU(s) visible" in p.stderr
+
+
+def test_gpus_default_follows_world_size():
+    """Under a launcher that sets WORLD_SIZE (torchrun --nproc-per-node N bench.py) without --gpus, the
+    rank count is WORLD_SIZE; an explicit --gpus that disagrees is refused (above)."""
+    p = _run(["--dry-run", "--no-cpu", "--steps", "1", "--warmup", "0"],
+             {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert _line(p.stdout)["n_gpus"] == 1

@@ -130,3 +130,36 @@ def test_svc_refusals(lib, svc):
     ts, _ = pinned(np.zeros((1, big_k, big_L), np.uint8))
     tr, _ = pinned(np.zeros((1, 4, big_L), np.uint8))
     assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), big_k, 4, big_L, 0) == -1
+
+
+def test_svc_deadline_withdraws_and_backs_off(lib, svc):
+    """A request not served within the deadline is withdrawn (the worker is ended and waited for; a
+    request it served on its way out still counts), the call returns FECGPU_ERR_INVALID so the caller
+    takes the launch path, and the following calls skip the service for a while.  A later request is
+    served normally: no withdrawn request is ever served by a later worker."""
+    o = Oracle()
+    k, r, L = 16, 4, 1200
+    src = synth_bytes(k * L, 11).reshape(1, k, L)
+    ts, _ = pinned(src)
+    tr, hr = pinned(np.zeros((1, r, L), np.uint8))
+    want = o.rlc_encode_batch(src, r, 5)
+    time.sleep(0.05)  # the worker has idled out: the next call launches one
+    m0 = lib.fecgpu_block_svc_deadline_misses(svc)
+    assert lib.fecgpu_block_svc_set_deadline(svc, 0) == 0
+    outcomes = []
+    for _ in range(20):
+        hr[:] = 0
+        rc = lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, 5)
+        assert rc in (0, -1)
+        if rc == 0:
+            assert np.array_equal(hr, want)
+        outcomes.append(rc)
+    misses = lib.fecgpu_block_svc_deadline_misses(svc) - m0
+    assert misses >= 1
+    assert outcomes.count(-1) >= 1  # withdrawn, or skipped during the back-off
+    assert lib.fecgpu_block_svc_set_deadline(svc, 2000) == 0  # also ends the back-off
+    for _ in range(5):
+        hr[:] = 0
+        assert lib.fecgpu_block_svc_rlc_encode(svc, ts.data_ptr(), tr.data_ptr(), k, r, L, 5) == 0
+        assert np.array_equal(hr, want)
+    assert lib.fecgpu_block_svc_deadline_misses(svc) - m0 == misses

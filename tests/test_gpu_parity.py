@@ -640,6 +640,81 @@ def test_decode_seeded_vs_oracle(eng, oracle, k, r, L, nb, plan):
     assert n_rec > 0
 
 
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 300), (32, 8, 1200, 120), (64, 16, 9000, 6),
+                                      (40, 20, 100, 60), (5, 3, 20, 70), (16, 8, 1216, 5000)])
+def test_decode_rows_vs_oracle(eng, oracle, k, r, L, nb):
+    """fecgpu_rlc_decode_rows (the batching adapter's receive-side gather): every received source and
+    repair read from its own row anywhere in memory, every recovered source written to its own row,
+    by address tables -- against the oracle's per-block decode with the same per-repair seeds.  Rows
+    live in one shuffled pool; rows of absent repairs and unrecovered sources are never read back."""
+    rng = np.random.default_rng(k * 13 + r + nb)
+    src_h = synth_bytes(nb * k * L, 900 + k).reshape(nb, k, L)
+    seeds = np.zeros((nb, r), np.uint32)
+    for b in range(nb):
+        for i in range(r):
+            seeds[b, i] = ((int(rng.integers(0, 1 << 24)) << 8) | i) if b % 2 else int(rng.integers(0, 1 << 32))
+    rep_h = oracle_encode_seeded(oracle, src_h, seeds)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        e = int(rng.integers(0, min(k, r) + 1))
+        miss = set(rng.choice(k, e, replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        nrep = int(rng.integers(max(0, e - 1), r + 1))
+        rp[b] = masks_from_lists(1, r, [rng.choice(r, nrep, replace=False).tolist()])[0]
+    nrows = nb * (k + r)
+    perm = rng.permutation(nrows)  # row q of the logical [src | rep] order lives at pool row perm[q]
+    pool_h = np.full((nrows, L), 0x5A, np.uint8)
+    pool_h[perm[:nb * k]] = src_h.reshape(nb * k, L)
+    pool_h[perm[nb * k:]] = rep_h.reshape(nb * r, L)
+    for b in range(nb):  # missing sources' rows: stale bytes the kernel must overwrite
+        for j in range(k):
+            if j not in bits(sp[b], k):
+                pool_h[perm[b * k + j]] = 0xA5
+    pool = to_dev(pool_h)
+    base = pool.data_ptr()
+    srow = torch.from_numpy((base + perm[:nb * k].astype(np.int64) * L).astype(np.int64)).to(DEV)
+    rrow = torch.from_numpy((base + perm[nb * k:].astype(np.int64) * L).astype(np.int64)).to(DEV)
+    st = torch.full((nb,), 0xEE, dtype=torch.uint8, device=DEV)
+    rec = torch.full((nb, 2), -1, dtype=torch.int64, device=DEV)
+    ws = eng.alloc_workspace(nb, k, r)
+    stream = torch.cuda.current_stream().cuda_stream
+    rc = eng.lib.fecgpu_rlc_decode_rows(srow.data_ptr(), rrow.data_ptr(), nb, k, r, L,
+                                        torch.from_numpy(seeds.view(np.int32)).to(DEV).data_ptr(),
+                                        to_dev(sp).data_ptr(), to_dev(rp).data_ptr(), st.data_ptr(), rec.data_ptr(),
+                                        ws.data_ptr(), ws.numel(), stream)
+    assert rc == 0, eng.err()
+    torch.cuda.synchronize()
+    got, st_h, rec_h = pool.cpu().numpy(), st.cpu().numpy(), rec.cpu().numpy().view(np.uint64)
+    n_rec = 0
+    for b in range(nb):
+        srcs = [src_h[b, j] if j in bits(sp[b], k) else None for j in range(k)]
+        reps = [rep_h[b, i] if i in bits(rp[b], r) else None for i in range(r)]
+        want_st, want = oracle.rlc_decode_block(0, srcs, reps, seeds[b])
+        assert st_h[b] == want_st, b
+        assert bits(rec_h[b], k) == sorted(want), b
+        for j, v in want.items():
+            assert np.array_equal(got[perm[b * k + j]], v), (b, j)
+        for q in range(k):  # received rows untouched
+            if q in bits(sp[b], k):
+                assert np.array_equal(got[perm[b * k + q]], src_h[b, q]), (b, q)
+        n_rec += len(want)
+    assert n_rec > 0
+
+
+def oracle_encode_seeded(oracle, src_h, seeds):
+    """Repairs of every block, repair i of block b seeded by seeds[b, i] (its own FPID)."""
+    nb, k, L = src_h.shape
+    r = seeds.shape[1]
+    mul, _ = oracle.gf_tables()
+    coef = np.array([[oracle.coefs(int(seeds[b, i]), k) for i in range(r)] for b in range(nb)], np.uint8)
+    rep_h = np.zeros((nb, r, L), np.uint8)
+    for i in range(r):
+        for j in range(k):
+            rep_h[:, i] ^= mul[coef[:, i, j][:, None], src_h[:, j]]
+    return rep_h
+
+
 def _ws_fields(ws, k, r, n_blocks):
     """Meaningful fields of each decode-plan record (unwritten bytes are scratch)."""
     em = min(k, r)

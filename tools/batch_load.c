@@ -21,7 +21,8 @@
 #include "fecgpu.h"
 #include "pquic_fec_batch.h"
 
-struct st_picoquic_cnx_t { int id; protoop_arg_t in[16], out[16]; };
+struct bl_arena;
+struct st_picoquic_cnx_t { int id; protoop_arg_t in[16], out[16]; struct bl_arena *arena; };
 
 static protoop_arg_t bl_get(picoquic_cnx_t *c, access_key_t ak, uint16_t p) {
     return ak == PQUIC_AK_CNX_INPUT ? c->in[p & 15] : c->out[p & 15];
@@ -31,43 +32,68 @@ static void bl_set(picoquic_cnx_t *c, access_key_t ak, uint16_t p, protoop_arg_t
 }
 /* The plugin allocator hands out fixed 2100-byte slots from a free list carved out of the plugin's
  * memory arena (picoquic/memory.c:72-95, 181-191; picoquic_internal.h:576); this load generator does
- * the same -- one contiguous arena, so the batcher can register it (pquic_fec_batch_register_heap) --
- * and completions cost what they cost in PQUIC rather than glibc malloc's price.  Larger requests
+ * the same, so completions cost what they cost in PQUIC rather than glibc malloc's price.  Every
+ * connection owns its plugin instances and their 16 MiB arena (PLUGIN_MEMORY, picoquic_internal.h:523;
+ * init_memory_management per inserted plugin, plugin.c:835; cached plugins consumed one per connection,
+ * plugin.c:946-950): with per-connection arenas each connection allocates from its own, registered with
+ * the batcher one by one.  A connection without one uses the sender thread's arena.  Larger requests
  * (and an exhausted arena) fall back to the heap, tagged. */
 enum { SLOT = 2112 };  /* 2100 B rounded to 64, plus room for the tag */
+#define PLUGIN_MEMORY ((size_t)16 << 20)
 typedef union slot_u { union slot_u *next; uint8_t bytes[SLOT]; } slot_u;
+typedef struct bl_arena {
+    uint8_t *base;
+    size_t bytes, used;
+    slot_u *free_slots;
+} bl_arena_t;
 /* per sender thread (bl_run_senders runs several, each a PQUIC process's single thread with its own heap) */
-static __thread slot_u *g_free_slots;
-static __thread uint8_t *g_arena;
-static __thread size_t g_arena_bytes, g_arena_used;
+static __thread bl_arena_t g_thread_arena;
 static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
-    (void)c;
     if (n > SLOT - 16) {
         uint8_t *p = malloc((size_t)n + 16);
         if (!p) return NULL;
         p[0] = 1;
         return p + 16;
     }
-    slot_u *s = g_free_slots;
+    bl_arena_t *a = c && c->arena ? c->arena : &g_thread_arena;
+    slot_u *s = a->free_slots;
     if (s) {
-        g_free_slots = s->next;
-    } else if (g_arena && g_arena_used + SLOT <= g_arena_bytes) {
-        s = (slot_u *)(g_arena + g_arena_used);
-        g_arena_used += SLOT;
+        a->free_slots = s->next;
+    } else if (a->base && a->used + SLOT <= a->bytes) {
+        s = (slot_u *)(a->base + a->used);
+        a->used += SLOT;
     } else if (!(s = malloc(sizeof *s))) {
         return NULL;
+    } else {
+        s->bytes[0] = 2;  /* heap slot: freed to the heap */
+        return s->bytes + 16;
     }
     s->bytes[0] = 0;
     return s->bytes + 16;
 }
 static void bl_free(picoquic_cnx_t *c, void *p) {
-    (void)c;
     if (!p) return;
     uint8_t *b = (uint8_t *)p - 16;
     if (b[0]) { free(b); return; }
+    bl_arena_t *a = c && c->arena ? c->arena : &g_thread_arena;
     slot_u *s = (slot_u *)b;
-    s->next = g_free_slots;
-    g_free_slots = s;
+    s->next = a->free_slots;
+    a->free_slots = s;
+}
+
+static int arena_map(bl_arena_t *a, size_t bytes, int hugepages) {
+    memset(a, 0, sizeof *a);
+    a->bytes = (bytes + 4095) & ~(size_t)4095;
+    void *p = mmap(NULL, a->bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return -1;
+    if (hugepages) madvise(p, a->bytes, MADV_HUGEPAGE);  /* before first touch */
+    a->base = p;
+    return 0;
+}
+
+static void arena_unmap(bl_arena_t *a) {
+    if (a->base) munmap(a->base, a->bytes);
+    memset(a, 0, sizeof *a);
 }
 
 /* the device's local CPUs (fecgpu_device_local_cpus) within `aff`; 0 when non-empty */
@@ -97,6 +123,7 @@ static uint64_t now_us(void) {
 typedef struct {
     pquic_fec_block_t fb;
     uint64_t t_submit;
+    picoquic_cnx_t *cnx;
     int busy;
 } slot_t;
 
@@ -106,6 +133,7 @@ static unsigned g_poll_blocks;  /* pquic_fec_batch_cfg_t.poll_blocks of the next
 static int g_hugepages;         /* the next runs' arena on transparent huge pages */
 static int g_detail;            /* time every submission (one more clock read per block) */
 static long g_pool_blocks = 32768;  /* blocks of distinct source payload (bl_run) */
+static int g_inflight = 4;          /* batches a sender keeps in flight at most (its block slots) */
 
 void bl_set_options(unsigned poll_blocks, int hugepages, int detail, long pool_blocks) {
     g_poll_blocks = poll_blocks;
@@ -113,6 +141,9 @@ void bl_set_options(unsigned poll_blocks, int hugepages, int detail, long pool_b
     g_detail = detail;
     if (pool_blocks > 0) g_pool_blocks = pool_blocks;
 }
+
+/* batches in flight per sender (1..16; default 4): the back-pressure that bounds queueing latency */
+void bl_set_inflight(int batches) { g_inflight = batches < 1 ? 1 : batches > 16 ? 16 : batches; }
 
 /* nanoseconds per now_us() call (the load generator stamps every block at submission and completion) */
 double bl_clock_cost(void) {
@@ -124,6 +155,7 @@ double bl_clock_cost(void) {
 
 static pthread_barrier_t *g_sync;  /* bl_run_senders: the senders' pass barrier */
 static __thread uint64_t g_span[2];  /* the last measured pass: start, end (us) */
+static __thread double g_rows[2];   /* the last bl_run's measured pass: rows in place, rows staged */
 static __thread double g_phases[6];  /* the last bl_run's measured pass: engine, stager, completion thread-us; wall us;
                              * caller us waiting for a free slot; caller us inside pquic_fec_batch_generate */
 
@@ -133,7 +165,26 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     g_lat[g_nlat++] = now_us() - s->t_submit;
     for (int i = 0; i < fb->total_repair_symbols; i++) {
         pquic_repair_symbol_t *rs = fb->repair_symbols[i];
-        if (rs) { bl_free(NULL, rs->data); bl_free(NULL, rs); fb->repair_symbols[i] = NULL; }
+        if (rs) { bl_free(s->cnx, rs->data); bl_free(s->cnx, rs); fb->repair_symbols[i] = NULL; }
+    }
+    s->busy = 0;
+}
+
+/* receiver: the framework decodes the recovered symbols' frames and frees them (fec_protoops.h:252-275) */
+static __thread long g_recovered;
+static __thread const pquic_source_symbol_t *g_recv_lo, *g_recv_hi;  /* the received symbols' descriptors */
+static void on_recovered(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
+    slot_t *s = user;
+    (void)ret;
+    g_lat[g_nlat++] = now_us() - s->t_submit;
+    for (int j = 0; j < fb->total_source_symbols; j++) {
+        pquic_source_symbol_t *ss = fb->source_symbols[j];
+        if (ss && (ss < g_recv_lo || ss >= g_recv_hi)) {  /* inserted by the recover (allocated by the adapter) */
+            g_recovered++;
+            bl_free(s->cnx, ss->data);
+            bl_free(s->cnx, ss);
+        }
+        fb->source_symbols[j] = NULL;
     }
     s->busy = 0;
 }
@@ -144,18 +195,31 @@ static int cmp_u64(const void *a, const void *b) {
 }
 
 /* out: [0] payload GiB/s, [1] p50 us, [2] p99 us, [3] max us, [4] batches, [5] wall s,
- *      [6] blocks completed, [7] mean blocks per batch.  register_heap: the symbols' arena (slot
- * allocator and payload) is registered with the batcher, which then gathers rows in place.
- * Returns 0 or -1. */
+ *      [6] blocks completed, [7] mean blocks per batch.  register_heap: bit 0 -- the symbols' arenas are
+ * registered with the batcher, which then reads and writes rows in place; bit 1 -- one 16 MiB arena per
+ * connection (PQUIC's topology, each registered on its own) instead of one arena for the sender.
+ * recover_e > 0: the receiver side instead -- every block arrives with recover_e sources lost and all r
+ * repairs, and goes through pquic_fec_batch_recover.  Returns 0 or -1. */
 static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks,
-                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, double out[8]);
+                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, int recover_e,
+                      double out[8]);
 
 int bl_run(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks, unsigned max_delay_us,
            int nstreams, double offered_gib_s, int register_heap, double out[8]) {
     pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device)) return -1;
     return run_sender(device, k, r, L, nconn, nblocks, batch_blocks, max_delay_us, nstreams, offered_gib_s,
-                      register_heap, out);
+                      register_heap, 0, out);
+}
+
+/* The receiver: `nblocks` blocks, each with `e` of its k sources lost (a rotating run) and its r repairs,
+ * recovered through the batcher (out as bl_run; [6] counts recovered symbols, not blocks). */
+int bl_run_recover(int device, int k, int r, int L, int e, int nconn, long nblocks, unsigned batch_blocks,
+                   unsigned max_delay_us, int nstreams, int register_heap, double out[8]) {
+    pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
+    if (e < 1 || e > r || e > k || pquic_fec_bind_host(&api, device)) return -1;
+    return run_sender(device, k, r, L, nconn, nblocks, batch_blocks, max_delay_us, nstreams, 0.0, register_heap, e,
+                      out);
 }
 
 /* `nsenders` bl_run senders at once, one thread each with its own batcher, arena and connections -- a
@@ -172,7 +236,7 @@ struct sender_arg {
 static void *sender_main(void *p) {
     struct sender_arg *a = p;
     a->rc = run_sender(a->device, a->k, a->r, a->L, a->nconn, a->nblocks, a->batch, a->delay, a->nstreams, 0.0,
-                       a->reg, a->out);
+                       a->reg, 0, a->out);
     a->span[0] = g_span[0];
     a->span[1] = g_span[1];
     return NULL;
@@ -221,11 +285,20 @@ static int sender_fail(int waits) {
     return -1;
 }
 
+static void xorshift_fill(uint8_t *p, size_t n, uint64_t x) {
+    for (size_t o = 0; o < n; o += 8) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        memcpy(p + o, &x, n - o < 8 ? n - o : 8);
+    }
+}
+
 static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, unsigned batch_blocks,
-                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, double out[8]) {
+                      unsigned max_delay_us, int nstreams, double offered_gib_s, int register_heap, int recover_e,
+                      double out[8]) {
     int waits = 0;  /* pass barriers this sender has passed (bl_run_senders) */
-    /* the sender runs on the device's socket, like the batcher's threads, so the arena it first
-     * touches is local to the device */
+    const int reg = register_heap & 1, per_conn = (register_heap >> 1) & 1;
+    /* the sender runs on the device's socket, like the batcher's threads, so the arenas it first
+     * touches are local to the device */
     cpu_set_t saved, near;
     const int pinned = !sched_getaffinity(0, sizeof saved, &saved) && !near_cpus(device, &saved, &near) &&
                        !sched_setaffinity(0, sizeof near, &near);
@@ -233,39 +306,79 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     pquic_fec_batcher_t *b = pquic_fec_batcher_create(&cfg);
     if (!b) return sender_fail(waits);
     /* blocks in flight at most: every queued batch plus one being filled, per connection slot */
-    const long nslots = (long)batch_blocks * 4 + nconn + 64;
+    const long nslots = (long)batch_blocks * g_inflight + nconn + 64;
     slot_t *slots = calloc(nslots, sizeof *slots);
-    /* Distinct payload for g_pool_blocks blocks, reused in turn.  The default pool (32768 blocks, 629 MB at
-     * k16 L1200) is well past the device's caches, so every source row the kernels read in place crosses
-     * PCIe; a small pool (64 blocks) stays cached on the device and overstates the gathered read rate. */
-    const long pool_blocks = g_pool_blocks > 0 ? g_pool_blocks : 1;
-    const size_t pool_bytes = (size_t)pool_blocks * k * L;
-    /* the arena: 2 slots per repair symbol of every block in flight (struct + data), plus the payload */
-    g_free_slots = NULL;
-    g_arena_bytes = ((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes;
-    g_arena_bytes = (g_arena_bytes + 4095) & ~(size_t)4095;
-    g_arena_used = 0;
-    g_arena = mmap(NULL, g_arena_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (g_arena == MAP_FAILED) return sender_fail(waits);
-    if (g_hugepages) madvise(g_arena, g_arena_bytes, MADV_HUGEPAGE);  /* before first touch */
-    uint8_t *pool = g_arena;  /* the payload (source symbols) lives in the arena as well */
-    g_arena_used = (pool_bytes + 63) & ~(size_t)63;
-    if (register_heap && pquic_fec_batch_register_heap(b, g_arena, g_arena_bytes)) return sender_fail(waits);
+    /* Distinct payload for g_pool_blocks blocks, reused in turn, spread over the connections: connection c
+     * sends pool blocks c, c + nconn, ... (its own arena's, with per-connection arenas).  The default pool
+     * (32768 blocks, 629 MB at k16 L1200) is well past the device's caches, so every source row the
+     * kernels read in place crosses PCIe; a small pool stays cached on the device and overstates the
+     * gathered read rate.  The receiver's pool carries each block's r repairs too. */
+    const long ppc = (g_pool_blocks + nconn - 1) / nconn;  /* pool blocks per connection */
+    const size_t blk_bytes = (size_t)(k + (recover_e ? r : 0)) * L;
+    const size_t pool_conn = (size_t)ppc * blk_bytes;
+    /* allocator slots: 2 per repair (generate) or recovered source (recover) of every block in flight */
+    const size_t slots_total = ((size_t)nslots * (recover_e ? recover_e : r) * 2 + 1024);
+    picoquic_cnx_t *cnx = calloc(nconn, sizeof *cnx);
+    bl_arena_t *ar = per_conn ? calloc(nconn, sizeof *ar) : NULL;
+    if (!slots || !cnx || (per_conn && !ar)) return sender_fail(waits);
+    uint8_t **pool = calloc(nconn, sizeof *pool);  /* connection c's payload */
+    if (!pool) return sender_fail(waits);
+    if (per_conn) {
+        /* PLUGIN_MEMORY per connection, larger only when a connection's share of the payload and its
+         * slots would not fit (few connections, big pools) */
+        size_t need = ((pool_conn + 63) & ~(size_t)63) + (slots_total / nconn + 64) * SLOT;
+        if (need < PLUGIN_MEMORY) need = PLUGIN_MEMORY;
+        for (int c = 0; c < nconn; c++) {
+            if (arena_map(&ar[c], need, g_hugepages)) return sender_fail(waits);
+            cnx[c].arena = &ar[c];
+            pool[c] = ar[c].base;
+            ar[c].used = (pool_conn + 63) & ~(size_t)63;
+        }
+    } else {
+        bl_arena_t *a = &g_thread_arena;
+        if (arena_map(a, slots_total * SLOT + pool_conn * nconn + 64, g_hugepages)) return sender_fail(waits);
+        for (int c = 0; c < nconn; c++) pool[c] = a->base + (size_t)c * pool_conn;
+        a->used = (pool_conn * nconn + 63) & ~(size_t)63;
+    }
+    for (int c = 0; c < nconn; c++) {
+        cnx[c].id = c;
+        xorshift_fill(pool[c], (size_t)ppc * k * L, 0x5EEDF3C0 + (uint64_t)c * 0x9E3779B97F4A7C15ull);
+    }
+    if (recover_e) {  /* the pool's repairs: each pool block q of connection c is block number c * ppc + q */
+        fecgpu_host_ctx_t *hc = fecgpu_host_ctx_create(device, 2, (size_t)64 << 20);
+        uint32_t *fbn = malloc(sizeof *fbn * (size_t)ppc);
+        uint8_t *rep = malloc((size_t)ppc * r * L);
+        if (!hc || !fbn || !rep) return sender_fail(waits);
+        for (int c = 0; c < nconn; c++) {
+            for (long q = 0; q < ppc; q++) fbn[q] = (uint32_t)(c * ppc + q) & 0xffffffu;
+            if (fecgpu_rlc_encode_host(hc, pool[c], rep, ppc, k, r, L, 0, fbn)) return sender_fail(waits);
+            memcpy(pool[c] + (size_t)ppc * k * L, rep, (size_t)ppc * r * L);
+        }
+        free(fbn);
+        free(rep);
+        fecgpu_host_ctx_destroy(hc);
+    }
+    if (reg) {
+        if (per_conn) {
+            for (int c = 0; c < nconn; c++)
+                if (pquic_fec_batch_register_heap(b, ar[c].base, ar[c].bytes)) return sender_fail(waits);
+        } else if (pquic_fec_batch_register_heap(b, g_thread_arena.base, g_thread_arena.bytes)) {
+            return sender_fail(waits);
+        }
+    }
     pquic_source_symbol_t *ss = calloc((size_t)nslots * k, sizeof *ss);
+    pquic_repair_symbol_t *rsy = recover_e ? calloc((size_t)nslots * r, sizeof *rsy) : NULL;
     g_lat = malloc(sizeof *g_lat * (size_t)(nblocks + nblocks / 5 + 1));
     g_nlat = 0;
-    picoquic_cnx_t *cnx = calloc(nconn, sizeof *cnx);
-    if (!slots || !pool || !ss || !g_lat || !cnx) return sender_fail(waits);
-    uint64_t x = 0x5EEDF3C0;
-    for (size_t o = 0; o < pool_bytes; o += 8) {  /* xorshift payload */
-        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-        memcpy(pool + o, &x, pool_bytes - o < 8 ? pool_bytes - o : 8);
-    }
-    for (int c = 0; c < nconn; c++) cnx[c].id = c;
+    g_recovered = 0;
+    g_recv_lo = ss;
+    g_recv_hi = ss + (size_t)nslots * k;
+    if (!ss || !g_lat || (recover_e && !rsy)) return sender_fail(waits);
     const double bytes_per_block = (double)k * L;
     long next_slot = 0;
     /* pass 0 warms up (pinned queue buffers allocated, device buffers grown), pass 1 is measured */
     uint64_t t0 = 0, t_wait = 0, t_submit = 0;
+    long rec0 = 0;
     pquic_fec_batch_stats_t st0;
     memset(&st0, 0, sizeof st0);
     for (int pass = 0; pass < 2; pass++) {
@@ -274,6 +387,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
             pquic_fec_batch_drain(b);
             pquic_fec_batch_get_stats(b, &st0);
             g_nlat = 0;
+            rec0 = g_recovered;
         }
         if (g_sync) pthread_barrier_wait(g_sync), waits++;  /* bl_run_senders: every sender starts each pass together */
         t0 = now_us();
@@ -291,21 +405,42 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
             }
             const long si = next_slot;
             next_slot = (next_slot + 1) % nslots;
+            const int c = (int)(blk % nconn);
+            const long q = (blk / nconn) % ppc;  /* the connection's pool block */
+            const uint8_t *pb = pool[c] + (size_t)q * k * L;
             memset(&s->fb, 0, sizeof s->fb);
-            const uint32_t fbn = (uint32_t)(blk / nconn) & 0xffffffu;
+            const uint32_t fbn = recover_e ? (uint32_t)(c * ppc + q) & 0xffffffu : (uint32_t)(blk / nconn) & 0xffffffu;
             s->fb.fec_block_number = fbn;
+            s->cnx = &cnx[c];
+            const int lost0 = recover_e ? (int)(blk % (k - recover_e + 1)) : k;  /* sources lost0 .. +e-1 */
             for (int j = 0; j < k; j++) {
+                if (j >= lost0 && j < lost0 + recover_e) continue;
                 pquic_source_symbol_t *sym = &ss[si * k + j];
                 sym->fpid.raw = (fbn << 8) | (uint32_t)j;
-                sym->data = pool + ((size_t)(blk % pool_blocks) * k + j) * L;
+                sym->data = (uint8_t *)pb + (size_t)j * L;
                 sym->data_length = (uint16_t)L;
                 s->fb.source_symbols[j] = sym;
+                s->fb.current_source_symbols++;
             }
-            s->fb.current_source_symbols = s->fb.total_source_symbols = (uint8_t)k;
+            s->fb.total_source_symbols = (uint8_t)k;
             s->fb.total_repair_symbols = (uint8_t)r;
+            if (recover_e) {
+                const uint8_t *pr = pool[c] + (size_t)ppc * k * L + (size_t)q * r * L;
+                for (int i = 0; i < r; i++) {
+                    pquic_repair_symbol_t *rs = &rsy[si * r + i];
+                    memset(rs, 0, sizeof *rs);
+                    rs->fpid.raw = ((uint64_t)fbn << 8) | (uint64_t)i;
+                    rs->data = (uint8_t *)pr + (size_t)i * L;
+                    rs->data_length = (uint16_t)L;
+                    s->fb.repair_symbols[i] = rs;
+                }
+                s->fb.current_repair_symbols = (uint8_t)r;
+            }
             s->busy = 1;
             s->t_submit = now_us();
-            if (pquic_fec_batch_generate(b, &cnx[blk % nconn], &s->fb, 0, s->t_submit, on_done, s)) return sender_fail(waits);
+            const int rc = recover_e ? pquic_fec_batch_recover(b, &cnx[c], &s->fb, 0, s->t_submit, on_recovered, s)
+                                     : pquic_fec_batch_generate(b, &cnx[c], &s->fb, 0, s->t_submit, on_done, s);
+            if (rc) return sender_fail(waits);
             if (g_detail) t_submit += now_us() - s->t_submit;
             if ((blk & 15) == 0) pquic_fec_batch_poll(b, now_us());
         }
@@ -317,7 +452,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     g_span[1] = t_end;
     pquic_fec_batch_stats_t st;
     pquic_fec_batch_get_stats(b, &st);
-    pquic_fec_batcher_destroy(b);  /* unregisters the arena */
+    pquic_fec_batcher_destroy(b);  /* unregisters the arenas */
     qsort(g_lat, g_nlat, sizeof *g_lat, cmp_u64);
     out[0] = nblocks * bytes_per_block / wall / 1073741824.0;
     out[1] = g_nlat ? (double)g_lat[g_nlat / 2] : 0;
@@ -325,20 +460,26 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     out[3] = g_nlat ? (double)g_lat[g_nlat - 1] : 0;
     out[4] = (double)(st.batches - st0.batches);
     out[5] = wall;
-    out[6] = (double)(st.completed - st0.completed);
-    out[7] = out[4] > 0 ? out[6] / out[4] : 0;
+    out[6] = recover_e ? (double)(g_recovered - rec0) : (double)(st.completed - st0.completed);
+    out[7] = out[4] > 0 ? (double)(st.completed - st0.completed) / out[4] : 0;
     g_phases[0] = (double)(st.engine_us - st0.engine_us);
     g_phases[1] = (double)(st.stage_us - st0.stage_us);
     g_phases[2] = (double)(st.complete_us - st0.complete_us);
     g_phases[3] = wall * 1e6;
     g_phases[4] = (double)t_wait;
     g_phases[5] = (double)t_submit;
-    free(slots); free(ss); free(g_lat); free(cnx);
+    g_rows[0] = (double)(st.rows_in_place - st0.rows_in_place);
+    g_rows[1] = (double)(st.rows_staged - st0.rows_staged);
+    free(slots); free(ss); free(rsy); free(g_lat); free(cnx); free(pool);
     g_lat = NULL;
     if (pinned) sched_setaffinity(0, sizeof saved, &saved);
-    g_free_slots = NULL;  /* every slot lives in the arena or was malloc'd and leaks here (tool only) */
-    munmap(g_arena, g_arena_bytes);
-    g_arena = NULL;
+    /* every slot lives in an arena or was malloc'd and leaks here (tool only) */
+    if (per_conn) {
+        for (int c = 0; c < nconn; c++) arena_unmap(&ar[c]);
+        free(ar);
+    } else {
+        arena_unmap(&g_thread_arena);
+    }
     return 0;
 }
 
@@ -364,13 +505,9 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
     const long nslots = (long)batch_blocks * 4 + nconn + 64;
     const long ring = ((nslots / nconn + 4) * step + k) * 2;  /* symbols per connection ring */
     const size_t pool_syms = 4096, pool_bytes = pool_syms * (size_t)L;
-    g_free_slots = NULL;
-    g_arena_bytes = (((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes + 4095) & ~(size_t)4095;
-    g_arena_used = 0;
-    g_arena = mmap(NULL, g_arena_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (g_arena == MAP_FAILED) return -1;
-    uint8_t *pool = g_arena;
-    g_arena_used = (pool_bytes + 63) & ~(size_t)63;
+    if (arena_map(&g_thread_arena, ((size_t)nslots * r * 2 + 1024) * SLOT + pool_bytes, 0)) return -1;
+    uint8_t *pool = g_thread_arena.base;
+    g_thread_arena.used = (pool_bytes + 63) & ~(size_t)63;
     slot_t *slots = calloc(nslots, sizeof *slots);
     pquic_source_symbol_t *rings = calloc((size_t)nconn * ring, sizeof *rings);
     long *sent = calloc(nconn, sizeof *sent);
@@ -414,6 +551,7 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
             s->fb.current_source_symbols = s->fb.total_source_symbols = (uint8_t)k;
             s->fb.total_repair_symbols = (uint8_t)r;
             s->busy = 1;
+            s->cnx = NULL;  /* the repairs come from the thread arena */
             s->t_submit = now_us();
             const int rc2 = window_api ? pquic_fec_batch_generate_window(b, &cnx[c], &s->fb, s->t_submit, on_done, s)
                                        : pquic_fec_batch_generate(b, &cnx[c], &s->fb, 0, s->t_submit, on_done, s);
@@ -438,9 +576,7 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
     free(slots); free(rings); free(sent); free(g_lat); free(cnx);
     g_lat = NULL;
     if (pinned) sched_setaffinity(0, sizeof saved, &saved);
-    g_free_slots = NULL;
-    munmap(g_arena, g_arena_bytes);
-    g_arena = NULL;
+    arena_unmap(&g_thread_arena);
     return 0;
 }
 
@@ -523,6 +659,12 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
  * us waiting for a free block slot (completions inside it included), [5] caller us in submissions. */
 void bl_last_phases(double out[6]) {
     for (int i = 0; i < 6; i++) out[i] = g_phases[i];
+}
+
+/* Rows the last bl_run's measured pass coded where they lie ([0]) and through the staging rows ([1]). */
+void bl_last_rows(double out[2]) {
+    out[0] = g_rows[0];
+    out[1] = g_rows[1];
 }
 
 /* The gathered generate path without the batcher: `ncalls` calls of fecgpu_rlc_encode_rows_host on
