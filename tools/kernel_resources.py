@@ -10,7 +10,7 @@ cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c"
        f"{ROOT}/pquic_amd/csrc/fec_engine.hip", "-o", "/dev/null", f"-I{ROOT}/include", f"-I{ROOT}/pquic_amd/csrc",
        "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
-want = re.compile(r"k_rlc_(encode_bs2?|recover_bs2?|encode_rows)<(\d+), (16|true|false)>")
+want = re.compile(r"k_rlc_(encode_bs2?|recover_bs2?|encode_rows|encode_sp)<(\d+), (\d+|true|false)>")
 rec, cur = {}, None
 for ln in out.splitlines():
     m = re.search(r"Function Name: (\S+)", ln)
