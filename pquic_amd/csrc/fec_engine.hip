@@ -55,10 +55,10 @@ static std::atomic<uint64_t> g_stats[4];
 // cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_SPLIT, K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
-                                           "small_lds", "block_svc", "ws_lds", "dec_waves", "split"};
+                                           "small_lds", "block_svc", "ws_lds", "dec_waves"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -102,10 +102,6 @@ static void knobs_from_env() {
   // recover data pass (register-prefetch bodies): 0 = the occupancy its registers allow, n = at most
   // n waves per SIMD
   g_knob[K_DEC_WAVES] = num(getenv("FECGPU_DEC_WAVES"), 0);
-  // encode tiles of 4 / 8 repairs at L <= 2 KiB: W waves share each block's rows (k_rlc_encode_sp;
-  // 0 = one wave per group of blocks, 2 or 4 = W)
-  const int sp = num(getenv("FECGPU_SPLIT"), 0);
-  g_knob[K_SPLIT] = sp == 2 || sp == 4 ? sp : 0;
 }
 
 static inline int knob(KnobId id) {
@@ -1432,73 +1428,6 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
   }
 }
 
-// Split encode (knob split = W): the W waves of a workgroup share each block of its group -- wave w
-// streams source rows w, w + W, ... -- and the partial planes of a block are summed in LDS, where the
-// last wave to arrive finishes the block while the others go on (bitslice_gen.h split_epilogue, no
-// barrier).  A CU then streams W times fewer
-// blocks at once, each W rows at a time: in the trivial-compute probe that pattern reads 6.0-6.4 TB/s
-// against 5.4-6.0 for one wave per block (profiles/r04_split_probe_k*.log).  k % W == 0 (every wave
-// the same number of rows per block: the waves meet at the same barriers), one column chunk (L <= 2 KiB),
-// 16-B pieces.
-constexpr int kRedRepairBytes = 64 * 32;  // one repair's partial planes, 8 dwords per lane (gen_bitslice.py)
-// LDS of a split workgroup: FEC_SPLIT_NBUF(RT) buffers of RT repairs, their arrival and release
-// counters (u32 each), then the waves' coefficient rows
-__host__ __device__ constexpr size_t split_red_bytes(int RT, int W) {
-  return (size_t)FEC_SPLIT_NBUF(RT, W) * RT * kRedRepairBytes + 16 * ((2 * FEC_SPLIT_NBUF(RT, W) * 4 + 15) / 16);
-}
-#define BS_CALL_ENCSP(RT, W)                                                                           \
-  bs_encsp##W##_r##RT##_v16(sp, rpp, (uint32_t)L, (uint32_t)rstep, (uint32_t)(rstep >> 32), sdl, ll,      \
-                            (uint32_t)(ng * KW), (uint32_t)KW, (uint32_t)rt, lds_addr(tab), ln.off[0],    \
-                            ln.off[1], lds_addr(lds_all) + 32u * (uint32_t)lane, lds_addr(cnt), ln.vm[0], ln.vm[1])
-template <int RT, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(RT == 8 ? FEC_V1_ENC8_WAVES : 1)))
-void k_rlc_encode_sp(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep, uint64_t nblocks, int k, int r,
-                     int L, uint32_t fbn_base, const uint32_t *fbn, int r0, int G, int ilv, uint64_t q0) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
-  constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int KW = k / W;                                     // rows per block of each wave
-  constexpr int NB = FEC_SPLIT_NBUF(RT, W);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(lds_all + (size_t)NB * RT * kRedRepairBytes);  // arr[NB], done[NB]
-  uint8_t *tabs = lds_all + split_red_bytes(RT, W);            // the waves' coefficient rows
-  uint8_t *tab = tabs + (size_t)wave * G * KW * CSB;        // this wave's
-  const int rt = r - r0 < RT ? r - r0 : RT;
-  const uint64_t NG = (nblocks + G - 1) / G;
-  const uint64_t bstep = ilv ? NG : 1;
-  const uint64_t q = q0 + blockIdx.x;
-  if (q >= NG) return;  // the whole workgroup
-  const uint64_t b0 = ilv ? q : q * G;
-  const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
-  const int ng = left < (uint64_t)G ? (int)left : G;
-  for (int x = threadIdx.x; x < (int)(split_red_bytes(RT, W) / 16); x += 64 * W)  // buffers and counters
-    reinterpret_cast<uint4 *>(lds_all)[x] = make_uint4(0, 0, 0, 0);
-  if ((int)threadIdx.x < G * RT) {  // TinyMT32 rows: thread -> (block g, repair r0 + i); source j -> wave j % W
-    const int g = threadIdx.x / RT, i = threadIdx.x % RT;
-    const bool live = g < ng && i < rt;
-    Tmt t;
-    if (live) tmt_init(t, rlc_seed(fbn ? fbn[b0 + g * bstep] : (uint32_t)((fbn_base + b0 + g * bstep) & 0xffffffu),
-                                   (uint32_t)(r0 + i)));
-    for (int j = 0; j < k; j++) {
-      uint16_t *row = reinterpret_cast<uint16_t *>(tabs + ((size_t)(j % W) * G * KW + (size_t)g * KW + j / W) * CSB);
-      row[FEC_BS_FIELD_SLOT(RT, i)] = live ? FEC_BS_FIELD(tmt_coef(t), i) : (uint16_t)0;  // 0 ends the chain
-    }
-  }
-  __syncthreads();
-  const BsLanes<16> ln(lane, L);
-  const uint64_t sp = (uint64_t)(uintptr_t)(src + (b0 * (uint64_t)k + wave) * L);  // row `wave` of block b0
-  const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L);
-  const uint64_t rstep = bstep * (uint64_t)r * L;
-  const uint64_t ll = (uint64_t)W * L;                                       // to the wave's next row
-  const uint64_t sdl = bstep * (uint64_t)k * L - (uint64_t)W * L * (KW - 1);  // to its first row of the next block
-  if (lane < ln.active) {
-    if constexpr (RT == 4 && W == 2) BS_CALL_ENCSP(4, 2);
-    else if constexpr (RT == 4) BS_CALL_ENCSP(4, 4);
-    else if constexpr (W == 2) BS_CALL_ENCSP(8, 2);
-    else BS_CALL_ENCSP(8, 4);
-  }
-}
-
 // Setup reads the workspace for all of a group's blocks at once (lanes spread over (block, input)
 // pairs), so each group pays one HBM round trip before its data pass, not one per block.
 // status != nullptr: single pass (e <= RT for every block, r0 == 0) -- the zero/undetermined
@@ -2174,22 +2103,6 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
   const uint64_t groups = (nb + G - 1) / G;
   FEC_LAUNCH_GROUPS((k_rlc_encode_bs<RT, VEC>), groups, 64 * W, lds, s, src, rep, nb, k, r, L, c.nchunks,
                     c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups())
-}
-
-// Split encode groups: G blocks per workgroup (halved for small batches as bs_group does), so the
-// G * RT TinyMT32 streams of a group run in parallel on the workgroup's threads.
-template <int RT, int W>
-static void launch_encode_sp(const uint8_t *src, uint8_t *rep, uint64_t nb, int k, int r, int L, uint32_t fbn_base,
-                             const uint32_t *fbn, int r0, hipStream_t s) {
-  int G = 4;
-  if (const int cap = knob(K_GROUP))
-    while (G > 1 && G > cap) G >>= 1;
-  if (const uint64_t ming = (uint64_t)knob(K_MIN_GROUPS))
-    while (G > 1 && (nb + G - 1) / G < ming) G >>= 1;
-  const size_t lds = split_red_bytes(RT, W) + (size_t)G * k * FEC_BS_COEF_ROW_BYTES(RT);
-  const uint64_t groups = (nb + G - 1) / G;
-  FEC_LAUNCH_GROUPS((k_rlc_encode_sp<RT, W>), groups, 64 * W, lds, s, src, rep, nb, k, r, L, fbn_base, fbn, r0, G,
-                    interleave_groups())
 }
 
 template <int RT, int VEC>
@@ -3039,7 +2952,6 @@ static bool knob_value_ok(int id, int v) {
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;
     case K_DEC_WAVES: return v >= 0 && v <= 8;
-    case K_SPLIT: return v == 0 || v == 2 || v == 4;
     default: return v == 0 || v == 1;  // on / off knobs
   }
 }
@@ -3125,20 +3037,6 @@ int fecgpu_rlc_encode(const void *src, void *rep, uint64_t nblocks, uint32_t k, 
   const BsCfg cfg = pick_bs_cfg((int)symbol_size);
   const EncTile et = pick_enc_tile(r);
   const int rt = et.rt;
-  const int W = knob(K_SPLIT);
-  if (W && et.waves == 1 && (rt == 4 || rt == 8) && cfg.vec == 16 && cfg.nchunks == 1 && k % W == 0 &&
-      k >= 2 * W) {  // split encode (k_rlc_encode_sp)
-    for (int r0 = 0; r0 < (int)r; r0 += rt) {
-      if (rt == 4 && W == 2) launch_encode_sp<4, 2>((const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn, r0, s);
-      else if (rt == 4) launch_encode_sp<4, 4>((const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn, r0, s);
-      else if (W == 2) launch_encode_sp<8, 2>((const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn, r0, s);
-      else launch_encode_sp<8, 4>((const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r, (int)symbol_size, fbn_base, fbn, r0, s);
-    }
-    HIPCHK(hipGetLastError());
-    g_stats[0]++;
-    g_stats[1] += nblocks;
-    return FECGPU_OK;
-  }
   if (use_ring(rt, k, cfg, true)) {
     for (int r0 = 0; r0 < (int)r; r0 += rt * et.waves) {
       FEC_BS2_DISPATCH(launch_encode_bs2, (const uint8_t *)src, (uint8_t *)rep, nblocks, (int)k, (int)r,

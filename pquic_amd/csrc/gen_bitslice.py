@@ -111,7 +111,7 @@ S_EPI = 86
 S_S = 88
 S_JL = 89        # enc: sources loaded in the current block (the prefetch crosses block boundaries)
 S_O2 = 90
-S_BLK = 92       # split encode: the block of the workgroup's stream the wave is in
+S_DJ = 92        # enc: pointer jump applied when a block's last source has been loaded
 SGPR_CLOBBER = list(range(60, 94))  # s0-s59 and s94-s101 stay with the compiler
 MASKS = [0x55555555, 0x33333333, 0x0F0F0F0F]
 STAGES = [  # (shift, mask index, pairs)
@@ -407,26 +407,19 @@ def regrange(base, n):
     return f"v{base}" if n == 1 else f"v[{base}:{base + n - 1}]"
 
 
-# Split encode (W waves per block): a lane's share of one repair's partial planes in the LDS reduction
-# buffer -- 8 dwords per lane, 64 lanes -- and the buffer of a tile is RT of them (split_epilogue).
-RED_REPAIR_BYTES = 64 * 32
-
-
-def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False, split: int = 0):
+def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     """Inline-asm text for one group of blocks x one column chunk.
 
-    split = W > 1 (encode): the block's rows are shared by the W waves of a workgroup -- this wave
-    streams rows w, w + W, ... (%[k] rows per block, %[ll] = W * L between them) -- and the partial
-    planes of each block meet in an LDS buffer, where the last wave to arrive finishes the block
-    (split_epilogue: no barrier, the other waves go on).  Operands %[red] (this lane's slice of the
-    workgroup's first buffer) and %[cnt] (the arrival and release counters)."""
+    The sources of all blocks of the group form ONE stream (flattened index s = g*k + j),
+    so the P-deep register prefetch runs across block boundaries; when j wraps, the
+    per-block epilogue subroutine (reached by s_swappc) transposes the accumulators back,
+    stores them and clears them.  mode 'enc' (addresses by stride) or 'dec' (addresses
+    from LDS tables written by the wrapper)."""
     ld, st, nw = LOADOP[VEC]
     NP = 32 // VEC
     DATA_BASE = data_base(mode)
     acc_base = DATA_BASE + 8 * P
     assert acc_base + 8 * RT <= 256
-    assert not split or (mode == "enc" and not sc and INPTR < DATA_BASE), "split: encode bodies (INPTR free)"
-    RV = INPTR  # split: this lane's address in the reduction buffer of the current block
     L = []
     a = L.append
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -460,9 +453,6 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False, split: int = 0)
     if mode == "enc":
         a(f"s_mov_b64 s[{S_CUR}:{S_CUR + 1}], %[src]")
         a(f"s_mov_b64 s[{S_OUT}:{S_OUT + 1}], %[rep]")
-        if split:
-            a(f"v_mov_b32 v{RV}, %[red]")
-            a(f"s_mov_b32 s{S_BLK}, 0")
     else:
         a(f"v_mov_b32 v{INPTR}, %[intab]")
         a(f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}")  # source 0's address
@@ -620,9 +610,6 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False, split: int = 0)
 
     # ---- per-block epilogue subroutine ----
     a(".Lepi_%=:")
-    if split:
-        L.extend(split_epilogue(RT, split, acc_base, nw, NP, st, live))
-        return L, acc_base + 8 * RT
     if mode == "enc":
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
@@ -676,109 +663,6 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False, split: int = 0)
     return L, acc_base + 8 * RT
 
 
-def split_nbuf(RT: int, W: int) -> int:
-    """Reduction buffers of a split workgroup (a wave may run that many blocks minus one ahead): as
-    many as leave the tile's occupancy to its registers (160 KiB of LDS per CU over the workgroups of
-    3 waves per SIMD at RT 4, 4 at RT 8)."""
-    return {(4, 4): 4, (4, 2): 2, (8, 4): 2, (8, 2): 1}[(RT, W)]
-
-
-def split_epilogue(RT, W, acc_base, nw, NP, st, live):
-    """The split encode's per-block epilogue, lock-free (see body), then the loop's exit.
-
-    Block b of the workgroup's stream (S_BLK) uses buffer x = b % NB of epoch e = b / NB.  A wave
-    first waits until the buffer is free (done[x] == e: block b - NB has been taken), XORs its
-    partial planes of every live repair into it (ds_xor_b64), and counts its arrival (ds_add_rtn_u32
-    on arr[x], one lane).  The wave whose arrival completes the block (old count e * W + W - 1) takes
-    the sums with ds_wrxchg_rtn_b64 (read and cleared in one operation) into its accumulators,
-    releases the buffer (done[x] += 1), transposes back and stores every repair of the block; the
-    others go straight on to their next block.  LDS operations of a wave execute in order, so a
-    wave's XORs land before its arrival is counted and the sums are read before the release.  The
-    slowest wave never waits (every block before its current one has been taken), so no wave waits
-    for ever."""
-    RV = INPTR
-    NB = split_nbuf(RT, W)
-    lg = NB.bit_length() - 1
-    X, T = t64_scratch(T_BASE)  # dead between a block's last case and the next source's combos
-    S_X, S_E, S_A, S_B = S_C[0], S_C[1], S_CQ, S_CQ + 1  # free in the epilogue
-    L = []
-    a = L.append
-    a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
-    a(f"s_mov_b32 s{S_RT}, %[rt]")
-    a(f"s_and_b32 s{S_X}, s{S_BLK}, {NB - 1}")
-    a(f"s_lshr_b32 s{S_E}, s{S_BLK}, {lg}")
-    a(f"s_lshl_b32 s{S_A}, s{S_X}, 2")
-    a(f"s_add_u32 s{S_A}, s{S_A}, %[cnt]")  # &arr[x]; done[x] at + 4 NB
-    a(f"v_mov_b32 v{T[3]}, s{S_A}")
-    a(".Lsp_wait_%=:")
-    a(f"ds_read_b32 v{T[2]}, v{T[3]} offset:{4 * NB}")
-    a("s_waitcnt lgkmcnt(0)")
-    a(f"v_readfirstlane_b32 s{S_A}, v{T[2]}")
-    a(f"s_cmp_eq_u32 s{S_A}, s{S_E}")
-    a(f"s_cbranch_scc1 .Lsp_go_%=")
-    a("s_sleep 1")
-    a(f"s_branch .Lsp_wait_%=")
-    a(".Lsp_go_%=:")
-    a(f"s_mul_i32 s{S_A}, s{S_X}, {RT * RED_REPAIR_BYTES}")
-    a(f"v_add_u32 v{T[2]}, s{S_A}, v{RV}")  # this lane's slice of buffer x
-    for i in range(RT):  # every live repair's partial planes into the buffer
-        accs = [acc_base + 8 * i + w for w in range(8)]
-        a(f"s_cmp_le_u32 s{S_RT}, {i}")
-        a(f"s_cbranch_scc1 .Lsp_xored_%=")
-        for q in range(4):
-            a(f"ds_xor_b64 v{T[2]}, v[{accs[2 * q]}:{accs[2 * q + 1]}] offset:{i * RED_REPAIR_BYTES + 8 * q}")
-    a(".Lsp_xored_%=:")
-    a("s_mov_b64 exec, 1")  # one arrival per wave (lane 0 is always live)
-    a(f"v_mov_b32 v{T[0]}, 1")
-    a(f"ds_add_rtn_u32 v{T[0]}, v{T[3]}, v{T[0]}")
-    a("s_waitcnt lgkmcnt(0)")
-    a(f"s_mov_b64 exec, {live}")
-    a(f"v_readfirstlane_b32 s{S_A}, v{T[0]}")
-    a(f"s_mul_i32 s{S_B}, s{S_E}, {W}")
-    a(f"s_add_u32 s{S_B}, s{S_B}, {W - 1}")
-    a(f"s_cmp_lg_u32 s{S_A}, s{S_B}")
-    a(f"s_cbranch_scc1 .Lepi_done_%=")  # not the last arrival: the block is someone else's to finish
-    a(f"v_mov_b32 v{T[0]}, 0")
-    a(f"v_mov_b32 v{T[1]}, 0")
-    for i in range(RT):  # the last arrival: the sums into its accumulators, the buffer cleared
-        accs = [acc_base + 8 * i + w for w in range(8)]
-        a(f"s_cmp_le_u32 s{S_RT}, {i}")
-        a(f"s_cbranch_scc1 .Lsp_took_%=")
-        for q in range(4):
-            a(f"ds_wrxchg_rtn_b64 v[{accs[2 * q]}:{accs[2 * q + 1]}], v{T[2]}, v[{T[0]}:{T[1]}] "
-              f"offset:{i * RED_REPAIR_BYTES + 8 * q}")
-    a(".Lsp_took_%=:")
-    a("s_waitcnt lgkmcnt(0)")
-    a("s_mov_b64 exec, 1")  # release: done[x] += 1
-    a(f"v_mov_b32 v{T[0]}, 1")
-    a(f"ds_add_u32 v{T[3]}, v{T[0]} offset:{4 * NB}")
-    a(f"s_mov_b64 exec, {live}")
-    for i in range(RT):
-        accs = [acc_base + 8 * i + w for w in range(8)]
-        a(f"s_cmp_le_u32 s{S_RT}, {i}")
-        a(f"s_cbranch_scc1 .Lepi_done_%=")
-        slots = [accs[SIG[o]] for o in range(8)]
-        L.extend(transpose64(slots, slots, X, T))
-        for q in range(NP):
-            a(f"s_mov_b64 exec, %[vm{q}]")
-            a(f"{st} %[off{q}], {regrange(accs[q * nw], nw)}, s[{S_O2}:{S_O2 + 1}]@STPOL@")
-        a(f"s_mov_b64 exec, {live}")
-        a(f"s_add_u32 s{S_O2}, s{S_O2}, %[L]")
-        a(f"s_addc_u32 s{S_O2 + 1}, s{S_O2 + 1}, 0")
-    a(".Lepi_done_%=:")
-    for r in range(acc_base, acc_base + 8 * RT):
-        a(f"v_mov_b32 v{r}, 0")
-    a(f"s_add_u32 s{S_BLK}, s{S_BLK}, 1")
-    a(f"s_add_u32 s{S_OUT}, s{S_OUT}, %[rslo]")  # next block of the group (64-bit step)
-    a(f"s_addc_u32 s{S_OUT + 1}, s{S_OUT + 1}, %[rshi]")
-    a(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
-    a(".Lexit_%=:")
-    a("s_waitcnt lgkmcnt(0)")
-    a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
-    a(f"s_mov_b32 m0, s{S_SAVEM0}")
-    return L
-
-
 def cstring(lines):
     # cache-policy suffixes of the symbol loads/stores come from FEC_LD_POL / FEC_ST_POL (C string
     # macros, defaults below) so a build can pick them without regenerating
@@ -789,19 +673,16 @@ def cstring(lines):
     return "\n".join(out)
 
 
-def emit_function(mode, RT, VEC, P, sc=False, split=0):
+def emit_function(mode, RT, VEC, P, sc=False):
     """sc: the shared-coefficient encode (window blocks, fbn 0): separate per-piece store offsets
     so0.. (a lane's pieces may belong to different windows, whose sources and repairs are laid
-    out with different strides).  split: W waves per block (body), two more operands: %[red] (this
-    lane's slice of the workgroup's reduction buffers) and %[cnt] (their counters)."""
-    lines, top = body(mode, RT, VEC, P, sc, split)
+    out with different strides)."""
+    lines, top = body(mode, RT, VEC, P, sc)
     NP = 32 // VEC
-    name = f"bs_{mode}{'sc' if sc else ''}{f'sp{split}' if split else ''}_r{RT}_v{VEC}"
+    name = f"bs_{mode}{'sc' if sc else ''}_r{RT}_v{VEC}"
     offs = ", ".join(f"uint32_t off{q}" for q in range(NP))
     if sc:
         offs += ", " + ", ".join(f"uint32_t so{q}" for q in range(NP))
-    if split:
-        offs += ", uint32_t red, uint32_t cnt"
     vms = ", ".join(f"uint64_t vm{q}" for q in range(NP))
     if mode == "enc":
         sig = (f"__device__ __forceinline__ void {name}(uint64_t src, uint64_t rep, uint32_t L, uint32_t rslo, "
@@ -816,8 +697,6 @@ def emit_function(mode, RT, VEC, P, sc=False, split=0):
     ins += [f'[off{q}] "v"(off{q})' for q in range(NP)]
     if sc:
         ins += [f'[so{q}] "v"(so{q})' for q in range(NP)]
-    if split:
-        ins += ['[red] "v"(red)', '[cnt] "s"(cnt)']
     ins += [f'[vm{q}] "s"(vm{q})' for q in range(NP)]
     clob = [f'"v{r}"' for r in range(T_BASE, top)] + [f'"s{r}"' for r in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
     out = [sig + " {", "  asm volatile(", cstring(lines), "      :",
@@ -1254,8 +1133,6 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
 
 
 CONFIGS = [(RT, VEC) for VEC in (16, 8, 4) for RT in (1, 2, 4, 8, 16)]
-SPLIT_RT = (4, 8)  # tiles with split bodies (W waves per block)
-SPLIT_W = (2, 4)
 
 
 _V1_LAYOUT_NAMES = ("T_BASE", "TL", "TH", "TMP", "CO", "COPTR", "INPTR", "OUTPTR", "NADDR", "DATA_BASE", "XS",
@@ -1392,20 +1269,6 @@ def main():
             tops[(mode, RT, VEC, P)] = top
             parts.append(fn)
             parts.append("")
-    # split encode bodies (W waves per block), 16-B pieces, the tile's usual register map
-    for RT in SPLIT_RT:
-        for W in SPLIT_W:
-            compact = RT in COMPACT_ENC
-            with _Layout(v1_compact_layout() if compact else None):
-                if compact:
-                    P = max(P for P in range(2, 33) if data_base("enc") + 8 * P + 8 * RT <= compact_vgprs(RT)
-                            and 2 * (P - (0 if EARLY_PF else 1)) <= 63)
-                else:
-                    P = prefetch_depth("enc", RT, 16)
-                fn, top = emit_function("enc", RT, 16, P, split=W)
-            tops[("encsp", RT, W, P)] = top
-            parts.append(fn)
-            parts.append("")
     # shared-coefficient encode bodies (window blocks): wide register map, 16-B pieces
     for RT in (1, 2, 4, 8):
         P = prefetch_depth("enc", RT, 16)
@@ -1413,9 +1276,6 @@ def main():
         tops[("encsc", RT, 16, P)] = top
         parts.append(fn)
         parts.append("")
-    parts.append("// split encode: reduction buffers per workgroup and tile size (gen_bitslice.py split_nbuf)")
-    parts.append("#define FEC_SPLIT_NBUF(RT, W) ((RT) <= 4 ? ((W) == 4 ? %d : %d) : ((W) == 4 ? %d : %d))"
-                 % (split_nbuf(4, 4), split_nbuf(4, 2), split_nbuf(8, 4), split_nbuf(8, 2)))
     parts.append(f"#define FEC_BS2_BASE {T2_BASE}")
     parts.append(f"#define FEC_BS2_RT16_WAVES {4 if os.environ.get('FEC_GEN2_PROBE_ALIAS') else 3}  // 16-repair ring encode waves/SIMD")
     parts.append(f"#define FEC_BS2_SLOT {S2_SLOT}  // ring slot bytes (the bodies address slots by immediates)")

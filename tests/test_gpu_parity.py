@@ -89,38 +89,6 @@ def test_encode_vs_oracle(eng, oracle, k, r, L, nb):
     assert np.array_equal(rep.cpu().numpy(), oracle.rlc_encode_batch(src_h, r, fbn_base))
 
 
-@pytest.mark.parametrize("W", [2, 4])
-@pytest.mark.parametrize("k,r,L,nb,ilv", [(16, 4, 1200, 257, 1), (32, 8, 1200, 129, 1), (16, 8, 1216, 300, 0),
-                                          (8, 4, 64, 70, 1), (12, 5, 100, 99, 1), (24, 12, 2048, 65, 0),
-                                          (16, 3, 20, 200, 1), (32, 4, 1200, 5000, 1), (16, 4, 1200, 1, 1),
-                                          (32, 8, 1200, 7, 0), (64, 8, 1200, 33, 1)])
-def test_split_encode_vs_oracle(eng, oracle, W, k, r, L, nb, ilv):
-    """Split encode (knob split = W: W waves share each block's rows and sum their partial planes in
-    LDS, k_rlc_encode_sp) against the oracle: 4- and 8-repair tiles with remainders, rows of 1..64 lanes,
-    groups of 1..4 blocks, contiguous and interleaved groups, the 24-bit block-number wrap."""
-    src_h = synth_bytes(nb * k * L, 2000 + k * r + W).reshape(nb, k, L)
-    rep = torch.full((nb, r, L), 0x5A, dtype=torch.uint8, device=DEV)
-    fbn_base = 0xFFFFF0 + k
-    with eng.knob("split", W), eng.knob("small_lds", 0), eng.knob("interleave", ilv):
-        eng.rlc_encode(to_dev(src_h), rep, k, r, L, fbn_base=fbn_base)
-        torch.cuda.synchronize()
-    assert np.array_equal(rep.cpu().numpy(), oracle.rlc_encode_batch(src_h, r, fbn_base))
-
-
-def test_split_encode_fbn_array(eng, oracle):
-    nb, k, r, L = 200, 16, 4, 1200
-    src_h = synth_bytes(nb * k * L, 77).reshape(nb, k, L)
-    fbns = np.random.default_rng(1).integers(0, 1 << 24, nb).astype(np.uint32)
-    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
-    with eng.knob("split", 4):
-        eng.rlc_encode(to_dev(src_h), rep, k, r, L, fbn=torch.from_numpy(fbns.view(np.int32)).to(DEV))
-        torch.cuda.synchronize()
-    got = rep.cpu().numpy()
-    for b in range(nb):
-        _, reps = oracle.rlc_encode_block(int(fbns[b]), [src_h[b, j] for j in range(k)], r)
-        assert np.array_equal(got[b], np.stack(reps)), b
-
-
 def test_encode_explicit_fbn_array(eng, oracle):
     nb, k, r, L = 40, 8, 3, 64
     src_h = synth_bytes(nb * k * L, 5).reshape(nb, k, L)
