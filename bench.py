@@ -466,78 +466,111 @@ def pcie_legs(torch, args, dev):
 def batching_legs(dev_index, args):
     """§8f row 1: the block framework's blocks through the batching adapter
     (include/pquic_fec_batch.h), end to end from host packet buffers: PCIe, kernels, completion on the
-    caller thread.  tools/batch_load.c plays the single-threaded sender over 64 connections, its
-    symbols in one plugin-style memory arena.  "saturated" / "paced": the arena is registered with the
-    batcher (pquic_fec_batch_register_heap), so the kernels read sources and write repairs in place;
-    "saturated_staged": unregistered, the stager threads copy every row through pinned staging."""
+    caller thread.  tools/batch_load.c plays the single-threaded sender (or receiver) over 64 or 512
+    connections, each with its own 16 MiB plugin arena (PLUGIN_MEMORY, picoquic_internal.h:523,576; one
+    plugin instance per connection, plugin.c:835,946-950) holding its symbols.  Registered arenas
+    (pquic_fec_batch_register_heap, one per connection): the kernels read sources / received symbols
+    and write repairs / recovered symbols in place; "staged": unregistered, the stager threads copy every
+    row through pinned staging.  A sender keeps at most 3 batches of 2048 blocks in flight (the
+    back-pressure that bounds the queueing latency)."""
     import ctypes as C
     path = os.path.join(ROOT, "tools", "libbatchload.so")
     if not os.path.exists(path):
         return {}
     lib = C.CDLL(path)
+    D = C.POINTER(C.c_double)
     lib.bl_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint, C.c_uint, C.c_int,
-                           C.c_double, C.c_int, C.POINTER(C.c_double)]
+                           C.c_double, C.c_int, D]
+    lib.bl_run_recover.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint,
+                                   C.c_uint, C.c_int, C.c_int, D]
     lib.bl_run_window.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, C.c_uint,
-                                  C.c_uint, C.c_int, C.c_int, C.POINTER(C.c_double)]
-    lib.bl_run_senders.argtypes = [C.c_int] + lib.bl_run.argtypes[:9] + [C.c_int, C.POINTER(C.c_double)]
+                                  C.c_uint, C.c_int, C.c_int, D]
+    lib.bl_run_senders.argtypes = [C.c_int] + lib.bl_run.argtypes[:9] + [C.c_int, D]
+    lib.bl_set_inflight.argtypes = [C.c_int]
+    lib.bl_last_rows.argtypes = [D]
+    REG, PER_CONN = 1, 2
+    batch, inflight = 2048, 3
+    lib.bl_set_inflight(inflight)
     legs = {}
-    # host-side rates on a shared CPU slice vary from run to run: the saturated legs report the run
-    # with the median rate of three, and every run's rate
-    for name, nblocks, batch, delay, offered, reg, runs in (("saturated", 200000, 4096, 2000, 0.0, 1, 3),
-                                                            ("saturated_staged", 200000, 4096, 2000, 0.0, 0, 3),
-                                                            ("paced_2GiBps", 100000, 4096, 250, 2.0, 1, 1)):
+
+    def median_of(runs, fn):
+        """host-side rates on a shared CPU slice vary from run to run: the run with the median rate"""
         res = []
         for _ in range(runs):
-            out = (C.c_double * 8)()
-            rc = lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, nblocks, batch, delay, 2, offered, reg, out)
+            out, rows = (C.c_double * 8)(), (C.c_double * 2)()
+            rc = fn(out)
             if rc:
-                break
-            res.append(list(out))
-        if len(res) < runs:
-            legs["batch_" + name] = {"error": rc}
-            continue
-        out = sorted(res, key=lambda o: o[0])[len(res) // 2]
-        legs["batch_" + name] = {
-            "k": args.k, "r": args.r, "L": args.symbol, "blocks": nblocks, "connections": 64,
-            "batch_blocks": batch, "max_delay_us": delay, "offered_GiB_s": offered or None,
-            "rows": "gathered in place (registered arena)" if reg else "staged by copies",
-            "source_pool_blocks": 32768,
-            "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
-            "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1),
-            "runs_payload_GiB_s": [round(o[0], 2) for o in res]}
-    # two sender threads, each with its own batcher, arena and 64 connections: a server running one
+                return rc, None, None
+            lib.bl_last_rows(rows)
+            res.append((list(out), list(rows)))
+        res.sort(key=lambda x: x[0][0])
+        out, rows = res[len(res) // 2]
+        return 0, out, {"runs_payload_GiB_s": [round(o[0][0], 2) for o in res], "rows_in_place": int(rows[0]),
+                        "rows_staged": int(rows[1])}
+
+    def leg(out, extra, **kw):
+        d = {"k": args.k, "r": args.r, "L": args.symbol, "batch_blocks": batch, "batches_in_flight": inflight,
+             "max_delay_us": 2000}
+        d.update(kw)
+        d.update({"payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
+                  "latency_us_max": out[3], "batches": int(out[4]), "mean_blocks_per_batch": round(out[7], 1)})
+        d.update(extra)
+        return d
+
+    for name, nconn, reg, runs in (("saturated", 64, REG | PER_CONN, 3), ("saturated_512conn", 512, REG | PER_CONN, 3),
+                                   ("saturated_staged", 64, PER_CONN, 3)):
+        rc, out, extra = median_of(runs, lambda o: lib.bl_run(dev_index, args.k, args.r, args.symbol, nconn, 200000,
+                                                              batch, 2000, 2, 0.0, reg, o))
+        legs["batch_" + name] = {"error": rc} if rc else leg(
+            out, extra, blocks=200000, connections=nconn, arenas="one 16 MiB arena per connection",
+            rows="in place (registered arenas)" if reg & REG else "staged by copies", source_pool_blocks=32768)
+    rc, out, extra = median_of(3, lambda o: lib.bl_run_recover(dev_index, args.k, args.r, args.symbol, args.erasures,
+                                                               64, 200000, batch, 2000, 2, REG | PER_CONN, o))
+    legs["batch_recover_saturated"] = {"error": rc} if rc else leg(
+        out, extra, blocks=200000, connections=64, erasures=args.erasures, recovered_symbols=int(out[6]),
+        arenas="one 16 MiB arena per connection",
+        rows="received symbols read and recovered symbols written in place (registered arenas; recovered "
+             "symbols allocated at submission)", source_pool_blocks=32768)
+    rc, out, extra = median_of(1, lambda o: lib.bl_run_recover(dev_index, args.k, args.r, args.symbol, args.erasures,
+                                                               64, 200000, batch, 2000, 2, PER_CONN, o))
+    legs["batch_recover_saturated_staged"] = {"error": rc} if rc else leg(
+        out, extra, blocks=200000, connections=64, erasures=args.erasures, recovered_symbols=int(out[6]),
+        rows="staged by copies")
+    rc, out, extra = median_of(1, lambda o: lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, 100000, 4096, 250,
+                                                       2, 2.0, REG | PER_CONN, o))
+    legs["batch_paced_2GiBps"] = {"error": rc} if rc else leg(
+        out, extra, blocks=100000, connections=64, offered_GiB_s=2.0, max_delay_us=250, batch_blocks=4096)
+    # two sender threads, each with its own batcher and 64 connections: a server running one
     # single-threaded PQUIC process per core on one GPU (one sender alone is bound by its own thread)
     res = []
     for _ in range(3):
         out = (C.c_double * 8)()
-        if lib.bl_run_senders(2, dev_index, args.k, args.r, args.symbol, 64, 200000, 4096, 2000, 2, 1, out):
+        if lib.bl_run_senders(2, dev_index, args.k, args.r, args.symbol, 64, 200000, batch, 2000, 2,
+                              REG | PER_CONN, out):
             break
         res.append(list(out))
     if len(res) == 3:
         out = sorted(res, key=lambda o: o[0])[1]
-        legs["batch_saturated_2senders"] = {
-            "k": args.k, "r": args.r, "L": args.symbol, "senders": 2, "blocks_per_sender": 200000,
-            "connections_per_sender": 64, "batch_blocks": 4096, "max_delay_us": 2000, "source_pool_blocks": 32768,
-            "rows": "gathered in place (registered arenas)",
-            "payload_GiB_s": round(out[0], 2), "latency_us_p50": out[1], "latency_us_p99": out[2],
-            "latency_us_max": out[3], "batches": int(out[4]),
-            "runs_payload_GiB_s": [round(o[0], 2) for o in res],
-            "note": "both senders start each pass at a barrier; rate = all blocks over first start to last drain; "
-                    "latency = the worse sender's percentile"}
+        legs["batch_saturated_2senders"] = leg(
+            out, {"runs_payload_GiB_s": [round(o[0], 2) for o in res]}, senders=2, blocks_per_sender=200000,
+            connections_per_sender=64, arenas="one 16 MiB arena per connection",
+            note="both senders start each pass at a barrier; rate = all blocks over first start to last drain; "
+                 "latency = the worse sender's percentile")
     else:
         legs["batch_saturated_2senders"] = {"error": -1}
+    lib.bl_set_inflight(4)
     # the sliding-window sender (window_framework_sender.h:209-260) at the redundancy controllers'
     # shapes: a window of the <= 30 symbols in flight every K new ones, N - K repairs
     for k, r, step in ((30, 1, 5), (30, 5, 25)):
-        leg = {"k": k, "r": r, "L": args.symbol, "step": step, "windows": 200000, "connections": 64,
-               "batch_blocks": 4096, "max_delay_us": 2000}
+        leg_w = {"k": k, "r": r, "L": args.symbol, "step": step, "windows": 200000, "connections": 64,
+                 "batch_blocks": 4096, "max_delay_us": 2000}
         for api, tag in ((1, "window_api"), (0, "block_api")):
             out = (C.c_double * 8)()
             rc = lib.bl_run_window(dev_index, k, r, args.symbol, step, 64, 200000, 4096, 2000, 2, api, out)
-            leg[tag] = {"error": rc} if rc else {
+            leg_w[tag] = {"error": rc} if rc else {
                 "stream_GiB_s": round(out[0], 2), "window_GiB_s": round(out[7], 2), "latency_us_p50": out[1],
                 "latency_us_p99": out[2], "batches": int(out[4])}
-        legs[f"batch_window_k{k}_r{r}_step{step}"] = leg
+        legs[f"batch_window_k{k}_r{r}_step{step}"] = leg_w
     return legs
 
 
@@ -560,6 +593,16 @@ def hook_latency_legs(dev_index):
            "generate_us_p50": out[0], "generate_us_p99": out[1], "generate_us_mean": round(out[2], 1),
            "recover_us_p50": out[3], "recover_us_p99": out[4], "recover_us_mean": round(out[5], 1),
            "recovered_per_call": out[6]}
+    # the same hooks while a bulk job (4096-block k16 r4 encodes from page-locked memory, back to back:
+    # the batching adapter's kind of kernel) occupies the GPU; the resident service withdraws a request
+    # it could not serve within 2 ms and the call takes the launch path
+    lib.bl_hook_latency_loaded.argtypes = [C.c_int, C.c_int, C.c_long, C.POINTER(C.c_double)]
+    lo = (C.c_double * 9)()
+    rc = lib.bl_hook_latency_loaded(dev_index, 4096, 2000, lo)
+    leg["under_bulk_load"] = {"error": rc} if rc else {
+        "bulk": "fecgpu_rlc_encode_host, 4096 blocks k16 r4 L1200 per call, page-locked, back to back",
+        "generate_us_p50": lo[0], "generate_us_p99": lo[1], "recover_us_p50": lo[3], "recover_us_p99": lo[4],
+        "bulk_calls_meanwhile": int(lo[7]), "requests_withdrawn_at_deadline": int(lo[8])}
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
     if os.path.exists(ref_path):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

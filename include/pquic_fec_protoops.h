@@ -116,9 +116,12 @@ protoop_arg_t pquic_fec_xor_recover(picoquic_cnx_t *cnx);
  * (incoming_encrypted.c:29-33, schedule_frames_on_path.c:47). */
 protoop_arg_t pquic_fec_packet_payload_to_source_symbol(picoquic_cnx_t *cnx);
 
-/* Counters of adapter activity (calls, blocks the reference would have crashed on). */
+/* Counters of adapter activity (calls, blocks the reference would have crashed on; calls whose request
+ * the resident block service withdrew at its deadline, which then took the launch path --
+ * fecgpu_block_svc_set_deadline). */
 typedef struct {
     uint64_t generate_calls, recover_calls, recovered_symbols, ref_ub_blocks, errors;
+    uint64_t svc_deadline_misses;
 } pquic_fec_protoop_stats_t;
 void pquic_fec_protoop_stats(pquic_fec_protoop_stats_t *out);
 

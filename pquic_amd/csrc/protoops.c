@@ -84,6 +84,9 @@ void pquic_fec_protoop_stats(pquic_fec_protoop_stats_t *out) {
     out->recovered_symbols = __atomic_load_n(&g_fec_stats.recovered_symbols, __ATOMIC_RELAXED);
     out->ref_ub_blocks = __atomic_load_n(&g_fec_stats.ref_ub_blocks, __ATOMIC_RELAXED);
     out->errors = __atomic_load_n(&g_fec_stats.errors, __ATOMIC_RELAXED);
+    pthread_mutex_lock(&g_mu);
+    out->svc_deadline_misses = g_svc ? fecgpu_block_svc_deadline_misses(g_svc) : 0;
+    pthread_mutex_unlock(&g_mu);
 }
 
 int pquic_fec_layout(uint64_t out[8]) {

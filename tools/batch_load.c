@@ -654,6 +654,52 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
     return 0;
 }
 
+/* The synchronous hooks while a bulk job occupies the same GPU: a background thread runs back-to-back
+ * fecgpu_rlc_encode_host calls of `bulk_blocks` k16 r4 L1200 blocks in page-locked host memory (the
+ * batching adapter's kind of job: kernels reading their rows over PCIe, ~2 ms per 4096 blocks) while
+ * this thread times `ncalls` generate and recover hooks exactly as bl_hook_latency does.
+ * out: [0..6] as bl_hook_latency, [7] bulk calls completed meanwhile, [8] hook requests the resident
+ * block service withdrew at its deadline (those calls took the launch path).  Returns 0 or -1. */
+struct bulk_arg { int device, blocks; volatile int stop; long calls; int rc; };
+static void *bulk_main(void *p) {
+    struct bulk_arg *a = p;
+    const size_t sb = (size_t)a->blocks * 16 * 1200, rb = (size_t)a->blocks * 4 * 1200;
+    fecgpu_host_ctx_t *c = fecgpu_host_ctx_create(a->device, 2, (size_t)64 << 20);
+    uint8_t *src = fecgpu_host_alloc(sb), *rep = fecgpu_host_alloc(rb);
+    if (!c || !src || !rep) {
+        a->rc = -1;
+    } else {
+        xorshift_fill(src, sb, 0x5EEDF3C0);
+        while (!a->stop) {
+            if (fecgpu_rlc_encode_host(c, src, rep, (uint64_t)a->blocks, 16, 4, 1200, 0, NULL)) { a->rc = -1; break; }
+            a->calls++;
+        }
+    }
+    fecgpu_host_free(src);
+    fecgpu_host_free(rep);
+    if (c) fecgpu_host_ctx_destroy(c);
+    return NULL;
+}
+
+int bl_hook_latency_loaded(int device, int bulk_blocks, long ncalls, double out[9]) {
+    struct bulk_arg a = {device, bulk_blocks, 0, 0, 0};
+    pthread_t th;
+    pquic_fec_protoop_stats_t s0, s1;
+    pquic_fec_protoop_stats(&s0);
+    if (pthread_create(&th, NULL, bulk_main, &a)) return -1;
+    while (a.calls < 2 && !a.rc) {  /* the bulk job is running */
+        struct timespec ts = {0, 1000000};
+        nanosleep(&ts, NULL);
+    }
+    const int rc = a.rc ? -1 : bl_hook_latency(device, 16, 4, 1200, 4, ncalls, out);
+    a.stop = 1;
+    pthread_join(th, NULL);
+    pquic_fec_protoop_stats(&s1);
+    out[7] = (double)a.calls;
+    out[8] = (double)(s1.svc_deadline_misses - s0.svc_deadline_misses);
+    return rc || a.rc ? -1 : 0;
+}
+
 /* Where the last bl_run's measured pass spent its time: out[0] engine-thread us (all engines, inside
  * the engine calls), [1] stager-thread us, [2] caller-thread us in completions, [3] wall us, [4] caller
  * us waiting for a free block slot (completions inside it included), [5] caller us in submissions. */
