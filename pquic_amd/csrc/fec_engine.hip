@@ -2287,6 +2287,17 @@ struct Bs2Lanes {
 
 static inline uint32_t bs2_slot_bytes(int) { return FEC_BS2_SLOT; }  // the bodies address slots by immediates
 
+// The lane id recomputed on the spot (v_mbcnt), opaque to the compiler: the RT = 16 ring bodies
+// leave it v0-v7, and their own lane arguments take six of those, so a lane-derived value the
+// compiler keeps live across a body (a hoisted 16 * (lane + 64), a block's header bytes) is spilled
+// to scratch and reloaded per item.  Deriving the lane values afresh per item / after the loop keeps
+// nothing per lane live across the asm.
+__device__ __forceinline__ int lane_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 #define BS2_LANE_ARGS ln.g1, ln.g2, ln.vmlo, ln.vmhi, ln.rd1, ln.rd2, ln.off0, ln.off1, ln.vm0, ln.vm1
 #define BS2_CALL_ENC(RT, ND) \
   bs2_enc_r##RT##_d##ND(sp, rpp, (uint32_t)L, rslo, rshi, sdl, ll, (uint32_t)rt, nsrc, (uint32_t)k, ca, ring, \
@@ -2377,7 +2388,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
         const int g = it / nchunks, ch = it - g * nchunks;
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-        const Bs2Lanes ln(lane, cb, 0u, ring);
+        const Bs2Lanes ln(lane_fresh(), cb, 0u, ring);
         const uint64_t b = b0 + g * bstep;
         const uint64_t sp = (uint64_t)(uintptr_t)(src + b * sbs + c0);
         const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b * (uint64_t)r + r0) * (uint64_t)L + c0);
@@ -2388,7 +2399,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
       for (int ch = 0; ch < nchunks; ch++) {
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-        const Bs2Lanes ln(lane, cb, 0u, ring);
+        const Bs2Lanes ln(lane_fresh(), cb, 0u, ring);
         const uint64_t sp = (uint64_t)(uintptr_t)(src + b0 * sbs + c0);
         const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b0 * (uint64_t)r + r0) * (uint64_t)L + c0);
         const uint64_t rstep = bstep * (uint64_t)r * L;
@@ -2493,7 +2504,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
         const int t = it / nchunks, ch = it - t * nchunks;
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-        const Bs2Lanes ln(lane, cb, (uint32_t)c0, ring);
+        const Bs2Lanes ln(lane_fresh(), cb, (uint32_t)c0, ring);
         bs2_dec_call(ln.npieces > 64, lds_addr(S.intab + (size_t)t * k), lds_addr(S.rec + (size_t)t * kDecRec),
                      (uint32_t)k, k, lds_addr(S.coef + (size_t)t * k * RecoverLds<RT>::CSB), ring, ln);
       }
@@ -2501,7 +2512,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
       for (int ch = 0; ch < nchunks; ch++) {
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
-        const Bs2Lanes ln(lane, cb, (uint32_t)c0, ring);
+        const Bs2Lanes ln(lane_fresh(), cb, (uint32_t)c0, ring);
         bs2_dec_call(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
                          lds_addr(S.coef), ring, ln);
       }
@@ -2509,11 +2520,14 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
     __syncthreads();
     if (wave != 0) return;
     if (status) {
-      if (lane < ng) {
-        const uint64_t b = b0 + lane * bstep;
+      const int ln0 = lane_fresh();  // the header bytes read again rather than kept across the bodies
+      if (ln0 < ng) {
+        const uint64_t b = b0 + ln0 * bstep;
+        const uint8_t *h = ws + b * (uint64_t)WL.stride;
+        const int st = h[0], e = h[1];
         uint64_t m0 = 0, m1 = 0;
-        if (act) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
-          const int t = __popcll(am & ((1ull << lane) - 1));
+        if (st == FECGPU_BLOCK_RECOVERED && e > r0) {  // rlc_fec_scheme_gf256.c:98-101, 218-236 (see rlc_finalize_block)
+          const int t = __popcll(am & ((1ull << ln0) - 1));
           const uint8_t *nzf = S.rec + (size_t)t * kDecRec + kDecRecNz;
           uint32_t det = 0;
           for (int u = e - 1; u >= 0; u--) {
@@ -2529,7 +2543,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
         recovered[2 * b + 1] = m1;
       }
     } else {
-      for (int x = lane; x < nact * 16; x += 64) {
+      for (int x = lane_fresh(); x < nact * 16; x += 64) {
         const uint8_t *rc = S.rec + (size_t)(x >> 4) * kDecRec;
         if (rc[kDecRecNz + (x & 15)])
           reinterpret_cast<uint8_t *>(reinterpret_cast<const uint64_t *>(rc)[kDecRecNzPtr])[x & 15] = 1;
