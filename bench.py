@@ -597,12 +597,13 @@ def hook_latency_legs(dev_index):
     # the batching adapter's kind of kernel) occupies the GPU; the resident service withdraws a request
     # it could not serve within 2 ms and the call takes the launch path
     lib.bl_hook_latency_loaded.argtypes = [C.c_int, C.c_int, C.c_long, C.POINTER(C.c_double)]
-    lo = (C.c_double * 9)()
+    lo = (C.c_double * 11)()
     rc = lib.bl_hook_latency_loaded(dev_index, 4096, 2000, lo)
     leg["under_bulk_load"] = {"error": rc} if rc else {
         "bulk": "fecgpu_rlc_encode_host, 4096 blocks k16 r4 L1200 per call, page-locked, back to back",
         "generate_us_p50": lo[0], "generate_us_p99": lo[1], "recover_us_p50": lo[3], "recover_us_p99": lo[4],
-        "bulk_calls_meanwhile": int(lo[7]), "requests_withdrawn_at_deadline": int(lo[8])}
+        "bulk_calls_meanwhile": int(lo[7]), "bulk_ms_per_call_mean": round(lo[9], 3),
+        "bulk_ms_per_call_max": round(lo[10], 3), "requests_withdrawn_at_deadline": int(lo[8])}
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
     if os.path.exists(ref_path):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -235,8 +235,9 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *ctx, void *src, const void *rep, u
  * One block per call, as the block framework calls fec_generate_repair_symbols / fec_recover
  * (block_framework_sender.h:187, fec_protoops.h:246): a worker workgroup stays resident on the device
  * and polls a page-locked mailbox, so a call costs a mailbox round trip over PCIe instead of a
- * kernel launch.  The worker ends by itself after 20 ms without a request (and after 2 s in all);
- * the next call relaunches it.  Every buffer must be page-locked (fecgpu_host_alloc, registered
+ * kernel launch.  The worker ends by itself after 20 ms without a request (and after 50 ms in all);
+ * the next call relaunches it.  It runs on a stream of the greatest priority (its own hardware queue
+ * unless the process creates other such streams), so the process's other kernels do not queue behind it.  Every buffer must be page-locked (fecgpu_host_alloc, registered
  * ranges); the rows are zero-copy.  Returns FECGPU_ERR_INVALID when the block does not fit the
  * worker (e > 16 unknowns, rows beyond its LDS), a buffer is not page-locked, knob block_svc is 0, or
  * the request was withdrawn at its deadline (below) -- the caller then takes the host path.

@@ -3572,9 +3572,12 @@ static uint64_t svc_now_us() {
 // scheduled within the deadline is most likely queued behind a long kernel, and so would the next be
 constexpr uint64_t kSvcBackoffUs = 50000;
 
-// worker lifetime: ends after 20 ms without a request (the next call relaunches it) and after 2 s
-// in all, so no launch outlives its caller by more than that (s_memrealtime: 100 MHz)
-constexpr uint64_t kSvcIdleTicks = 2000000, kSvcLifeTicks = 200000000;
+// worker lifetime: ends after 20 ms without a request (the next call relaunches it) and after 50 ms
+// in all (s_memrealtime: 100 MHz).  The worker runs on a stream of the greatest priority, which the
+// runtime maps to a hardware queue of its own unless the process creates other such streams; should
+// it share one, kernels queued behind the resident worker wait at most its lifetime (sustained hook
+// traffic then pays one relaunch per 50 ms).
+constexpr uint64_t kSvcIdleTicks = 2000000, kSvcLifeTicks = 5000000;
 constexpr uint32_t kSvcLds = 60 * 1024;  // dynamic LDS of the worker (the mailbox copy is static)
 
 fecgpu_block_svc_t *fecgpu_block_svc_create(int device) {
@@ -3583,7 +3586,9 @@ fecgpu_block_svc_t *fecgpu_block_svc_create(int device) {
   if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
   auto *v = new fecgpu_block_svc;
   v->device = device;
-  bool ok = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess &&
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  bool ok = hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
             hipEventCreateWithFlags(&v->ev, hipEventDisableTiming) == hipSuccess &&
             hipHostMalloc((void **)&v->mb, sizeof(BlockSvcMailbox), hipHostMallocDefault) == hipSuccess;
   if (ok) {

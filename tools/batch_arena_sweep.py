@@ -45,11 +45,12 @@ for nconn in (64, 512):
         line(f"rec {nconn:3d} conn e4 batch 4096 {'registered' if reg & 1 else 'staged'} rc {rc}", out, rows)
         print(f"    recovered symbols {out[6]:.0f}", flush=True)
 for bulk in (0, 4096):
-    out = (C.c_double * 9)()
+    out = (C.c_double * 11)()
     if bulk:
         rc = lib.bl_hook_latency_loaded(0, bulk, 2000, out)
     else:
         lib.bl_hook_latency.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_long, D]
         rc = lib.bl_hook_latency(0, 16, 4, 1200, 4, 2000, out)
     print(f"hooks, bulk {bulk:4d} blocks: rc {rc} generate p50 {out[0]:.0f} p99 {out[1]:.0f} us, recover p50 "
-          f"{out[3]:.0f} p99 {out[4]:.0f} us, bulk calls {out[7]:.0f}, withdrawn {out[8]:.0f}", flush=True)
+          f"{out[3]:.0f} p99 {out[4]:.0f} us, bulk calls {out[7]:.0f} (mean {out[9]:.2f} max {out[10]:.2f} ms), "
+          f"withdrawn {out[8]:.0f}", flush=True)

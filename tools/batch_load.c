@@ -658,9 +658,17 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
  * fecgpu_rlc_encode_host calls of `bulk_blocks` k16 r4 L1200 blocks in page-locked host memory (the
  * batching adapter's kind of job: kernels reading their rows over PCIe, ~2 ms per 4096 blocks) while
  * this thread times `ncalls` generate and recover hooks exactly as bl_hook_latency does.
- * out: [0..6] as bl_hook_latency, [7] bulk calls completed meanwhile, [8] hook requests the resident
- * block service withdrew at its deadline (those calls took the launch path).  Returns 0 or -1. */
-struct bulk_arg { int device, blocks; volatile int stop; long calls; int rc; };
+ * out: [0..6] as bl_hook_latency, [7] bulk calls started while the hooks ran, [8] hook requests the
+ * resident block service withdrew at its deadline (those calls took the launch path), [9] / [10] mean /
+ * max ms of those bulk calls (how long the hooks' worker held the bulk job up).  Returns 0 or -1. */
+struct bulk_arg {
+    int device, blocks;
+    volatile int stop, window;  /* window: the hooks are being timed */
+    volatile long calls;
+    long in_window;
+    double sum_ms, max_ms;
+    int rc;
+};
 static void *bulk_main(void *p) {
     struct bulk_arg *a = p;
     const size_t sb = (size_t)a->blocks * 16 * 1200, rb = (size_t)a->blocks * 4 * 1200;
@@ -671,7 +679,15 @@ static void *bulk_main(void *p) {
     } else {
         xorshift_fill(src, sb, 0x5EEDF3C0);
         while (!a->stop) {
+            const int w = a->window;
+            const uint64_t t0 = now_us();
             if (fecgpu_rlc_encode_host(c, src, rep, (uint64_t)a->blocks, 16, 4, 1200, 0, NULL)) { a->rc = -1; break; }
+            const double ms = (now_us() - t0) * 1e-3;
+            if (w) {  /* a call started while the hooks were timed (one held up past the window included) */
+                a->in_window++;
+                a->sum_ms += ms;
+                if (ms > a->max_ms) a->max_ms = ms;
+            }
             a->calls++;
         }
     }
@@ -681,8 +697,8 @@ static void *bulk_main(void *p) {
     return NULL;
 }
 
-int bl_hook_latency_loaded(int device, int bulk_blocks, long ncalls, double out[9]) {
-    struct bulk_arg a = {device, bulk_blocks, 0, 0, 0};
+int bl_hook_latency_loaded(int device, int bulk_blocks, long ncalls, double out[11]) {
+    struct bulk_arg a = {device, bulk_blocks, 0, 0, 0, 0, 0.0, 0.0, 0};
     pthread_t th;
     pquic_fec_protoop_stats_t s0, s1;
     pquic_fec_protoop_stats(&s0);
@@ -691,12 +707,16 @@ int bl_hook_latency_loaded(int device, int bulk_blocks, long ncalls, double out[
         struct timespec ts = {0, 1000000};
         nanosleep(&ts, NULL);
     }
+    a.window = 1;
     const int rc = a.rc ? -1 : bl_hook_latency(device, 16, 4, 1200, 4, ncalls, out);
+    a.window = 0;
     a.stop = 1;
     pthread_join(th, NULL);
     pquic_fec_protoop_stats(&s1);
-    out[7] = (double)a.calls;
+    out[7] = (double)a.in_window;
     out[8] = (double)(s1.svc_deadline_misses - s0.svc_deadline_misses);
+    out[9] = a.in_window ? a.sum_ms / a.in_window : 0;
+    out[10] = a.max_ms;
     return rc || a.rc ? -1 : 0;
 }
 

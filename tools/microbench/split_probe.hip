@@ -57,6 +57,37 @@ __global__ __launch_bounds__(64) void col(const uint8_t *__restrict__ src, uint8
   }
 }
 
+// colU / adj Wn: col's one wave per block with U rows in flight; adj packs W such waves in a workgroup
+// on adjacent blocks (wave w of workgroup q: block q W + w) -- fewer distinct regions in flight without
+// any reduction between the waves.
+template <int U, int W>
+__global__ __launch_bounds__(64 * W) void adj(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep, uint64_t nb) {
+  const int lane = threadIdx.x & 63;
+  if (lane >= A) return;
+  const uint32_t o0 = 16 * lane, o1 = 16 * (lane + A);
+  const bool ok1 = lane + A < L / 16;
+  const uint64_t b = (uint64_t)blockIdx.x * W + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  u32x4 x0 = 0, x1 = 0;
+  for (int j0 = 0; j0 < K; j0 += U) {
+    u32x4 a0[U], a1[U];
+#pragma unroll
+    for (int jj = 0; jj < U; jj++) {
+      const uint8_t *p = src + (b * K + j0 + jj) * (uint64_t)L;
+      a0[jj] = ld<true>((const u32x4 *)(p + o0));
+      a1[jj] = ok1 ? ld<true>((const u32x4 *)(p + o1)) : (u32x4)0;
+    }
+#pragma unroll
+    for (int jj = 0; jj < U; jj++) { x0 ^= a0[jj]; x1 ^= a1[jj]; }
+  }
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    uint8_t *p = rep + (b * R + i) * (uint64_t)L;
+    __builtin_nontemporal_store(x0 + (uint32_t)i, (u32x4 *)(p + o0));
+    if (ok1) __builtin_nontemporal_store(x1 + (uint32_t)i, (u32x4 *)(p + o1));
+  }
+}
+
 template <int W, bool NT>
 __global__ __launch_bounds__(64 * W) void split(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep, uint64_t nb) {
   __shared__ u32x4 red[2][W][2][64];
@@ -121,7 +152,8 @@ __global__ __launch_bounds__(64 * W) void lin(const uint8_t *__restrict__ src, u
   }
 }
 
-int main() {
+int main(int argc, char **argv) {
+  const bool adj_only = argc > 1;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const uint64_t nb = (uint64_t)(1 << 20) * 16 / K;  // 2^20 blocks at k16, 2^19 at k32 (19.3 GB)
@@ -130,7 +162,7 @@ int main() {
   CK(hipMemset(src, 3, nb * K * L)); CK(hipMemset(rep, 5, nb * R * L));
   const double bytes = (double)nb * (K + R) * L;
   printf("# k%d r%d L%d, %llu blocks, %.2f GB per launch\n", K, R, L, (unsigned long long)nb, bytes / 1e9);
-  auto run = [&](const char *name, auto kern, int W, size_t lds_per_wave, size_t stat) {
+  auto run = [&](const char *name, auto kern, int W, size_t lds_per_wave, size_t stat, int per_wg = 1) {
     // grid: one workgroup per block (the engine's one-group-per-workgroup launch); dynamic LDS tops
     // the kernel's static LDS up to lds_per_wave per wave
     const size_t lds = lds_per_wave * W > stat ? lds_per_wave * W - stat : 0;
@@ -138,7 +170,7 @@ int main() {
     int n = 0;
     for (int it = 0; it < 5; it++) {
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(kern, dim3((uint32_t)nb), dim3(64 * W), lds, 0, src, rep, nb);
+      hipLaunchKernelGGL(kern, dim3((uint32_t)((nb + per_wg - 1) / per_wg)), dim3(64 * W), lds, 0, src, rep, nb);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       if (it) { best = std::min(best, ms); sum += ms; n++; }
@@ -153,14 +185,27 @@ int main() {
 #define RUNK(NAME, KERN, W, STAT)                                \
       snprintf(nm, sizeof nm, "%-22s %d waves/SIMD", NAME, wps); \
       run(nm, KERN, W, per, STAT);
+#define RUNA(NAME, KERN, W)                                      \
+      snprintf(nm, sizeof nm, "%-22s %d waves/SIMD", NAME, wps); \
+      run(nm, KERN, W, per, 0, W);
       RUNK("col G1", col, 1, 0)
-      RUNK("split W2 nt", (split<2, true>), 2, 4096 * 2)
+      if (!adj_only) {
+        RUNK("split W2 nt", (split<2, true>), 2, 4096 * 2)
+        RUNK("split W4 nt", (split<4, true>), 4, 4096 * 4)
+        RUNK("split W4 default", (split<4, false>), 4, 4096 * 4)
+        RUNK("split W8 nt", (split<8, true>), 8, 4096 * 8)
+        RUNK("lin W1", lin<1>, 1, 0)
+        RUNK("lin W4", lin<4>, 4, 0)
+        RUNK("lin W8", lin<8>, 8, 0)
+      }
+      RUNA("adj U8 W1", (adj<8, 1>), 1)
+      RUNA("adj U16 W1", (adj<16, 1>), 1)
+      RUNA("adj U4 W1", (adj<4, 1>), 1)
+      RUNA("adj U8 W2", (adj<8, 2>), 2)
+      RUNA("adj U8 W4", (adj<8, 4>), 4)
+      RUNA("adj U8 W8", (adj<8, 8>), 8)
+      RUNA("adj U16 W4", (adj<16, 4>), 4)
       RUNK("split W4 nt", (split<4, true>), 4, 4096 * 4)
-      RUNK("split W4 default", (split<4, false>), 4, 4096 * 4)
-      RUNK("split W8 nt", (split<8, true>), 8, 4096 * 8)
-      RUNK("lin W1", lin<1>, 1, 0)
-      RUNK("lin W4", lin<4>, 4, 0)
-      RUNK("lin W8", lin<8>, 8, 0)
     }
   }
   return 0;
