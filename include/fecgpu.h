@@ -297,8 +297,8 @@ int fecgpu_host_device_address(const void *p, size_t bytes, uint64_t *dev);
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream);
 
 /* Experiment knobs (A/B runs, cross-checks of alternative kernels in the tests).  Every knob has
- * a measured default; the environment variable named in DESIGN.md §6.1 seeds it ONCE per process
- * (first engine call), after which only these calls change it.  Names and accepted values:
+ * a measured default and only these calls change it (the library reads no environment variables;
+ * tools/ab_inproc.py maps the FECGPU_* names of earlier rounds onto them).  Names and accepted values:
  * "plan" (0 auto, 1 wave in LDS, 2 lane, 3 reg, 4 tile, 5 wave in registers where it fits),
  * "interleave" (0/1), "group" (0 = defaults, else a cap on blocks per group), "enc_tile_rt" (0 =
  * default tiling, else 1/2/4/8/16) / "enc_tile_waves" (0..4), "zc_read" (0/1), "ring" (the LDS-ring

@@ -51,8 +51,8 @@ static std::atomic<uint64_t> g_stats[4];
 
 // ---------------------------------------------------------------------------------------------
 // Experiment knobs (A/B runs; the tests cross-check alternative kernels).  The defaults are the
-// measured best.  They are read from the environment ONCE, on first use, so the engine's behaviour
-// cannot drift between calls; fecgpu_set_knob changes one explicitly (include/fecgpu.h).
+// measured best, and only fecgpu_set_knob changes one (include/fecgpu.h): the library reads no
+// environment variables, so nothing outside the caller's own calls can change which kernels run.
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_N };
@@ -63,49 +63,40 @@ enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4,
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
 
-static void knobs_from_env() {
-  auto num = [](const char *v, int def) { return v ? atoi(v) : def; };
-  const char *e;
-  e = getenv("FECGPU_PLAN");
-  g_knob[K_PLAN] = !e ? PLAN_AUTO : !strcmp(e, "wave") ? PLAN_WAVE : !strcmp(e, "lane") ? PLAN_LANE
-                 : !strcmp(e, "reg") ? PLAN_REG : !strcmp(e, "tile") ? PLAN_TILE
-                 : !strcmp(e, "wreg") ? PLAN_WREG : PLAN_AUTO;
-  g_knob[K_INTERLEAVE] = num(getenv("FECGPU_INTERLEAVE"), 1) != 0;
-  g_knob[K_GROUP] = num(getenv("FECGPU_GROUP"), 0);  // 0: the measured per-shape defaults
-  int a = 0, b = 0;
-  if ((e = getenv("FECGPU_ENC_TILE")) && sscanf(e, "%d,%d", &a, &b) == 2 &&
-      (a == 1 || a == 2 || a == 4 || a == 8 || a == 16) && b >= 1 && b <= 4) {
-    g_knob[K_ENC_RT] = a;
-    g_knob[K_ENC_W] = b;
-  }
-  g_knob[K_ZC_READ] = num(getenv("FECGPU_ZC_READ"), 1) != 0;
+static void knobs_default() {
+  g_knob[K_PLAN] = PLAN_AUTO;  // plan kernel by batch size and shape
+  g_knob[K_INTERLEAVE] = 1;    // interleaved block groups
+  g_knob[K_GROUP] = 0;         // 0: the measured per-shape group sizes
+  g_knob[K_ENC_RT] = 0;        // encode tiles by r (0), one wave per group (enc_tile_waves 0)
+  g_knob[K_ENC_W] = 0;
+  g_knob[K_ZC_READ] = 1;       // page-locked host buffers read by the kernels in place
   // LDS-ring data path (bs2 bodies) for 16-repair / 16-unknown tiles: 2 (default) on, 0 off
-  g_knob[K_RING] = num(getenv("FECGPU_RING"), 2) ? 2 : 0;
+  g_knob[K_RING] = 2;
   // window encode on the shared-coefficient kernel (k_rlc_encode_sc): 0 never, 1 (default) for
   // overlapping windows, 2 wherever it applies (tests)
-  g_knob[K_WINDOW_SC] = num(getenv("FECGPU_WINDOW_SC"), 1);
+  g_knob[K_WINDOW_SC] = 1;
   // batches too small to fill the chip stream fewer blocks per wave: groups of blocks shrink until
   // there are at least this many groups (0: the per-shape group sizes at every batch size)
-  g_knob[K_MIN_GROUPS] = num(getenv("FECGPU_MIN_GROUPS"), 1024);
+  g_knob[K_MIN_GROUPS] = 1024;
   // ring tiles of symbols wider than one column chunk: one wave per chunk of a block at once (1) or
   // one wave coding the chunks in turn (0)
-  g_knob[K_CHUNK_WAVES] = num(getenv("FECGPU_CHUNK_WAVES"), 1) != 0;
+  g_knob[K_CHUNK_WAVES] = 1;
   // batches of <= kSmallLdsMaxBlocks blocks: rows staged in LDS by a workgroup per block (1) or the
   // bitsliced one-wave-per-block kernels (0)
-  g_knob[K_SMALL_LDS] = num(getenv("FECGPU_SMALL_LDS"), 1) != 0;
+  g_knob[K_SMALL_LDS] = 1;
   // fecgpu_block_svc_*: the resident worker serves requests (1) or every call returns
   // FECGPU_ERR_INVALID so the caller takes the launch path (0)
-  g_knob[K_BLOCK_SVC] = num(getenv("FECGPU_BLOCK_SVC"), 1) != 0;
+  g_knob[K_BLOCK_SVC] = 1;
   // recover data pass: a group's workspace records copied into LDS in one round trip (1) or read
   // where they lie during the setup (0)
-  g_knob[K_WS_LDS] = num(getenv("FECGPU_WS_LDS"), 1) != 0;
+  g_knob[K_WS_LDS] = 1;
   // recover data pass (register-prefetch bodies): 0 = the occupancy its registers allow, n = at most
   // n waves per SIMD
-  g_knob[K_DEC_WAVES] = num(getenv("FECGPU_DEC_WAVES"), 0);
+  g_knob[K_DEC_WAVES] = 0;
 }
 
 static inline int knob(KnobId id) {
-  std::call_once(g_knob_once, knobs_from_env);
+  std::call_once(g_knob_once, knobs_default);
   return g_knob[id].load(std::memory_order_relaxed);
 }
 
@@ -2938,7 +2929,7 @@ const char *fecgpu_version(void) { return FECGPU_VERSION; }
 const char *fecgpu_last_error(void) { return g_err; }
 
 int fecgpu_init(int device) {
-  std::call_once(g_knob_once, knobs_from_env);
+  std::call_once(g_knob_once, knobs_default);
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device)
     return set_err(FECGPU_ERR_NO_DEVICE, "%s", "no HIP device");
@@ -2954,7 +2945,7 @@ int fecgpu_init(int device) {
   return rc;
 }
 
-// The values each knob accepts (the same ranges knobs_from_env admits): a tile of 3 repairs would
+// The values each knob accepts: a tile of 3 repairs would
 // dispatch a 16-repair body while stepping r0 by 3, a negative group cap would become a huge
 // unsigned one.
 static bool knob_value_ok(int id, int v) {
@@ -2971,7 +2962,7 @@ static bool knob_value_ok(int id, int v) {
 }
 
 int fecgpu_set_knob(const char *name, int value) {
-  std::call_once(g_knob_once, knobs_from_env);
+  std::call_once(g_knob_once, knobs_default);
   for (int i = 0; i < K_N; i++)
     if (name && !strcmp(name, kKnobName[i])) {
       if (!knob_value_ok(i, value)) return set_err(FECGPU_ERR_INVALID, "value out of range for knob %s", name);
@@ -2982,7 +2973,7 @@ int fecgpu_set_knob(const char *name, int value) {
 }
 
 int fecgpu_get_knob(const char *name, int *value) {
-  std::call_once(g_knob_once, knobs_from_env);
+  std::call_once(g_knob_once, knobs_default);
   for (int i = 0; i < K_N; i++)
     if (name && value && !strcmp(name, kKnobName[i])) {
       *value = g_knob[i].load(std::memory_order_relaxed);

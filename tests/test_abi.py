@@ -139,3 +139,15 @@ def test_generated_bodies_match_generator(tmp_path):
     subprocess.run([sys.executable, gen], check=True, env=env, capture_output=True)
     with open(os.path.join(root, "pquic_amd", "csrc", "bitslice_gen.h")) as f:
         assert out.read_text() == f.read()
+
+
+def test_knobs_are_not_read_from_the_environment(lib):
+    """The engine's kernel choices change only through fecgpu_set_knob: no FECGPU_* environment name
+    is left in the library (the batching adapter's thread counts, PQUIC_FEC_BATCH_*, are its only
+    environment settings), and a knob keeps its default whatever the environment holds."""
+    data = open(LIB, "rb").read()
+    names = set(re.findall(rb"FECGPU_[A-Z_]{3,}", data))
+    assert not {n for n in names if not n.startswith((b"FECGPU_ERR", b"FECGPU_OK", b"FECGPU_BLOCK"))}, names
+    v = C.c_int(-1)
+    lib.fecgpu_get_knob.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
+    assert lib.fecgpu_get_knob(b"min_groups", C.byref(v)) == 0 and v.value == 1024
