@@ -395,6 +395,12 @@ int mh_batch_connections(int n, size_t bytes) {
     return 0;
 }
 
+/* connection i closes: its arena leaves the batcher's registry (its rows are staged from then on) */
+int mh_batch_unregister_connection(int i) {
+    if (i < 0 || i >= g_ncnx) return -1;
+    return pquic_fec_batch_unregister_heap(g_batcher, g_cnxs[i].arena->base);
+}
+
 int mh_batch_use_connection(int i) {
     if (i >= g_ncnx) return -1;
     g_cur = i < 0 ? &g_bcnx : &g_cnxs[i];

@@ -281,11 +281,25 @@ def _decode_jobs():
     return jobs
 
 
+def _recover_on(bt, conns, i, *args, now=0):
+    """bt.recover on connection i % conns (its own registered arena: the gather path), or on the
+    default connection (no arena registered: rows staged) when conns is 0."""
+    if conns:
+        bt.use(i % conns)
+    return bt.recover(*args, now=now)
+
+
+@pytest.mark.parametrize("conns", [0, 3])
 @pytest.mark.parametrize("batch_blocks", [3, 128])
-def test_batch_recover_matches_reference(batch_blocks):
-    bt = Batch(batch_blocks)
-    jobs = _decode_jobs()
-    tickets = [bt.recover(c["scheme"] == "xor", c["fbn"], s, r, f, now=i) for i, (c, s, r, f) in enumerate(jobs)]
+def test_batch_recover_matches_reference(batch_blocks, conns):
+    """Every reference decode fixture (crash patterns included) through the batcher, rows staged
+    (conns 0) or read and written in place in per-connection arenas (conns 3)."""
+    # the gather path reads rows in place only at the batch stride: 1200-B cases (the others stay
+    # covered staged, conns 0)
+    bt = Batch(batch_blocks, max_symbol=1200 if conns else 9000, connections=conns, conn_bytes=16 << 20)
+    jobs = [j for j in _decode_jobs() if not conns or max([len(x) for x in j[1] + j[2] if x is not None] + [1]) <= 1200]
+    tickets = [_recover_on(bt, conns, i, c["scheme"] == "xor", c["fbn"], s, r, f, now=i)
+               for i, (c, s, r, f) in enumerate(jobs)]
     bt.L.mh_batch_drain()
     n = 0
     for t, (case, srcs, _, _) in zip(tickets, jobs):
@@ -301,7 +315,9 @@ def test_batch_recover_matches_reference(batch_blocks):
         present = sum(s is not None for s in srcs)
         assert cur == (present + len(rec) if case["scheme"] == "rlc" else present)
         n += 1
-    assert n > 350
+    assert n > (200 if conns else 350)
+    if conns:
+        assert bt.stats()["rows_in_place"] > 1000
     bt.close()
 
 
@@ -358,21 +374,26 @@ def test_batch_mixed_keys_and_symbol_cap():
     bt.close()
 
 
+@pytest.mark.parametrize("conns", [0, 3])
 @pytest.mark.parametrize("batch_blocks", [4, 64])
-def test_batch_recover_window_framework_blocks(batch_blocks):
+def test_batch_recover_window_framework_blocks(batch_blocks, conns):
     """The batcher on window-framework-shaped blocks (window_cases.json): block numbered by its
     window start, repairs seeded by their own FPIDs (block number 0, or mixed), mixed in one
-    queue with block-framework blocks of the same (k, r)."""
-    bt = Batch(batch_blocks)
+    queue with block-framework blocks of the same (k, r); rows staged (conns 0) or on the gather
+    path in per-connection arenas (conns 3)."""
+    bt = Batch(batch_blocks, max_symbol=1200 if conns else 9000, connections=conns, conn_bytes=16 << 20)
     o = Oracle()
     d = load("window_cases.json")
     jobs = []
     for i, case in enumerate(d["cases"]):
         srcs_full, reps_full, fpids = window_inputs(case, o)
+        if conns and max(len(x) for x in srcs_full + reps_full) > 1200:
+            continue
         k, r = case["k"], case["r"]
         srcs = [None if j in case["src_missing"] else srcs_full[j] for j in range(k)]
         reps = [reps_full[i2] if i2 in case["rep_present"] else None for i2 in range(r)]
-        jobs.append((case, srcs, bt.recover(case["scheme"] == "xor", case["fbn"], srcs, reps, fpids, now=i)))
+        jobs.append((case, srcs, _recover_on(bt, conns, i, case["scheme"] == "xor", case["fbn"], srcs, reps, fpids,
+                                             now=i)))
     bt.L.mh_batch_drain()
     n = 0
     for case, srcs, t in jobs:
@@ -388,7 +409,9 @@ def test_batch_recover_window_framework_blocks(batch_blocks):
         present = sum(s is not None for s in srcs)
         assert cur == (present + len(rec) if case["scheme"] == "rlc" else present)
         n += 1
-    assert n > 150
+    assert n > (60 if conns else 150)
+    if conns:
+        assert bt.stats()["rows_in_place"] > 200
     bt.close()
 
 
@@ -667,4 +690,44 @@ def test_batch_completions_follow_submission_order():
     bt.L.mh_batch_drain()
     order = [bt.L.mh_batch_order(t) for t in tickets]
     assert order == sorted(order) and min(order) >= 0
+    bt.close()
+
+
+@pytest.mark.gpu
+def test_batch_connection_closes_arena_unregistered():
+    """A connection closing takes its arena out of the registry (pquic_fec_batch_unregister_heap) while
+    the others keep theirs: that connection's rows are staged from then on, the others' stay in place,
+    every repair still equals the reference's, and the range cannot be unregistered twice."""
+    ncon = 4
+    bt = Batch(8, max_symbol=1200, connections=ncon, conn_bytes=256 << 10)
+    bt.L.mh_batch_unregister_connection.argtypes = [C.c_int]
+    rng = np.random.default_rng(11)
+    o = Oracle()
+
+    def job():
+        srcs = [rng.integers(0, 256, 1200, dtype=np.uint8) for _ in range(6)]
+        fbn = int(rng.integers(0, 1 << 24))
+        rep = o.rlc_encode_batch(np.stack(srcs)[None], 3, fbn)[0]
+        return (False, fbn, srcs, 3, ("hex", [x.tobytes().hex() for x in rep]), [(fbn << 8) | i for i in range(3)], 0)
+
+    def run(conns):
+        done = []
+        for c in conns:
+            bt.use(c)
+            j = job()
+            done.append((bt.generate(*j[:4], now=len(done)), j))
+        bt.L.mh_batch_drain()
+        for t, j in done:
+            _check_generate(bt, t, j)
+
+    run(list(range(ncon)) * 4)
+    st0 = bt.stats()
+    assert st0["rows_staged"] == 0 and st0["rows_in_place"] == 16 * (6 + 3)
+    assert bt.L.mh_batch_unregister_connection(1) == 0
+    assert bt.L.mh_batch_unregister_connection(1) != 0  # not registered any more
+    run([0, 1, 2, 3, 1, 1])
+    st1 = bt.stats()
+    assert st1["rows_staged"] - st0["rows_staged"] == 3 * (6 + 3)
+    assert st1["rows_in_place"] - st0["rows_in_place"] == 3 * (6 + 3)
+    assert st1["engine_errors"] == 0
     bt.close()
