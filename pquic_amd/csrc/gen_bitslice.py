@@ -1210,6 +1210,11 @@ def main():
              "// L9000 encode / decode -1.2 % (profiles/r04_ab_ld_policy.log)",
              "#define FEC_LD_POL \" nt\"",
              "#endif",
+             "#ifndef FEC_LD_POL_SC",
+             "// the shared-coefficient window bodies keep the default policy: overlapping windows read each",
+             "// source row k / step times, the repeats from L2 (nt: k32 r8 step 8 14.96 -> 19.30 ms)",
+             "#define FEC_LD_POL_SC \"\"",
+             "#endif",
              "#ifndef FEC_LD_POL_COMPACT",
              "#define FEC_LD_POL_COMPACT FEC_LD_POL  // the compact-map bodies (8-repair encode tiles)",
              "#endif",
@@ -1280,6 +1285,7 @@ def main():
     for RT in (1, 2, 4, 8):
         P = prefetch_depth("enc", RT, 16)
         fn, top = emit_function("enc", RT, 16, P, sc=True)
+        fn = fn.replace('" FEC_LD_POL "', '" FEC_LD_POL_SC "')  # overlapping windows re-read rows from L2
         tops[("encsc", RT, 16, P)] = top
         parts.append(fn)
         parts.append("")
