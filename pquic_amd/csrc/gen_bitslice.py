@@ -1216,7 +1216,10 @@ def main():
              "#define FEC_LD_POL_SC \"\"",
              "#endif",
              "#ifndef FEC_LD_POL_COMPACT",
-             "#define FEC_LD_POL_COMPACT FEC_LD_POL  // the compact-map bodies (8-repair encode tiles)",
+             "// the compact-map bodies (8-repair encode tiles) keep the default policy: nt loads leave the k32 r8",
+             "// encode's time unchanged (+0.1 %, profiles/r04_ab_ld_policy2.log) and raise its HBM reads from",
+             "// 1.004x to 1.032x the algorithmic bytes (profiles/r04_pmc_nt.json)",
+             "#define FEC_LD_POL_COMPACT \"\"",
              "#endif",
              "#ifndef FEC_ST_POL",
              "#define FEC_ST_POL \" nt\"  // repair / recovered symbol stores",

@@ -88,6 +88,53 @@ __global__ __launch_bounds__(64 * W) void adj(const uint8_t *__restrict__ src, u
   }
 }
 
+// dec: the decode apply's pattern -- per block the k - E received sources (E = R erased, at rotating
+// slots) and the E repairs, read in slot order, and E recovered rows written packed to dst[b][E][L]
+// (the bench's apply); `sorted` reads the received sources first, then the repairs.
+template <bool SORTED>
+__global__ __launch_bounds__(64) void dec(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep, uint64_t nb) {
+  const int lane = threadIdx.x;
+  if (lane >= A) return;
+  const uint32_t o0 = 16 * lane, o1 = 16 * (lane + A);
+  const bool ok1 = lane + A < L / 16;
+  const uint64_t b = blockIdx.x;
+  const int e0 = (int)((b * 7) % K);  // erased sources e0, e0 + K/R, ... (mod K)
+  const uint8_t *rp = rep + b * (uint64_t)R * L;  // repairs read from rep; recovered rows written after them
+  uint8_t *dst = rep + (nb + b) * (uint64_t)R * L;
+  const uint8_t *rows[K];
+  int nr = 0, ne = 0;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    bool er = false;
+#pragma unroll
+    for (int u = 0; u < R; u++) er |= j == (e0 + u * (K / R)) % K;
+    if (er) {
+      if (!SORTED) rows[nr++] = rp + (uint64_t)(ne++) * L;  // the equation that replaces it, in its slot
+    } else {
+      rows[nr++] = src + (b * K + j) * (uint64_t)L;
+    }
+  }
+  if (SORTED)
+    for (int u = 0; u < R; u++) rows[nr++] = rp + (uint64_t)u * L;
+  u32x4 x0 = 0, x1 = 0;
+  for (int j0 = 0; j0 < K; j0 += 8) {
+    u32x4 a0[8], a1[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) {
+      a0[jj] = ld<true>((const u32x4 *)(rows[j0 + jj] + o0));
+      a1[jj] = ok1 ? ld<true>((const u32x4 *)(rows[j0 + jj] + o1)) : (u32x4)0;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) { x0 ^= a0[jj]; x1 ^= a1[jj]; }
+  }
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    uint8_t *p = dst + (uint64_t)i * L;
+    __builtin_nontemporal_store(x0 + (uint32_t)i, (u32x4 *)(p + o0));
+    if (ok1) __builtin_nontemporal_store(x1 + (uint32_t)i, (u32x4 *)(p + o1));
+  }
+}
+
 template <int W, bool NT>
 __global__ __launch_bounds__(64 * W) void split(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep, uint64_t nb) {
   __shared__ u32x4 red[2][W][2][64];
@@ -153,13 +200,13 @@ __global__ __launch_bounds__(64 * W) void lin(const uint8_t *__restrict__ src, u
 }
 
 int main(int argc, char **argv) {
-  const bool adj_only = argc > 1;
+  const bool adj_only = argc > 1, dec_only = argc > 1 && argv[1][0] == 'd';
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const uint64_t nb = (uint64_t)(1 << 20) * 16 / K;  // 2^20 blocks at k16, 2^19 at k32 (19.3 GB)
   uint8_t *src, *rep;
-  CK(hipMalloc(&src, nb * K * L)); CK(hipMalloc(&rep, nb * R * L));
-  CK(hipMemset(src, 3, nb * K * L)); CK(hipMemset(rep, 5, nb * R * L));
+  CK(hipMalloc(&src, nb * K * L)); CK(hipMalloc(&rep, 2 * nb * R * L));  // dec: recovered rows after the repairs
+  CK(hipMemset(src, 3, nb * K * L)); CK(hipMemset(rep, 5, 2 * nb * R * L));
   const double bytes = (double)nb * (K + R) * L;
   printf("# k%d r%d L%d, %llu blocks, %.2f GB per launch\n", K, R, L, (unsigned long long)nb, bytes / 1e9);
   auto run = [&](const char *name, auto kern, int W, size_t lds_per_wave, size_t stat, int per_wg = 1) {
@@ -189,6 +236,11 @@ int main(int argc, char **argv) {
       snprintf(nm, sizeof nm, "%-22s %d waves/SIMD", NAME, wps); \
       run(nm, KERN, W, per, 0, W);
       RUNK("col G1", col, 1, 0)
+      if (dec_only) {
+        RUNK("dec slot order", dec<false>, 1, 0)
+        RUNK("dec sorted", dec<true>, 1, 0)
+        continue;
+      }
       if (!adj_only) {
         RUNK("split W2 nt", (split<2, true>), 2, 4096 * 2)
         RUNK("split W4 nt", (split<4, true>), 4, 4096 * 4)
