@@ -25,12 +25,13 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E 8.0 TB/s)
 # measured on MI355X (profiles/r01_copy_style_probe.log, tools/microbench/copy_style_probe.hip): the best
 # plain-streaming rates -- one-shot float4 copy (1:1) and a one-shot 4:1 read:write mix (nt loads and
-# stores); and the FEC data path's own access pattern with trivial compute
-# (profiles/r01_block_pattern_probe.log: k16 r4 rows, one wave per interleaved group of 4 blocks --
-# the encode's default group -- at 3 waves/SIMD; groups of 16 measured 5438-5476 on that box)
+# stores); and the roofline kernel's (the k16 e4 decode apply's) own access pattern with trivial compute:
+# per block the 12 received sources and 4 repairs read in slot order, 4 recovered rows written packed,
+# one wave per block (profiles/r04_dec_probe_k16.log, tools/microbench/split_probe.hip "dec": 5498-5569
+# GB/s at 3 and 4 waves/SIMD; the encode's one-wave pattern on that box 5475-5685)
 MEASURED_COPY_GBS = 6282.0
 MEASURED_MIX41_GBS = 6440.0
-PATTERN_CEILING_GBS = 5564.0
+PATTERN_CEILING_GBS = 5530.0
 METRIC = "FEC encode+decode GiB/s (device-resident, 1200B symbols)"
 
 
