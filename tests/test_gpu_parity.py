@@ -1,5 +1,8 @@
 """Device engine (libpquic_fec.so on an MI355X) against the CPU oracle and the
 reference-generated golden fixtures.  Integer/byte work: every comparison is bit-exact."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -25,6 +28,7 @@ def oracle():
 
 
 DEV = "cuda:0"
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 
 def to_dev(a):
@@ -444,6 +448,69 @@ def test_full_size_roundtrip_k16(eng, oracle):
         st_ref[t] = stb[0]
     assert np.array_equal(st.cpu().numpy()[sample], st_ref)
     del src, rep, work
+    torch.cuda.empty_cache()
+
+
+def test_full_size_bench_decode_path_k16(eng, oracle):
+    """The bench's own decode path at full size (2^20 blocks, k16 r4, 4 random erasures per block, the
+    bench's make_erasures): the plan on a second stream beside the encode, then the packed apply
+    (recovered rows into new rows, dst[b][4][L]).  Statuses and recovered masks equal the one-shot
+    decode's, every recovered row equals its original, and a sample of blocks equals the oracle's
+    recovered bytes."""
+    sys.path.insert(0, ROOT)
+    from bench import check_recovered, make_erasures
+    nb, k, r, e, L = 1 << 20, 16, 4, 4, 1200
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=DEV)
+    eng.synth_fill(src, src.numel(), 0xB3)
+    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
+    sp, miss = make_erasures(torch, nb, k, e, 7, DEV)
+    rp = torch.zeros((nb, 2), dtype=torch.int64, device=DEV)
+    rp[:, 0] = (1 << r) - 1
+    ws = eng.alloc_workspace(nb, k, r)
+    plan_stream = torch.cuda.Stream()
+    stream = torch.cuda.current_stream()
+    go = torch.cuda.Event()
+    go.record(stream)
+    plan_stream.wait_event(go)
+    eng.rlc_decode_plan(sp, rp, k, r, nb, ws, stream=plan_stream)
+    planned = torch.cuda.Event()
+    planned.record(plan_stream)
+    eng.rlc_encode(src, rep, k, r, L)
+    stream.wait_event(planned)
+    work = src.clone()
+    idx = (torch.arange(nb, device=DEV).unsqueeze(1) * k + miss.to(DEV)).reshape(-1)
+    work.view(nb * k, L)[idx] = 0xA5  # the erased rows hold garbage; the apply must not read them
+    dst = torch.full((nb, e, L), 0x5A, dtype=torch.uint8, device=DEV)
+    st = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+    eng.rlc_decode_apply_packed(work, rep, dst, st, rec, k, r, L, nb, ws)
+    st1 = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    rec1 = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+    one = work.clone()
+    eng.rlc_decode(one, rep, sp, rp, st1, rec1, k, r, L)
+    torch.cuda.synchronize()
+    assert torch.equal(st, st1) and torch.equal(rec, rec1)
+    ok = st == 0
+    assert 0.002 < (st == 2).float().mean().item() < 0.03
+    check_recovered(torch, dst, src, ok, miss, nb, k, L, "packed apply at 2^20 blocks")
+    del one
+    # sample vs the oracle: statuses and the recovered bytes, row u = the u-th erased source
+    sample = np.random.default_rng(3).choice(nb, 256, replace=False)
+    s_src = src[sample].cpu().numpy()
+    s_rep = rep[sample].cpu().numpy()
+    s_sp = sp.cpu().numpy().view(np.uint64)[sample]
+    s_rp = rp.cpu().numpy().view(np.uint64)[sample]
+    msort = miss.sort(dim=1).values.numpy()[sample]
+    got_st = st.cpu().numpy()[sample]
+    got_dst = dst[sample].cpu().numpy()
+    for t, b in enumerate(sample):
+        ref = s_src[t:t + 1].copy()
+        ref[0, msort[t]] = 0
+        stb, recb = oracle.rlc_decode_batch(ref, s_rep[t:t + 1], s_sp[t:t + 1], s_rp[t:t + 1], int(b))
+        assert got_st[t] == stb[0], b
+        if stb[0] == 0:
+            assert np.array_equal(got_dst[t], ref[0, msort[t]]), b
+    del src, rep, work, dst
     torch.cuda.empty_cache()
 
 
