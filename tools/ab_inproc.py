@@ -103,7 +103,10 @@ for (k, r, nb, mode, L) in CASES:
                       (sym, wrep, None, None, None, None, None)))
         continue
     bufs = setup(k, r, nb, min(k, r), L)
-    cases.append((f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}"), k, r, nb, mode, L, bufs))
+    label = f"{mode} k{k} r{r}" + ("" if L == 1200 else f" L{L}")
+    if any(c[0] == label for c in cases):  # the same shape at another batch size: labels (and the
+        label += f" 2^{nb.bit_length() - 1}"  # digests and times keyed by them) must stay distinct
+    cases.append((label, k, r, nb, mode, L, bufs))
 
 
 def run(case, eng):
