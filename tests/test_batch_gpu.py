@@ -731,3 +731,40 @@ def test_batch_connection_closes_arena_unregistered():
     assert st1["rows_in_place"] - st0["rows_in_place"] == 3 * (6 + 3)
     assert st1["engine_errors"] == 0
     bt.close()
+
+
+def test_batch_recover_arena_full_part_way_through_a_block():
+    """Recover on the gather path when the arena fills part way through a block's allocations: the
+    first block's received symbols (12 slots) and its first recovered symbol (2 slots) lie in the
+    registered arena, its second recovered symbol's data and everything after come from the heap.
+    The recovered rows written in place keep their bytes, the staged ones are copied in, and every
+    block equals the oracle's recovery."""
+    k, r, L = 6, 3, 1200
+    bt = Batch(4, max_symbol=L, arena=True, arena_bytes=15 * 2112)
+    rng = np.random.default_rng(17)
+    o = Oracle()
+    jobs = []
+    for b in range(3):
+        fbn = int(rng.integers(0, 1 << 24))
+        full = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        reps = o.rlc_encode_block(fbn, full, r)[1]
+        miss = {1, 3, 4}
+        srcs = [None if j in miss else full[j] for j in range(k)]
+        st, rec = o.rlc_decode_block(fbn, srcs, list(reps))
+        assert sorted(rec) == sorted(miss)
+        t = bt.recover(False, fbn, srcs, list(reps), [(fbn << 8) | i for i in range(r)], now=b)
+        jobs.append((t, fbn, srcs, rec))
+    bt.L.mh_batch_drain()
+    for t, fbn, srcs, want in jobs:
+        ret, calls = bt.status(t)
+        assert calls == 1 and ret == 0
+        got, cur = bt.recovered(t)
+        assert sorted(got) == sorted(want), fbn
+        for j in got:
+            assert got[j].tobytes() == want[j].tobytes(), (fbn, j)
+            assert bt.last_fpids[j] == ((fbn << 8) + j) & 0xFFFFFFFF
+        assert cur == sum(s is not None for s in srcs) + len(got)
+    st = bt.stats()
+    assert st["engine_errors"] == 0
+    assert st["rows_in_place"] == 6 + 1 and st["rows_staged"] > 0, st
+    bt.close()
