@@ -41,3 +41,40 @@ for rep_ in range(2):
     print(f"loaded: rc {rc} generate p50 {lo[0]:.0f} p99 {lo[1]:.0f} us, recover p50 {lo[3]:.0f} p99 {lo[4]:.0f} us; "
           f"bulk calls meanwhile {lo[7]:.0f} (mean {lo[9]:.2f} ms, max {lo[10]:.2f} ms), withdrawn {lo[8]:.0f}",
           flush=True)
+
+# The same hooks beside a DEVICE-resident bulk job (k16 r4 encodes of 4096 blocks in HBM, back to back,
+# from a Python thread on its own stream; ctypes releases the GIL while the hooks run): no PCIe traffic
+# competes with the hooks' rows, only the GPU's compute units.
+import threading  # noqa: E402
+import time  # noqa: E402
+
+bsrc = torch.empty((4096, k, L), dtype=torch.uint8, device=dev)
+eng.synth_fill(bsrc, bsrc.numel(), 2, 0)
+brep = torch.empty((4096, r, L), dtype=torch.uint8, device=dev)
+stop, calls, durs = False, [0], []
+
+
+def bulk():
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        while not stop:
+            t0 = time.perf_counter()
+            for _ in range(8):
+                eng.rlc_encode(bsrc, brep, k, r, L)
+            s.synchronize()
+            durs.append((time.perf_counter() - t0) * 1e3 / 8)
+            calls[0] += 8
+
+
+th = threading.Thread(target=bulk)
+th.start()
+time.sleep(0.5)
+for rep_ in range(2):
+    out = (C.c_double * 7)()
+    c0 = calls[0]
+    rc = lib.bl_hook_latency(0, 16, 4, 1200, 4, 2000, out)
+    print(f"device bulk: rc {rc} generate p50 {out[0]:.0f} p99 {out[1]:.0f} us, recover p50 {out[3]:.0f} p99 "
+          f"{out[4]:.0f} us; bulk encodes meanwhile {calls[0] - c0} ({sum(durs[-20:]) / max(1, len(durs[-20:])):.3f} ms each)",
+          flush=True)
+stop = True
+th.join()
