@@ -255,11 +255,13 @@ int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *svc, const void *src,
                                        uint64_t *recovered);
 /* worker generations launched so far (diagnostics: one per idle gap) */
 uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *svc);
-/* A call waits at most `deadline_us` (default 2000) for the worker to serve its request.  Past it the
- * worker is ended and waited for: the request is then either done (the call succeeds) or withdrawn --
- * no worker serves it later -- and the call returns FECGPU_ERR_INVALID, so the caller takes the host
- * path; for the next 50 ms every call returns FECGPU_ERR_INVALID at once (the worker was most likely
- * queued behind a long kernel).  0: withdraw whatever is not done at the first check (tests). */
+/* A call waits at most `deadline_us` (default 2000) for a worker to take its request.  Past it the
+ * request is withdrawn on the spot unless a worker has claimed it (compare-and-swap on the request
+ * number, against the worker's own claim): a withdrawn request is never served later, and the call
+ * returns FECGPU_ERR_INVALID without waiting for the worker (it may be queued behind a long kernel),
+ * so the caller takes the host path; for the next 50 ms every call returns FECGPU_ERR_INVALID at once.
+ * A request a worker claimed before the deadline is being served and is waited for (the call
+ * succeeds).  0: withdraw whatever is not done at the first check (tests). */
 int fecgpu_block_svc_set_deadline(fecgpu_block_svc_t *svc, uint64_t deadline_us);
 /* requests withdrawn at the deadline so far */
 uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *svc);
@@ -324,6 +326,9 @@ typedef struct {
     /* host path: page-locked buffers found in the library's registry of its own fecgpu_host_alloc /
      * fecgpu_host_register ranges, and those that needed a hipPointerGetAttributes query instead */
     uint64_t pinned_registry_hits, pinned_registry_misses;
+    /* zero-copy bulk calls while the synchronous hooks are in use: slices launched, and slices held back
+     * until a pending hook request had finished (host_path.hip, Pacer) */
+    uint64_t yield_slices, yield_waits;
 } fecgpu_stats_t;
 void fecgpu_get_stats(fecgpu_stats_t *out);
 

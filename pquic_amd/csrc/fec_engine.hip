@@ -55,10 +55,12 @@ static std::atomic<uint64_t> g_stats[4];
 // environment variables, so nothing outside the caller's own calls can change which kernels run.
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
-              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_N };
+              K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
+              K_YIELD_GATE_US, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
-                                           "small_lds", "block_svc", "ws_lds", "dec_waves"};
+                                           "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
+                                           "yield_depth", "yield_gate_us"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -93,6 +95,12 @@ static void knobs_default() {
   // recover data pass (register-prefetch bodies): 0 = the occupancy its registers allow, n = at most
   // n waves per SIMD
   g_knob[K_DEC_WAVES] = 0;
+  // zero-copy bulk calls while the hooks are in use (host_path.hip, Pacer): slices of this many KiB of
+  // payload (0: never slice), at most yield_depth in flight, and a slice held back at most
+  // yield_gate_us while a hook request is pending (0: not held)
+  g_knob[K_YIELD_SLICE_KB] = 3072;
+  g_knob[K_YIELD_DEPTH] = 4;
+  g_knob[K_YIELD_GATE_US] = 0;
 }
 
 static inline int knob(KnobId id) {
@@ -103,6 +111,11 @@ static inline int knob(KnobId id) {
 // host_path.hip reads the zero-copy knob through this (library-internal)
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_window_sc(void) { return knob(K_WINDOW_SC); }
+extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us) {
+  *slice_kb = knob(K_YIELD_SLICE_KB);
+  *depth = knob(K_YIELD_DEPTH);
+  *gate_us = knob(K_YIELD_GATE_US);
+}
 
 static int set_err(int code, const char *fmt, const char *what) {
   snprintf(g_err, sizeof g_err, fmt, what);
@@ -1980,8 +1993,13 @@ __global__ __launch_bounds__(kLdsThreads) void k_rlc_decode_lds(const uint8_t *_
 // The mailbox: the request (everything a block needs beside its rows, so the worker fetches it with
 // one parallel load: wave 0's lanes read 16 B each) then the device-written words.
 constexpr int kSvcMaxR = 128;
+// Request numbers: the host posts n by storing it into req.seq (release); the worker claims a pending
+// request by compare-and-swap n -> n | kSvcClaimed before it reads the request, and the host withdraws
+// one by compare-and-swap n -> n - 1 (the last number served).  Exactly one of the two succeeds, so a
+// withdrawn request is never served and a claimed one is always finished.
+constexpr uint64_t kSvcClaimed = 1ull << 63;
 struct alignas(64) BlockSvcReq {
-  uint64_t seq;                     // request number, written last by the host (release)
+  uint64_t seq;                     // request number, written last by the host (release); | kSvcClaimed
   uint32_t op, k, r, L, fbn, wreg;  // op 1 = RLC encode, 2 = RLC decode with per-repair seeds
   uint64_t src, rep, dst;           // device addresses of the block's rows (page-locked host memory)
   uint64_t sp[2], rp[2];            // presence masks (decode)
@@ -2016,7 +2034,12 @@ __global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, 
     if (threadIdx.x == 0) {
       int g = 0;
       for (;;) {
-        if (sys_load(&mb->req.seq) != done) {
+        uint64_t s = sys_load(&mb->req.seq);
+        // a posted, unclaimed request: claim it (the host may withdraw it at the same moment; one wins)
+        if (!(s & kSvcClaimed) && s != done &&
+            __hip_atomic_compare_exchange_strong(&mb->req.seq, &s, s | kSvcClaimed, __ATOMIC_ACQ_REL,
+                                                 __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          done = s;  // the number this pass serves
           g = 1;
           break;
         }
@@ -2058,7 +2081,6 @@ __global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave's outputs reach host memory first
     __syncthreads();
     if (threadIdx.x == 0) {
-      done = R.seq;
       __hip_atomic_store(&mb->done, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       t_last = __builtin_amdgcn_s_memrealtime();
     }
@@ -2957,6 +2979,9 @@ static bool knob_value_ok(int id, int v) {
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;
     case K_DEC_WAVES: return v >= 0 && v <= 8;
+    case K_YIELD_SLICE_KB: return v >= 0 && v <= (1 << 20);
+    case K_YIELD_DEPTH: return v >= 1 && v <= 16;
+    case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
     default: return v == 0 || v == 1;  // on / off knobs
   }
 }
@@ -2991,6 +3016,7 @@ int fecgpu_debug_stamps(uint64_t out[16]) {  // diagnostic builds: the phase sta
 #endif
 
 void fecgpu_host_registry_stats(uint64_t *hits, uint64_t *misses);  // host_path.hip (library-internal)
+void fecgpu_host_yield_stats(uint64_t *slices, uint64_t *waits);      // host_path.hip (library-internal)
 
 void fecgpu_get_stats(fecgpu_stats_t *out) {
   out->encode_calls = g_stats[0].load();
@@ -2998,6 +3024,7 @@ void fecgpu_get_stats(fecgpu_stats_t *out) {
   out->decode_calls = g_stats[2].load();
   out->decode_blocks = g_stats[3].load();
   fecgpu_host_registry_stats(&out->pinned_registry_hits, &out->pinned_registry_misses);
+  fecgpu_host_yield_stats(&out->yield_slices, &out->yield_waits);
 }
 
 // Encode tiling: repairs per wave (RT) and waves per workgroup sharing the source stream.
@@ -3559,6 +3586,16 @@ static uint64_t svc_now_us() {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
 }
+
+// Hook requests in flight (posted, not yet returned) across every service of the process, and the
+// time of the last one: the zero-copy bulk paths (host_path.hip, Pacer) slice their launches while
+// hooks are in use and start no slice while one is pending.
+static std::atomic<int> g_svc_pending{0};
+static std::atomic<uint64_t> g_svc_last_us{0};
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_svc_hooks_pending(void) { return g_svc_pending.load(); }
+extern "C" __attribute__((visibility("hidden"))) uint64_t fecgpu_svc_last_request_us(void) {
+  return g_svc_last_us.load(std::memory_order_relaxed);
+}
 // after a withdrawn request the hooks use the launch path for this long: a worker that was not
 // scheduled within the deadline is most likely queued behind a long kernel, and so would the next be
 constexpr uint64_t kSvcBackoffUs = 50000;
@@ -3615,7 +3652,7 @@ void fecgpu_block_svc_destroy(fecgpu_block_svc_t *v) {
 static int svc_ensure(fecgpu_block_svc_t *v) {
   if (v->launched && hipEventQuery(v->ev) == hipErrorNotReady) return FECGPU_OK;
   (void)hipGetLastError();
-  __atomic_store_n(&v->mb->quit, 0ull, __ATOMIC_RELEASE);  // a withdrawal ended the last worker with it
+  __atomic_store_n(&v->mb->quit, 0ull, __ATOMIC_RELEASE);
   hipLaunchKernelGGL(k_block_svc, dim3(1), dim3(kLdsThreads), kSvcLds, v->stream, v->mb_dev, kSvcIdleTicks,
                      kSvcLifeTicks);
   HIPCHK(hipGetLastError());
@@ -3624,36 +3661,69 @@ static int svc_ensure(fecgpu_block_svc_t *v) {
   return FECGPU_OK;
 }
 
-// Takes back request `seq` (posted, not served): no worker may serve it later, when its rows are
-// the caller's again.  The request number goes back to the last one served, so a worker started
-// later sees nothing pending.
-static void svc_unpost(fecgpu_block_svc_t *v, uint64_t seq) {
-  __atomic_store_n(&v->mb->req.seq, seq - 1, __ATOMIC_RELEASE);
-  v->seq = seq - 1;
+// Takes back request `seq` unless a worker has claimed it: compare-and-swap seq -> seq - 1 (the last
+// number served), against the worker's claim seq -> seq | kSvcClaimed.  Returns true when the request
+// is withdrawn (no worker can serve it later, when its rows are the caller's again); false when a
+// worker claimed it first and is serving it.
+static bool svc_unpost(fecgpu_block_svc_t *v, uint64_t seq) {
+  uint64_t expect = seq;
+  if (__atomic_compare_exchange_n(&v->mb->req.seq, &expect, seq - 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+    v->seq = seq - 1;
+    return true;
+  }
+  return false;
 }
 
-// The deadline passed with request `seq` unserved: the worker is told to end and is waited for (a
-// worker serves a posted request before it looks at the quit flag, so once it has ended the request
-// is either done or was never seen), then the request is taken back if nobody served it.  Returns OK
-// when it was served after all, else FECGPU_ERR_INVALID: the caller runs the block through the launch
-// path, as for a block the service does not take.  The next calls skip the service for a while.
+// A claimed request is being served: wait for it, as long as its worker lives (a worker that ended or
+// faulted without finishing it reports an error).
+static int svc_wait_claimed(fecgpu_block_svc_t *v, uint64_t seq) {
+  for (uint64_t spin = 1;; spin++) {
+    if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+    __builtin_ia32_pause();
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipEventQuery(v->ev);
+      if (q == hipErrorNotReady) continue;
+      if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+      return set_err(FECGPU_ERR_HIP, "block service: worker ended without finishing a claimed request (%s)",
+                     hipGetErrorString(q));
+    }
+  }
+}
+
+// Takes request `seq` back on an error path; a request a worker has claimed is waited for instead.
+static int svc_abandon(fecgpu_block_svc_t *v, uint64_t seq, int rc) {
+  if (svc_unpost(v, seq)) return rc;
+  const int w = svc_wait_claimed(v, seq);
+  return w ? w : rc;
+}
+
+// The deadline passed with request `seq` unserved.  If no worker has claimed it, it is withdrawn on
+// the spot -- no wait for the worker, which may be queued behind a long kernel: it starts when the
+// GPU lets it, finds nothing pending and serves later requests or ends on its idle limit -- and the
+// call returns FECGPU_ERR_INVALID, so the caller runs the block through the launch path, as for a
+// block the service does not take; the next calls skip the service for a while and the withdrawal is
+// counted.  If a worker claimed it in the meantime it is running now and is waited for (OK).
 static int svc_withdraw(fecgpu_block_svc_t *v, uint64_t seq) {
-  __atomic_store_n(&v->mb->quit, 1ull, __ATOMIC_RELEASE);
-  const hipError_t e = hipEventSynchronize(v->ev);
+  if (!svc_unpost(v, seq)) return svc_wait_claimed(v, seq);
   v->misses++;
   v->backoff_until = svc_now_us() + kSvcBackoffUs;
-  if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
-  svc_unpost(v, seq);
-  if (e != hipSuccess) return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(e));
   return set_err(FECGPU_ERR_INVALID, "%s", "block service: deadline passed, request withdrawn");
 }
 
 // Posts the request already written into the mailbox and waits for its completion, at most
 // v->deadline_us before it is withdrawn (svc_withdraw).  The request number is posted only once a
 // worker is running or launched, and taken back on every error return.
+static int svc_run_posted(fecgpu_block_svc_t *v, uint64_t t0);
 static int svc_run(fecgpu_block_svc_t *v) {
   const uint64_t t0 = svc_now_us();
   if (t0 < v->backoff_until) return FECGPU_ERR_INVALID;  // a recent withdrawal: the launch path for now
+  g_svc_last_us.store(t0, std::memory_order_relaxed);
+  g_svc_pending.fetch_add(1);
+  const int rc = svc_run_posted(v, t0);
+  g_svc_pending.fetch_sub(1);
+  return rc;
+}
+static int svc_run_posted(fecgpu_block_svc_t *v, uint64_t t0) {
   if (int rc = svc_ensure(v)) return rc;
   const uint64_t seq = v->seq + 1;
   v->seq = seq;
@@ -3665,16 +3735,11 @@ static int svc_run(fecgpu_block_svc_t *v) {
     if ((spin & 1023) == 0) {
       const hipError_t q = hipEventQuery(v->ev);
       if (q == hipErrorNotReady) continue;
-      if (q != hipSuccess) {
-        svc_unpost(v, seq);
-        return set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(q));
-      }
+      if (q != hipSuccess)
+        return svc_abandon(v, seq, set_err(FECGPU_ERR_HIP, "block service: %s", hipGetErrorString(q)));
       // the worker ended (idle limit reached as the request was posted): the next one serves it
       if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
-      if (int rc = svc_ensure(v)) {
-        svc_unpost(v, seq);
-        return rc;
-      }
+      if (int rc = svc_ensure(v)) return svc_abandon(v, seq, rc);
     }
   }
 }

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <algorithm>
 #include <atomic>
 #include <mutex>
@@ -19,6 +20,7 @@
 
 namespace {
 constexpr int kMaxStreams = 4;
+constexpr int kMaxYieldDepth = 16;
 
 struct Slot {
   hipStream_t st = nullptr;
@@ -42,6 +44,7 @@ struct fecgpu_host_ctx {
   int ns = 1;
   size_t chunk_bytes = 64u << 20;
   Slot slot[kMaxStreams];
+  hipEvent_t yev[16] = {};  // the Pacer's slice completions (created on first use)
   std::mutex mu;
 };
 
@@ -80,6 +83,8 @@ void fecgpu_host_ctx_destroy(fecgpu_host_ctx_t *c) {
     if (s.d_aux) (void)hipFree(s.d_aux);
     if (s.d_ws) (void)hipFree(s.d_ws);
   }
+  for (hipEvent_t e : c->yev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -117,6 +122,7 @@ extern "C" __attribute__((visibility("hidden"))) void fecgpu_host_registry_stats
   *hits = g_pin_hits.load();
   *misses = g_pin_misses.load();
 }
+
 
 // Device address of [p, p + len) when ALL of it is page-locked host memory (hipHostMalloc'd or
 // registered), else nullptr: the kernels then read and write the caller's memory directly, so an
@@ -165,6 +171,73 @@ int fecgpu_rlc_decode_to_internal(const void *src, const void *rep, void *dst, u
 int fecgpu_knob_window_sc(void);  // fec_engine.hip (library-internal)
 static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 
+// ---- zero-copy bulk calls yield to the synchronous hooks ----
+// A hook's rows cross the same PCIe link as a zero-copy bulk call's, and the hook's reads complete only
+// once the bulk kernel running at that moment ends: beside back-to-back bulk calls of 4096 / 1024 / 512 /
+// 256 blocks (1.58 / 0.47 / 0.30 / 0.17 ms each) the hooks' p99 was 1471 / 417 / 271 / 138 us
+// (profiles/r05_hook_sweep.log; rocprofv3 trace in profiles/r05_hook_trace_summary.txt: the slow calls
+// spend no time in HIP calls and involve no worker launch -- the resident worker's reads wait).  So
+// while the block service is in use (a hook request within the last kYieldWindowUs), a zero-copy launch
+// is cut into slices of about yield_slice_kb of payload on one stream, at most yield_depth in flight
+// (knobs): a hook then waits for at most the slice running when it arrives.  Optionally (yield_gate_us)
+// no slice starts while a hook request is pending.  Without hooks nothing changes (one launch).
+int fecgpu_svc_hooks_pending(void);                                  // fec_engine.hip (library-internal)
+uint64_t fecgpu_svc_last_request_us(void);                           // fec_engine.hip (library-internal)
+void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us);     // fec_engine.hip (library-internal)
+namespace {
+constexpr uint64_t kYieldWindowUs = 100000;
+std::atomic<uint64_t> g_yield_slices{0}, g_yield_waits{0};
+
+uint64_t mono_us() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+struct Pacer {
+  fecgpu_host_ctx_t *c;
+  hipStream_t st;
+  uint64_t slice = 0;  // blocks per slice; 0: hooks idle or the call is small, launch it whole
+  int n = 0;           // slices launched
+  int depth = 4, gate_us = 0;
+  Pacer(fecgpu_host_ctx_t *c_, hipStream_t st_, uint64_t nblocks, size_t bytes_per_block) : c(c_), st(st_) {
+    const uint64_t last = fecgpu_svc_last_request_us();
+    if (!last || mono_us() - last > kYieldWindowUs) return;
+    int kb = 0;
+    fecgpu_knob_yield(&kb, &depth, &gate_us);
+    if (!kb || depth > kMaxYieldDepth) return;
+    uint64_t per = ((uint64_t)kb << 10) / (bytes_per_block ? bytes_per_block : 1);
+    if (per < 32) per = 32;
+    if (per >= nblocks) return;
+    for (int i = 0; i < depth; i++)
+      if (!c->yev[i] && hipEventCreateWithFlags(&c->yev[i], hipEventDisableTiming) != hipSuccess) return;
+    slice = per;
+  }
+  // before slice n: at most `depth` in flight, and (gate) none started while a hook request is pending
+  hipError_t before() {
+    if (!slice) return hipSuccess;
+    if (n >= depth)
+      if (hipError_t e = hipEventSynchronize(c->yev[n % depth])) return e;
+    if (gate_us && fecgpu_svc_hooks_pending() > 0) {
+      g_yield_waits++;
+      const uint64_t t0 = mono_us();
+      while (fecgpu_svc_hooks_pending() > 0 && mono_us() - t0 < (uint64_t)gate_us) __builtin_ia32_pause();
+    }
+    return hipSuccess;
+  }
+  hipError_t after() {
+    if (!slice) return hipSuccess;
+    g_yield_slices++;
+    return hipEventRecord(c->yev[n++ % depth], st);
+  }
+};
+}  // namespace
+
+__attribute__((visibility("hidden"))) void fecgpu_host_yield_stats(uint64_t *slices, uint64_t *waits) {
+  *slices = g_yield_slices.load();
+  *waits = g_yield_waits.load();
+}
+
 static uint64_t sub_batch(const fecgpu_host_ctx_t *c, uint64_t nblocks, size_t per_block) {
   uint64_t n = c->chunk_bytes / (per_block ? per_block : 1);
   if (n < 1) n = 1;
@@ -200,6 +273,29 @@ int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   const uint64_t n = sub_batch(c, nblocks, sb);
   uint8_t *zs = zc_read() ? mapped_host(src, nblocks * sb) : nullptr, *zr = zs ? mapped_host(rep, nblocks * rb) : nullptr;
   int si = 0, rc = FECGPU_OK;
+  if (zs && zr) {  // page-locked, hooks in use: slices that yield to them (Pacer)
+    Slot &s = c->slot[0];
+    Pacer pc(c, s.st, nblocks, sb + rb);
+    if (pc.slice) {
+      const uint32_t *df = nullptr;
+      do {
+        if (fbn) {
+          LCHK(grow(&s.d_aux, &s.cap_aux, nblocks * 4));
+          LCHK(hipMemcpyAsync(s.d_aux, fbn, nblocks * 4, hipMemcpyHostToDevice, s.st));
+          df = (const uint32_t *)s.d_aux;
+        }
+        for (uint64_t b0 = 0; b0 < nblocks; b0 += pc.slice) {
+          const uint64_t m = nblocks - b0 < pc.slice ? nblocks - b0 : pc.slice;
+          LCHK(pc.before());
+          if ((rc = fecgpu_rlc_encode(zs + b0 * sb, zr + b0 * rb, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu),
+                                      df ? df + b0 : nullptr, s.st)))
+            break;
+          LCHK(pc.after());
+        }
+      } while (0);
+      return finish(c, rc);
+    }
+  }
   for (uint64_t b0 = 0; b0 < nblocks; b0 += n, si = (si + 1) % c->ns) {
     Slot &s = c->slot[si];
     const uint64_t m = nblocks - b0 < n ? nblocks - b0 : n;
@@ -246,7 +342,13 @@ int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       dr = (const uint64_t *)(a + nblocks * k * 8);
       df = fbn ? (const uint32_t *)(a + nblocks * (k + r) * 8) : nullptr;
     }
-    rc = fecgpu_rlc_encode_rows(ds, dr, nblocks, k, r, L, 0, df, s.st);
+    Pacer pc(c, s.st, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
+    for (uint64_t b0 = 0, step = pc.slice ? pc.slice : nblocks; b0 < nblocks; b0 += step) {
+      const uint64_t m = nblocks - b0 < step ? nblocks - b0 : step;
+      LCHK(pc.before());
+      if ((rc = fecgpu_rlc_encode_rows(ds + b0 * k, dr + b0 * r, m, k, r, L, 0, df ? df + b0 : nullptr, s.st))) break;
+      LCHK(pc.after());
+    }
   } while (0);
   return finish(c, rc);
 }
@@ -468,7 +570,15 @@ int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       LCHK(hipMemcpyAsync(recovered, drec, nblocks * 16, hipMemcpyDeviceToHost, s.st));
       break;
     }
-    rc = fecgpu_rlc_decode_rows(ds, dr, nblocks, k, r, L, dseed, dsp, drp, dst, drec, s.d_ws, s.cap_ws, s.st);
+    Pacer pc(c, s.st, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
+    for (uint64_t b0 = 0, step = pc.slice ? pc.slice : nblocks; b0 < nblocks; b0 += step) {
+      const uint64_t m = nblocks - b0 < step ? nblocks - b0 : step;
+      LCHK(pc.before());
+      if ((rc = fecgpu_rlc_decode_rows(ds + b0 * k, dr + b0 * nseed, m, k, r, L, dseed + b0 * nseed, dsp + 2 * b0,
+                                       drp + 2 * b0, dst + b0, drec + 2 * b0, s.d_ws, s.cap_ws, s.st)))
+        break;
+      LCHK(pc.after());
+    }
   } while (0);
   return finish(c, rc);
 }

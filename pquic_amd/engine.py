@@ -26,7 +26,8 @@ class FecGpuError(RuntimeError):
 class FecGpuStats(C.Structure):
     _fields_ = [("encode_calls", C.c_uint64), ("encode_blocks", C.c_uint64),
                 ("decode_calls", C.c_uint64), ("decode_blocks", C.c_uint64),
-                ("pinned_registry_hits", C.c_uint64), ("pinned_registry_misses", C.c_uint64)]
+                ("pinned_registry_hits", C.c_uint64), ("pinned_registry_misses", C.c_uint64),
+                ("yield_slices", C.c_uint64), ("yield_waits", C.c_uint64)]
 
 
 def load_library(path: str = LIB_PATH, private: bool = False):

@@ -12,7 +12,8 @@ from golden_io import load
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 LIB = os.path.join(ROOT, "pquic_amd", "lib", "libpquic_fec.so")
-MINIHOST = os.path.join(ROOT, "tests", "host", "libminihost.so")
+# PQUIC_TEST_MINIHOST: a sanitizer build over the CPU engine stand-in (tests/sanitize, test_sanitize.py)
+MINIHOST = os.environ.get("PQUIC_TEST_MINIHOST") or os.path.join(ROOT, "tests", "host", "libminihost.so")
 
 
 def declared_functions():
@@ -104,6 +105,28 @@ def test_integration_stub_compiles_against_picoquic(tmp_path):
                         f"-I{os.path.join(ROOT, 'include')}", os.path.join(ROOT, "tests", "host", "integration_stub.c"),
                         "-o", str(tmp_path / "stub.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_integration_option_b_allocates_in_the_inserted_fec_plugin(tmp_path):
+    """INTEGRATION.md §4 (Option B): the native create_fec_schemes registered by the stub allocates its
+    scheme in the arena of the FEC composition the host inserted -- under each shipped manifest name
+    (fec.plugin:1, fec_rlc_gf256_window.plugin:1, fec_rlc_gf256_window_protect_end_of_stream_only_
+    inflight.plugin:1), given at install or found by prefix -- and never in another plugin's; a
+    connection without a FEC plugin gets PICOQUIC_ERROR_MEMORY, not a NULL dereference.  Built against
+    picoquic's own headers and structures (survey container only), run on the CPU (no device call)."""
+    import subprocess
+    pico = "/root/reference/picoquic"
+    if not os.path.isdir(pico):
+        pytest.skip("reference tree not present")
+    exe = str(tmp_path / "integration_driver")
+    lib = os.path.join(ROOT, "pquic_amd", "lib")
+    r = subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", f"-I{pico}", f"-I{os.path.join(ROOT, 'include')}",
+                        os.path.join(ROOT, "tests", "host", "integration_driver.c"), f"-L{lib}", "-lpquic_fec",
+                        f"-Wl,-rpath,{lib}", "-o", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(" ok\n") == 8 and "all ok" in r.stdout
 
 
 def test_oversized_block_rejected_without_device_call():

@@ -14,7 +14,8 @@ import pytest
 from golden_io import load
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-MINIHOST = os.path.join(ROOT, "tests", "host", "libminihost.so")
+# PQUIC_TEST_MINIHOST: a sanitizer build over the CPU engine stand-in (tests/sanitize, test_sanitize.py)
+MINIHOST = os.environ.get("PQUIC_TEST_MINIHOST") or os.path.join(ROOT, "tests", "host", "libminihost.so")
 u64p, u32p, u8p = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)
 
 

@@ -8,7 +8,8 @@ import os
 import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-LIB = os.path.join(ROOT, "pquic_amd", "lib", "libpquic_fec.so")
+# PQUIC_TEST_MINIHOST: the frame codecs from a sanitizer build (tests/sanitize, test_sanitize.py)
+LIB = os.environ.get("PQUIC_TEST_MINIHOST") or os.path.join(ROOT, "pquic_amd", "lib", "libpquic_fec.so")
 GOLD = os.path.join(ROOT, "tests", "golden", "frames.json")
 
 
@@ -149,7 +150,7 @@ def test_payload_to_source_symbol(lib, gold):
 def test_payload_to_source_symbol_protoop():
     """The protoop adapter (inputs through get_cnx, frames through the host's skip_frame) on the
     same vectors, driven by the picoquic stand-in; a NULL buffer returns PICOQUIC_ERROR_MEMORY."""
-    so = os.path.join(ROOT, "tests", "host", "libminihost.so")
+    so = os.environ.get("PQUIC_TEST_MINIHOST") or os.path.join(ROOT, "tests", "host", "libminihost.so")
     if not os.path.exists(so):
         pytest.skip("mini host not built")
     M = C.CDLL(so)

@@ -13,7 +13,8 @@ from oracle_py import Oracle
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-MINIHOST = os.path.join(ROOT, "tests", "host", "libminihost.so")
+# PQUIC_TEST_MINIHOST: a sanitizer build over the CPU engine stand-in (tests/sanitize, test_sanitize.py)
+MINIHOST = os.environ.get("PQUIC_TEST_MINIHOST") or os.path.join(ROOT, "tests", "host", "libminihost.so")
 
 
 def _p(a, t=C.c_uint8):

@@ -587,6 +587,17 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
  * with the bound allocator.  `e` sources are erased for recover (all r repairs present).
  * out: [0] generate p50 us, [1] p99, [2] mean, [3] recover p50, [4] p99, [5] mean,
  *      [6] recovered symbols per recover call (check).  Returns 0 or -1. */
+/* Every timed hook call of the last bl_hook_latency: op (0 generate, 1 recover), start (CLOCK_MONOTONIC
+ * us) and duration (us), for lining calls up with a kernel trace (bl_hook_calls). */
+static uint64_t *g_hook_calls;
+static long g_hook_ncalls;
+
+long bl_hook_calls(uint64_t *out, long max) {
+    const long n = g_hook_ncalls < max ? g_hook_ncalls : max;
+    if (out && g_hook_calls) memcpy(out, g_hook_calls, sizeof *out * 3 * (size_t)n);
+    return n;
+}
+
 int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double out[7]) {
     pquic_fec_host_api_t api = {bl_get, bl_set, bl_malloc, bl_free, NULL};
     if (pquic_fec_bind_host(&api, device) || k > 100 || r > 100 || e > r || e > k) return -1;
@@ -598,6 +609,9 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
     pquic_source_symbol_t *ss = calloc((size_t)k, sizeof *ss);
     uint64_t *lat = malloc(sizeof *lat * (size_t)ncalls);
     if (!pool || !ss || !lat) return -1;
+    free(g_hook_calls);
+    g_hook_ncalls = 0;
+    g_hook_calls = malloc(sizeof *g_hook_calls * 3 * 2 * (size_t)ncalls);
     uint64_t x = 0x5EEDF3C0;
     for (size_t o = 0; o < (size_t)k * L; o++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; pool[o] = (uint8_t)x; }
     pquic_fec_block_t fb;
@@ -639,7 +653,13 @@ int bl_hook_latency(int device, int k, int r, int L, int e, long ncalls, double 
             }
             for (int i = 0; i < r; i++)
                 if (fb.repair_symbols[i]) { bl_free(NULL, fb.repair_symbols[i]->data); bl_free(NULL, fb.repair_symbols[i]); }
-            if (c >= 0) lat[c] = t1 - t0;
+            if (c >= 0) {
+                lat[c] = t1 - t0;
+                if (g_hook_calls) {
+                    uint64_t *h = g_hook_calls + 3 * g_hook_ncalls++;
+                    h[0] = (uint64_t)op; h[1] = t0; h[2] = t1 - t0;
+                }
+            }
         }
         double sum = 0;
         for (long c = 0; c < ncalls; c++) sum += (double)lat[c];
