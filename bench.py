@@ -64,6 +64,15 @@ def parse():
     return a
 
 
+def traffic_build(kernel_tag: str):
+    """Which build and run the committed PMC figure for `kernel_tag` was measured on (its "measured_at")."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(kernel_tag, {}).get("measured_at")
+    except Exception:
+        return None
+
+
 def load_traffic(kernel_tag: str, blocks: int | None = None):
     """HBM bytes per launch from the committed PMC profile (profiles/pmc_traffic.json), scaled to
     `blocks` when the profile recorded its per-block figure."""
@@ -951,6 +960,9 @@ def main():
             roof = {"bound": "hbm", "kernel": f"{apply_kernel_name(k, r, L)} (RLC decode apply k={k} e={e})",
                     "achieved": round(app_gbs, 1), "bytes_per_launch": app_bytes, "launch_ms": round(apply_ms, 4),
                     "traffic": load_traffic(f"rlc_decode_apply_k{k}_e{e}", nb)}
+        # the PMC traffic figure is measured in its own rocprofv3 --pmc passes, not in this run: name its build
+        roof["traffic_measured_at"] = traffic_build(f"rlc_encode_{tag}" if (not e or enc_ms >= apply_ms)
+                                                    else f"rlc_decode_apply_k{k}_e{e}")
         roof.update({"peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(roof["achieved"] / HBM_PEAK_GBS, 4),
                      "measured_copy_peak": MEASURED_COPY_GBS,
                      "frac_of_measured_copy": round(roof["achieved"] / MEASURED_COPY_GBS, 4),

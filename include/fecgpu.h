@@ -214,7 +214,8 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *ctx, void *src, const void 
 int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
                                 uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size, const uint32_t *fbn);
 /* fecgpu_rlc_decode_rows from the host: the row tables, seeds, masks, status and recovered are host
- * arrays (page-locked ones are used in place, others copied); the rows must be device-accessible. */
+ * arrays (page-locked ones are used in place, others copied); the rows must be device-accessible.  With
+ * r == 0 the repair table and the seeds have no entries and are not read (NULL is accepted). */
 int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *ctx, const uint64_t *src_rows, const uint64_t *rep_rows,
                                 uint64_t nblocks, uint32_t k, uint32_t r, uint32_t symbol_size,
                                 const uint32_t *rep_seed, const uint64_t *src_present, const uint64_t *rep_present,

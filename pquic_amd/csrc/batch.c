@@ -156,9 +156,17 @@ static uint64_t heap_dev(const pquic_fec_batcher_t *b, const void *p, size_t n, 
     return h->dev + (a - h->base);
 }
 
+/* Page-locking a 16 MiB arena takes milliseconds: it happens outside heaps_mu, so stagers keep looking rows
+ * up meanwhile; only the insertion into the sorted registry takes the lock (and re-checks for overlap). */
 int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t bytes) {
     if (!b || !base || !bytes) return -1;
     const uintptr_t a = (uintptr_t)base;
+    if (fecgpu_host_register(base, bytes) != FECGPU_OK) return -1;
+    uint64_t dev = 0;
+    if (fecgpu_host_device_address(base, bytes, &dev) != FECGPU_OK) {
+        fecgpu_host_unregister(base);
+        return -1;
+    }
     pthread_rwlock_wrlock(&b->heaps_mu);
     const int f = heap_floor(b, a);
     const int overlap = (f >= 0 && a - b->heaps[f].base < b->heaps[f].size) ||
@@ -172,12 +180,6 @@ int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t byt
             b->heaps = nh;
             b->heaps_cap = nc;
         }
-        if (fecgpu_host_register(base, bytes) != FECGPU_OK) goto out;
-        uint64_t dev = 0;
-        if (fecgpu_host_device_address(base, bytes, &dev) != FECGPU_OK) {
-            fecgpu_host_unregister(base);
-            goto out;
-        }
         memmove(&b->heaps[f + 2], &b->heaps[f + 1], sizeof *b->heaps * (size_t)(b->nheaps - f - 1));
         b->heaps[f + 1] = (heap_t){a, bytes, dev};
         b->nheaps++;
@@ -185,21 +187,25 @@ int pquic_fec_batch_register_heap(pquic_fec_batcher_t *b, void *base, size_t byt
     }
 out:
     pthread_rwlock_unlock(&b->heaps_mu);
+    if (rc) fecgpu_host_unregister(base);
     return rc;
 }
 
+/* The arena leaves the registry under heaps_mu (no stager is between a lookup and its use of it) and is
+ * unpinned after the lock is released: nothing queued refers to it (the caller's contract) and no later
+ * lookup can find it. */
 int pquic_fec_batch_unregister_heap(pquic_fec_batcher_t *b, void *base) {
     if (!b || !base) return -1;
-    pthread_rwlock_wrlock(&b->heaps_mu);  /* no stager is between a lookup and its use of the heap */
+    pthread_rwlock_wrlock(&b->heaps_mu);
     const int f = heap_floor(b, (uintptr_t)base);
-    int rc = -1;
+    int found = 0;
     if (f >= 0 && b->heaps[f].base == (uintptr_t)base) {
         memmove(&b->heaps[f], &b->heaps[f + 1], sizeof *b->heaps * (size_t)(b->nheaps - f - 1));
         b->nheaps--;
-        rc = fecgpu_host_unregister(base) == FECGPU_OK ? 0 : -1;
+        found = 1;
     }
     pthread_rwlock_unlock(&b->heaps_mu);
-    return rc;
+    return found && fecgpu_host_unregister(base) == FECGPU_OK ? 0 : -1;
 }
 
 static void job_free(job_t *j) {

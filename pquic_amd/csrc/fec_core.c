@@ -192,17 +192,22 @@ protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
     const int k = fb->total_source_symbols;
     const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
+    /* first the symbols allocated for sources the reference leaves unrecovered go back to the arena, so
+     * an allocation retried below for a recovered one (its pre-allocation had failed) finds their room,
+     * as the reference's allocations after decoding would (it allocates only what it recovers) */
+    for (int j = 0; j < k; j++) {
+        const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
+        if (!got && pre[j]) {
+            g_fec_api.my_free(cnx, pre[j]->data);
+            g_fec_api.my_free(cnx, pre[j]);
+            pre[j] = NULL;
+        }
+    }
     for (int j = 0; j < k; j++) {  /* :218-236, in source order as the reference inserts them */
         const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
         pquic_source_symbol_t *ss = pre[j];
         pre[j] = NULL;
-        if (!got) {
-            if (ss) {  /* allocated for a source the reference leaves unrecovered */
-                g_fec_api.my_free(cnx, ss->data);
-                g_fec_api.my_free(cnx, ss);
-            }
-            continue;
-        }
+        if (!got) continue;
         if (!ss) {
             if (!(ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) continue;
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);

@@ -56,11 +56,11 @@ static std::atomic<uint64_t> g_stats[4];
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
-              K_YIELD_GATE_US, K_N };
+              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
-                                           "yield_depth", "yield_gate_us"};
+                                           "yield_depth", "yield_gate_us", "yield_streams", "yield_always"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -96,11 +96,16 @@ static void knobs_default() {
   // n waves per SIMD
   g_knob[K_DEC_WAVES] = 0;
   // zero-copy bulk calls while the hooks are in use (host_path.hip, Pacer): slices of this many KiB of
-  // payload (0: never slice), at most yield_depth in flight, and a slice held back at most
-  // yield_gate_us while a hook request is pending (0: not held)
-  g_knob[K_YIELD_SLICE_KB] = 3072;
-  g_knob[K_YIELD_DEPTH] = 4;
+  // payload (0: never slice), at most yield_depth in flight, alternating over yield_streams of the
+  // context's streams, and a slice held back at most yield_gate_us while a hook request is pending (0:
+  // not held).  Beside back-to-back 4096-block zero-copy encodes (profiles/r05_pacer_sweep.log): 2560 KiB,
+  // 16, 2 streams -> hooks p99 174 / 184 us (generate / recover; unsliced 1473 / 1486) for bulk calls
+  // 9 % longer (1.725 against 1.582 ms); 2048 KiB -> p99 142-152 us, +12 %; 3072 KiB -> 207-218 us, +7 %
+  g_knob[K_YIELD_SLICE_KB] = 2560;
+  g_knob[K_YIELD_DEPTH] = 16;
   g_knob[K_YIELD_GATE_US] = 0;
+  g_knob[K_YIELD_STREAMS] = 2;
+  g_knob[K_YIELD_ALWAYS] = 0;   // A/B: slice even when no hook has run lately
 }
 
 static inline int knob(KnobId id) {
@@ -111,10 +116,13 @@ static inline int knob(KnobId id) {
 // host_path.hip reads the zero-copy knob through this (library-internal)
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_window_sc(void) { return knob(K_WINDOW_SC); }
-extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us) {
+extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us,
+                                                                        int *streams, int *always) {
   *slice_kb = knob(K_YIELD_SLICE_KB);
   *depth = knob(K_YIELD_DEPTH);
   *gate_us = knob(K_YIELD_GATE_US);
+  *streams = knob(K_YIELD_STREAMS);
+  *always = knob(K_YIELD_ALWAYS);
 }
 
 static int set_err(int code, const char *fmt, const char *what) {
@@ -2982,6 +2990,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_SLICE_KB: return v >= 0 && v <= (1 << 20);
     case K_YIELD_DEPTH: return v >= 1 && v <= 16;
     case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
+    case K_YIELD_STREAMS: return v >= 1 && v <= 4;
     default: return v == 0 || v == 1;  // on / off knobs
   }
 }
@@ -3578,6 +3587,8 @@ struct fecgpu_block_svc {
   uint64_t deadline_us = 2000;      // a request not served by then is withdrawn (svc_withdraw)
   uint64_t backoff_until = 0;       // after a withdrawal the calls take the launch path until then (us)
   uint64_t misses = 0;              // requests withdrawn at the deadline
+  uint64_t t_launch_us = 0;         // the running worker's launch, host clock
+  uint64_t t_done_us = 0;           // the last request it finished, host clock
   std::mutex mu;
 };
 
@@ -3648,9 +3659,16 @@ void fecgpu_block_svc_destroy(fecgpu_block_svc_t *v) {
   delete v;
 }
 
-// (re)launch the worker unless one is running
+// (re)launch the worker unless one is running.  A worker that finished a request within the last 5 ms
+// and was launched less than 30 ms ago is running for sure (it ends after 20 ms idle, 50 ms in all):
+// then no runtime call is made, one fewer per hook beside a bulk job's own launches and event waits in
+// the same runtime (a worker that faults is still caught by the poll loop's periodic query).
 static int svc_ensure(fecgpu_block_svc_t *v) {
-  if (v->launched && hipEventQuery(v->ev) == hipErrorNotReady) return FECGPU_OK;
+  if (v->launched) {
+    const uint64_t now = svc_now_us();
+    if (now - v->t_done_us < 5000 && now - v->t_launch_us < 30000) return FECGPU_OK;
+    if (hipEventQuery(v->ev) == hipErrorNotReady) return FECGPU_OK;
+  }
   (void)hipGetLastError();
   __atomic_store_n(&v->mb->quit, 0ull, __ATOMIC_RELEASE);
   hipLaunchKernelGGL(k_block_svc, dim3(1), dim3(kLdsThreads), kSvcLds, v->stream, v->mb_dev, kSvcIdleTicks,
@@ -3658,6 +3676,8 @@ static int svc_ensure(fecgpu_block_svc_t *v) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(v->ev, v->stream));
   v->launched = true;
+  v->t_launch_us = svc_now_us();
+  v->t_done_us = 0;
   return FECGPU_OK;
 }
 
@@ -3721,6 +3741,7 @@ static int svc_run(fecgpu_block_svc_t *v) {
   g_svc_pending.fetch_add(1);
   const int rc = svc_run_posted(v, t0);
   g_svc_pending.fetch_sub(1);
+  if (rc == FECGPU_OK) v->t_done_us = svc_now_us();
   return rc;
 }
 static int svc_run_posted(fecgpu_block_svc_t *v, uint64_t t0) {

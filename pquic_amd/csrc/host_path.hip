@@ -178,12 +178,15 @@ static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 // (profiles/r05_hook_sweep.log; rocprofv3 trace in profiles/r05_hook_trace_summary.txt: the slow calls
 // spend no time in HIP calls and involve no worker launch -- the resident worker's reads wait).  So
 // while the block service is in use (a hook request within the last kYieldWindowUs), a zero-copy launch
-// is cut into slices of about yield_slice_kb of payload on one stream, at most yield_depth in flight
-// (knobs): a hook then waits for at most the slice running when it arrives.  Optionally (yield_gate_us)
-// no slice starts while a hook request is pending.  Without hooks nothing changes (one launch).
+// is cut into slices of about yield_slice_kb of payload, alternating over yield_streams of the context's
+// streams (consecutive slices overlap, so the cut costs less), at most yield_depth in flight (knobs;
+// defaults and their measurement in fec_engine.hip knobs_default).  Optionally (yield_gate_us) no
+// slice starts while a hook request is pending.  Without hooks nothing changes (one launch).  The
+// hooks still wait for the slices running when they arrive; the slice size trades their p99 against
+// the bulk call's time (about 60-80 us of PCIe transfer per 2.5 MiB slice).
 int fecgpu_svc_hooks_pending(void);                                  // fec_engine.hip (library-internal)
 uint64_t fecgpu_svc_last_request_us(void);                           // fec_engine.hip (library-internal)
-void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us);     // fec_engine.hip (library-internal)
+void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us, int *streams, int *always);  // fec_engine.hip
 namespace {
 constexpr uint64_t kYieldWindowUs = 100000;
 std::atomic<uint64_t> g_yield_slices{0}, g_yield_waits{0};
@@ -196,15 +199,15 @@ uint64_t mono_us() {
 
 struct Pacer {
   fecgpu_host_ctx_t *c;
-  hipStream_t st;
   uint64_t slice = 0;  // blocks per slice; 0: hooks idle or the call is small, launch it whole
   int n = 0;           // slices launched
-  int depth = 4, gate_us = 0;
-  Pacer(fecgpu_host_ctx_t *c_, hipStream_t st_, uint64_t nblocks, size_t bytes_per_block) : c(c_), st(st_) {
+  int depth = 4, gate_us = 0, streams = 1;
+  Pacer(fecgpu_host_ctx_t *c_, uint64_t nblocks, size_t bytes_per_block) : c(c_) {
+    int kb = 0, always = 0;
+    fecgpu_knob_yield(&kb, &depth, &gate_us, &streams, &always);
     const uint64_t last = fecgpu_svc_last_request_us();
-    if (!last || mono_us() - last > kYieldWindowUs) return;
-    int kb = 0;
-    fecgpu_knob_yield(&kb, &depth, &gate_us);
+    if (!always && (!last || mono_us() - last > kYieldWindowUs)) return;
+    if (streams > c->ns) streams = c->ns;
     if (!kb || depth > kMaxYieldDepth) return;
     uint64_t per = ((uint64_t)kb << 10) / (bytes_per_block ? bytes_per_block : 1);
     if (per < 32) per = 32;
@@ -213,6 +216,8 @@ struct Pacer {
       if (!c->yev[i] && hipEventCreateWithFlags(&c->yev[i], hipEventDisableTiming) != hipSuccess) return;
     slice = per;
   }
+  // the stream of the next slice (slices alternate over `streams` of the context's streams)
+  hipStream_t stream(hipStream_t whole) const { return slice ? c->slot[n % streams].st : whole; }
   // before slice n: at most `depth` in flight, and (gate) none started while a hook request is pending
   hipError_t before() {
     if (!slice) return hipSuccess;
@@ -228,7 +233,9 @@ struct Pacer {
   hipError_t after() {
     if (!slice) return hipSuccess;
     g_yield_slices++;
-    return hipEventRecord(c->yev[n++ % depth], st);
+    const hipError_t e = hipEventRecord(c->yev[n % depth], c->slot[n % streams].st);
+    n++;
+    return e;
   }
 };
 }  // namespace
@@ -275,20 +282,21 @@ int fecgpu_rlc_encode_host(fecgpu_host_ctx_t *c, const void *src, void *rep, uin
   int si = 0, rc = FECGPU_OK;
   if (zs && zr) {  // page-locked, hooks in use: slices that yield to them (Pacer)
     Slot &s = c->slot[0];
-    Pacer pc(c, s.st, nblocks, sb + rb);
+    Pacer pc(c, nblocks, sb + rb);
     if (pc.slice) {
       const uint32_t *df = nullptr;
       do {
         if (fbn) {
           LCHK(grow(&s.d_aux, &s.cap_aux, nblocks * 4));
           LCHK(hipMemcpyAsync(s.d_aux, fbn, nblocks * 4, hipMemcpyHostToDevice, s.st));
+          if (pc.streams > 1) LCHK(hipStreamSynchronize(s.st));  // slices on the other streams read it
           df = (const uint32_t *)s.d_aux;
         }
         for (uint64_t b0 = 0; b0 < nblocks; b0 += pc.slice) {
           const uint64_t m = nblocks - b0 < pc.slice ? nblocks - b0 : pc.slice;
           LCHK(pc.before());
           if ((rc = fecgpu_rlc_encode(zs + b0 * sb, zr + b0 * rb, m, k, r, L, (uint32_t)((fbn_base + b0) & 0xffffffu),
-                                      df ? df + b0 : nullptr, s.st)))
+                                      df ? df + b0 : nullptr, pc.stream(s.st))))
             break;
           LCHK(pc.after());
         }
@@ -342,11 +350,14 @@ int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       dr = (const uint64_t *)(a + nblocks * k * 8);
       df = fbn ? (const uint32_t *)(a + nblocks * (k + r) * 8) : nullptr;
     }
-    Pacer pc(c, s.st, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
+    Pacer pc(c, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
+    if (pc.slice && pc.streams > 1) LCHK(hipStreamSynchronize(s.st));  // copied tables, read from other streams
     for (uint64_t b0 = 0, step = pc.slice ? pc.slice : nblocks; b0 < nblocks; b0 += step) {
       const uint64_t m = nblocks - b0 < step ? nblocks - b0 : step;
       LCHK(pc.before());
-      if ((rc = fecgpu_rlc_encode_rows(ds + b0 * k, dr + b0 * r, m, k, r, L, 0, df ? df + b0 : nullptr, s.st))) break;
+      if ((rc = fecgpu_rlc_encode_rows(ds + b0 * k, dr + b0 * r, m, k, r, L, 0, df ? df + b0 : nullptr,
+                                       pc.stream(s.st))))
+        break;
       LCHK(pc.after());
     }
   } while (0);
@@ -529,16 +540,18 @@ int fecgpu_rlc_decode_host_seeded(fecgpu_host_ctx_t *c, void *src, const void *r
 int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, const uint64_t *rep_rows,
                                 uint64_t nblocks, uint32_t k, uint32_t r, uint32_t L, const uint32_t *seeds,
                                 const uint64_t *sp, const uint64_t *rp, uint8_t *status, uint64_t *recovered) {
-  if (!c || !src_rows || !rep_rows || !sp || !rp || !status || !recovered || (r && !seeds)) return FECGPU_ERR_INVALID;
+  if (!c || !src_rows || (r && (!rep_rows || !seeds)) || !sp || !rp || !status || !recovered) return FECGPU_ERR_INVALID;
   if (!nblocks) return FECGPU_OK;
   std::lock_guard<std::mutex> g(c->mu);
   HCHK(hipSetDevice(c->device));
   Slot &s = c->slot[0];
   const uint32_t nseed = r ? r : 1;
-  // every array page-locked (the batching adapter's job tables): the kernels use them in place
+  // every array page-locked (the batching adapter's job tables): the kernels use them in place.  With
+  // r == 0 the repair table and seeds have no entries and are never read: the source table stands in
   const uint64_t *ds = (const uint64_t *)mapped_host(src_rows, nblocks * k * 8);
-  const uint64_t *dr = ds ? (const uint64_t *)mapped_host(rep_rows, nblocks * nseed * 8) : nullptr;
-  const uint32_t *dseed = dr ? (const uint32_t *)mapped_host(seeds, nblocks * nseed * 4) : nullptr;
+  const uint64_t *dr = !ds ? nullptr : r ? (const uint64_t *)mapped_host(rep_rows, nblocks * r * 8) : ds;
+  const uint32_t *dseed = !dr ? nullptr : r ? (const uint32_t *)mapped_host(seeds, nblocks * r * 4)
+                                            : (const uint32_t *)ds;
   const uint64_t *dsp = dseed ? (const uint64_t *)mapped_host(sp, nblocks * 16) : nullptr;
   const uint64_t *drp = dsp ? (const uint64_t *)mapped_host(rp, nblocks * 16) : nullptr;
   uint8_t *dst = drp ? mapped_host(status, nblocks) : nullptr;
@@ -560,7 +573,7 @@ int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       drec = m + 4 * nblocks;
       dst = (uint8_t *)(m + 6 * nblocks);
       LCHK(hipMemcpyAsync((void *)ds, src_rows, nblocks * k * 8, hipMemcpyHostToDevice, s.st));
-      LCHK(hipMemcpyAsync((void *)dr, rep_rows, nblocks * nseed * 8, hipMemcpyHostToDevice, s.st));
+      if (r) LCHK(hipMemcpyAsync((void *)dr, rep_rows, nblocks * r * 8, hipMemcpyHostToDevice, s.st));
       if (r) LCHK(hipMemcpyAsync((void *)dseed, seeds, nblocks * r * 4, hipMemcpyHostToDevice, s.st));
       LCHK(hipMemcpyAsync((void *)dsp, sp, nblocks * 16, hipMemcpyHostToDevice, s.st));
       LCHK(hipMemcpyAsync((void *)drp, rp, nblocks * 16, hipMemcpyHostToDevice, s.st));
@@ -570,12 +583,15 @@ int fecgpu_rlc_decode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
       LCHK(hipMemcpyAsync(recovered, drec, nblocks * 16, hipMemcpyDeviceToHost, s.st));
       break;
     }
-    Pacer pc(c, s.st, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
+    Pacer pc(c, nblocks, (size_t)(k + r) * L);  // hooks in use: slices that yield to them
     for (uint64_t b0 = 0, step = pc.slice ? pc.slice : nblocks; b0 < nblocks; b0 += step) {
       const uint64_t m = nblocks - b0 < step ? nblocks - b0 : step;
       LCHK(pc.before());
+      // one workspace per stream the slices alternate over
+      Slot &ws = c->slot[pc.slice ? pc.n % pc.streams : 0];
+      if (&ws != &s) LCHK(grow(&ws.d_ws, &ws.cap_ws, fecgpu_rlc_decode_workspace(m, k, r)));
       if ((rc = fecgpu_rlc_decode_rows(ds + b0 * k, dr + b0 * nseed, m, k, r, L, dseed + b0 * nseed, dsp + 2 * b0,
-                                       drp + 2 * b0, dst + b0, drec + 2 * b0, s.d_ws, s.cap_ws, s.st)))
+                                       drp + 2 * b0, dst + b0, drec + 2 * b0, ws.d_ws, ws.cap_ws, pc.stream(s.st))))
         break;
       LCHK(pc.after());
     }

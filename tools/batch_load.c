@@ -692,7 +692,7 @@ struct bulk_arg {
 static void *bulk_main(void *p) {
     struct bulk_arg *a = p;
     const size_t sb = (size_t)a->blocks * 16 * 1200, rb = (size_t)a->blocks * 4 * 1200;
-    fecgpu_host_ctx_t *c = fecgpu_host_ctx_create(a->device, 2, (size_t)64 << 20);
+    fecgpu_host_ctx_t *c = fecgpu_host_ctx_create(a->device, 4, (size_t)64 << 20);
     uint8_t *src = fecgpu_host_alloc(sb), *rep = fecgpu_host_alloc(rb);
     if (!c || !src || !rep) {
         a->rc = -1;
@@ -806,4 +806,26 @@ out:
     if (c) fecgpu_host_ctx_destroy(c);
     munmap(arena, bytes);
     return rc;
+}
+
+/* The bulk job of bl_hook_latency_loaded alone: `ncalls` back-to-back fecgpu_rlc_encode_host calls of
+ * `blocks` k16 r4 L1200 blocks in page-locked memory.  out: [0] ms per call, [1] GiB/s of sources. */
+int bl_bulk_rate(int device, int blocks, int ncalls, double out[2]) {
+    const size_t sb = (size_t)blocks * 16 * 1200, rb = (size_t)blocks * 4 * 1200;
+    fecgpu_host_ctx_t *c = fecgpu_host_ctx_create(device, 4, (size_t)64 << 20);
+    uint8_t *src = fecgpu_host_alloc(sb), *rep = fecgpu_host_alloc(rb);
+    int rc = -1;
+    if (c && src && rep) {
+        xorshift_fill(src, sb, 0x5EEDF3C0);
+        rc = fecgpu_rlc_encode_host(c, src, rep, (uint64_t)blocks, 16, 4, 1200, 0, NULL);  /* warm-up */
+        const uint64_t t0 = now_us();
+        for (int n = 0; n < ncalls && !rc; n++) rc = fecgpu_rlc_encode_host(c, src, rep, (uint64_t)blocks, 16, 4, 1200, 0, NULL);
+        const double s = (now_us() - t0) * 1e-6;
+        out[0] = s * 1e3 / ncalls;
+        out[1] = (double)ncalls * sb / s / 1073741824.0;
+    }
+    fecgpu_host_free(src);
+    fecgpu_host_free(rep);
+    if (c) fecgpu_host_ctx_destroy(c);
+    return rc ? -1 : 0;
 }

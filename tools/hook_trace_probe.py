@@ -42,20 +42,31 @@ lib.bl_hook_calls.argtypes = [C.POINTER(C.c_uint64), C.c_long]
 lib.bl_hook_calls.restype = C.c_long
 rc = 0
 if pacer:
-    for kb, depth, gate in ((0, 4, 0), (3072, 4, 0), (1536, 4, 0), (6144, 4, 0), (3072, 2, 0), (3072, 8, 0),
-                            (3072, 4, 50), (1536, 8, 0), (0, 4, 0)):
-        eng.set_knob("yield_slice_kb", kb)
-        eng.set_knob("yield_depth", depth)
-        eng.set_knob("yield_gate_us", gate)
+    def knobs(kb, depth, gate, streams, always):
+        for n, v in (("yield_slice_kb", kb), ("yield_depth", depth), ("yield_gate_us", gate),
+                     ("yield_streams", streams), ("yield_always", always)):
+            eng.set_knob(n, v)
+    # the bulk job alone, slices forced (what slicing costs without any hook)
+    lib.bl_bulk_rate.argtypes = [C.c_int, C.c_int, C.c_int, D]
+    for kb, streams, depth in ((0, 1, 4), (2048, 2, 16), (2560, 2, 16), (3072, 2, 16), (4096, 2, 16)):
+        knobs(kb, depth, 0, streams, 1)
+        out = (C.c_double * 2)()
+        rc |= lib.bl_bulk_rate(0, 4096, 200, out)
+        print(f"bulk alone, slices {kb:5d} KiB on {streams} stream(s), depth {depth}: {out[0]:.3f} ms per 4096-block call "
+              f"({out[1]:.1f} GiB/s of sources)", flush=True)
+    for kb, depth, gate, streams in ((0, 4, 0, 1), (2048, 16, 0, 2), (2560, 16, 0, 2), (3072, 16, 0, 2),
+                                     (2048, 12, 0, 2), (4096, 16, 0, 2), (2048, 16, 0, 2), (3072, 16, 0, 2),
+                                     (0, 4, 0, 1)):
+        knobs(kb, depth, gate, streams, 0)
         s0 = eng.stats()
         lo = (C.c_double * 11)()
         rc |= lib.bl_hook_latency_loaded(0, 4096, ncalls, lo)
         s1 = eng.stats()
         gibs = 4096 * 16 * 1200 / (lo[9] * 1e-3) / 2**30 if lo[9] else 0
-        print(f"slice {kb:5d} KiB depth {depth:2d} gate {gate:4d} us: generate p50 {lo[0]:.0f} p99 {lo[1]:.0f} us, "
-              f"recover p50 {lo[3]:.0f} p99 {lo[4]:.0f} us; bulk {lo[7]:.0f} calls, mean {lo[9]:.3f} ms "
-              f"({gibs:.1f} GiB/s of sources), max {lo[10]:.2f} ms; slices {s1['yield_slices'] - s0['yield_slices']}, "
-              f"held {s1['yield_waits'] - s0['yield_waits']}", flush=True)
+        print(f"hooks + bulk, slices {kb:5d} KiB depth {depth:2d} gate {gate:4d} us streams {streams}: generate p50 "
+              f"{lo[0]:.0f} p99 {lo[1]:.0f} us, recover p50 {lo[3]:.0f} p99 {lo[4]:.0f} us; bulk {lo[7]:.0f} calls, "
+              f"mean {lo[9]:.3f} ms ({gibs:.1f} GiB/s of sources), max {lo[10]:.2f} ms; slices "
+              f"{s1['yield_slices'] - s0['yield_slices']}, held {s1['yield_waits'] - s0['yield_waits']}", flush=True)
     sys.exit(0 if rc == 0 else 1)
 for bulk in ((4096, 1024, 512, 256) if sweep else (4096,)):
     lo = (C.c_double * 11)()
