@@ -2274,8 +2274,18 @@ static bool launch_encode_sc(const uint8_t *sym, uint8_t *rep, uint64_t nwin, in
 // ---------------------------------------------------------------------------------------------
 #define FEC_BS2_D(MODE, RT) FEC_BS2_D_##MODE##_RT##RT
 
-// ring depths (sources in flight + 1) of the shipped ring bodies: 16-repair / 16-unknown tiles
-struct Bs2Depth16 { static constexpr int enc = FEC_BS2_D(ENC, 16), dec = FEC_BS2_D(DEC, 16); };
+// ring depths (sources in flight + 1) of the shipped ring bodies: 16-repair / 16-unknown tiles.  A build
+// whose generator also emitted 4-unknown ring bodies (FEC_GEN2_TILES=4,16) can run the 4-unknown
+// recover tiles on the ring as well (knob ring = 4; A/B experiments)
+template <int RT> struct Bs2Depth;
+template <> struct Bs2Depth<16> { static constexpr int enc = FEC_BS2_D(ENC, 16), dec = FEC_BS2_D(DEC, 16); };
+#ifdef FEC_BS2_D_DEC_RT4
+#define FEC_BS2_HAS_RT4 1
+template <> struct Bs2Depth<4> { static constexpr int enc = FEC_BS2_D(ENC, 4), dec = FEC_BS2_D(DEC, 4); };
+#else
+#define FEC_BS2_HAS_RT4 0
+#endif
+using Bs2Depth16 = Bs2Depth<16>;
 
 // Lane geometry of one chunk of cb bytes (cb >= 16) as 16-B pieces, the last pulled back to end at cb.
 // DMA: instruction 1 moves pieces 0..63 (lane = piece), instruction 2 pieces 64.. (lane = piece - 64);
@@ -2332,8 +2342,15 @@ __device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp
   if (two) BS2_CALL_ENC(16, 2); else BS2_CALL_ENC(16, 1);
 }
 
+template <int RT>
 __device__ __forceinline__ void bs2_dec_call(bool two, uint32_t ia, uint32_t oa, uint32_t nsrc, int k, uint32_t ca,
                                              uint32_t ring, const Bs2Lanes &ln) {
+#if FEC_BS2_HAS_RT4
+  if constexpr (RT == 4) {
+    if (two) BS2_CALL_DEC(4, 2); else BS2_CALL_DEC(4, 1);
+    return;
+  }
+#endif
   if (two) BS2_CALL_DEC(16, 2); else BS2_CALL_DEC(16, 1);
 }
 
@@ -2437,7 +2454,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
 // CW: as in k_rlc_encode_bs2, kCwWaves waves code the group's (block, chunk) items; the setup is
 // spread over every thread of the workgroup and wave 0 writes the statuses once all items are done.
 template <int RT, bool CW>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 ? 3 : RT == 8 ? 4 : 1)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 ? 3 : RT >= 4 ? 4 : 1)))
 void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint8_t *ws, int r0, int G,
@@ -2450,7 +2467,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
   const int tid = CW ? (int)threadIdx.x : lane, nthr = CW ? (int)blockDim.x : 64;
   RecoverLds<RT> S(lds, G, k);
   const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) +
-                        (uint32_t)wave * Bs2Depth16::dec * slotb;
+                        (uint32_t)wave * Bs2Depth<RT>::dec * slotb;
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = ilv ? NG : 1;
   {  // one group per workgroup: no grid-stride loop invariants live across the asm body
@@ -2526,7 +2543,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
         const Bs2Lanes ln(lane_fresh(), cb, (uint32_t)c0, ring);
-        bs2_dec_call(ln.npieces > 64, lds_addr(S.intab + (size_t)t * k), lds_addr(S.rec + (size_t)t * kDecRec),
+        bs2_dec_call<RT>(ln.npieces > 64, lds_addr(S.intab + (size_t)t * k), lds_addr(S.rec + (size_t)t * kDecRec),
                      (uint32_t)k, k, lds_addr(S.coef + (size_t)t * k * RecoverLds<RT>::CSB), ring, ln);
       }
     } else if (nact) {
@@ -2534,7 +2551,7 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
         const int c0 = ch * chunk_bytes;
         const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
         const Bs2Lanes ln(lane_fresh(), cb, (uint32_t)c0, ring);
-        bs2_dec_call(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
+        bs2_dec_call<RT>(ln.npieces > 64, lds_addr(S.intab), lds_addr(S.rec), (uint32_t)(nact * k), k,
                          lds_addr(S.coef), ring, ln);
       }
     }
@@ -2587,8 +2604,11 @@ static inline int bs2_group(int RT, int k, int per_j, int per_block, bool enc, i
 // RT = 8: 4, RT = 16: 2 waves per SIMD).
 // resident waves per CU the LDS budget is sized for (RT = 16 reaches 3 per SIMD only with the
 // two-temporary register map of a FEC_GEN2_BASE=8 build)
+#ifndef FEC_BS2_RT4_WAVES_PER_CU
+#define FEC_BS2_RT4_WAVES_PER_CU 16
+#endif
 static inline int bs2_waves_per_cu(int RT) {
-  return RT <= 4 ? 20 : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 4 * FEC_BS2_RT16_WAVES : 8;
+  return RT <= 4 ? FEC_BS2_RT4_WAVES_PER_CU : RT == 8 ? 16 : FEC_BS2_BASE <= 8 ? 4 * FEC_BS2_RT16_WAVES : 8;
 }
 
 // Chunk waves (knob chunk_waves, default on): symbols wider than one column chunk are coded by
@@ -2630,7 +2650,7 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
                                uint8_t *ws, int r0, uint8_t *status, uint64_t *recovered, hipStream_t s,
                                uint8_t *dst, int dst_rows) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
-  const size_t ring_bytes = (size_t)Bs2Depth16::dec * slotb;
+  const size_t ring_bytes = (size_t)Bs2Depth<RT>::dec * slotb;
   const int per_j = FEC_BS_COEF_ROW_BYTES(RT) + 8, per_block = kDecRec + 80;
   if (const int G = c.nchunks > 1 ? cw_group(RT, k, per_j, per_block, ring_bytes, nb) : 0) {
     const size_t lds = pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) + kCwWaves * ring_bytes;
@@ -2648,10 +2668,20 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
 // of at least D sources (one epilogue in any wait window, see gen_bitslice.py body2); knob ring = 0
 // keeps those tiles on the register-prefetch body (A/B).
 static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
-  if (knob(K_RING) == 0 || rt != 16 || cfg.vec != 16) return false;
-  return (int)k >= (enc ? Bs2Depth16::enc : Bs2Depth16::dec);
+  if (knob(K_RING) == 0 || cfg.vec != 16) return false;
+  if (rt == 16) return (int)k >= (enc ? Bs2Depth16::enc : Bs2Depth16::dec);
+#if FEC_BS2_HAS_RT4
+  if (rt == 4 && !enc && knob(K_RING) == 4) return (int)k >= Bs2Depth<4>::dec;
+#endif
+  return false;
 }
 
+#if FEC_BS2_HAS_RT4
+#define FEC_BS2_DISPATCH_DEC(FN, ...) \
+  if (rt == 4) FN<4>(__VA_ARGS__); else FN<16>(__VA_ARGS__);
+#else
+#define FEC_BS2_DISPATCH_DEC(FN, ...) FN<16>(__VA_ARGS__);
+#endif
 #define FEC_BS2_DISPATCH(FN, ...) FN<16>(__VA_ARGS__);
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
@@ -2983,7 +3013,7 @@ static bool knob_value_ok(int id, int v) {
     case K_PLAN: return v >= PLAN_AUTO && v <= PLAN_WREG;
     case K_ENC_RT: return v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16;
     case K_ENC_W: return v >= 0 && v <= 4;
-    case K_RING: return v == 0 || v == 2;
+    case K_RING: return v == 0 || v == 2 || (v == 4 && FEC_BS2_HAS_RT4);
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;
     case K_DEC_WAVES: return v >= 0 && v <= 8;
@@ -3333,7 +3363,7 @@ static int decode_apply_impl(const void *src, const void *rep, void *dst, uint64
   const bool ring = use_ring(rt, k, cfg, false);
   for (int r0 = 0; r0 < (int)L.em; r0 += rt) {
     if (ring) {
-      FEC_BS2_DISPATCH(launch_recover_bs2, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
+      FEC_BS2_DISPATCH_DEC(launch_recover_bs2, (uint8_t *)src, (const uint8_t *)rep, nblocks, (int)k, (int)r,
                        (int)symbol_size, cfg, ws, r0, fused ? status : nullptr, fused ? recovered : nullptr, s,
                        (uint8_t *)dst, dst_rows)
     } else {

@@ -733,7 +733,9 @@ def regmap2(mode: str, ntmp: int = 4):
     return {"pl": list(range(B, B + 8)), "tl": tl, "th": th, "tmp": tmp, "acc": nxt}
 
 
-S2_SLOT = 2048  # bytes per ring slot: a whole column chunk; the unrolled steps address slots by immediates
+# bytes per ring slot: a whole column chunk; the unrolled steps address slots by immediates.  FEC_GEN2_SLOT
+# (A/B builds only): smaller slots fit more of them in LDS, valid only for chunks that fit a slot
+S2_SLOT = int(os.environ.get("FEC_GEN2_SLOT", "2048"))
 
 
 def body2(mode: str, RT: int, D: int, NDMA: int):

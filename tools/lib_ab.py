@@ -2,7 +2,9 @@
 path: k16 r4 encode and k16 e4 decode apply (2^20 blocks, random erasures, recovered rows at their
 slots and packed), k32 r8 encode and k32 e8 decode apply (2^19 blocks).  Every build runs on the same
 buffers; variants alternate over cycles; prints the median and min kernel time per (variant, case).
-usage: python tools/lib_ab.py name=path.so[:knob=value,...] ... [--cycles=N]"""
+--check: before timing, every variant's packed apply (k16 e4, k32 e8) must give the first variant's statuses,
+recovered masks and recovered rows (the rows of unknowns whose bit is set), byte for byte.
+usage: python tools/lib_ab.py name=path.so[:knob=value,...] ... [--cycles=N] [--check]"""
 import ctypes as C
 import os
 import statistics
@@ -52,7 +54,8 @@ def dec_setup(k, r, e, L, nb, seed):
     ws = eng0.alloc_workspace(nb, k, r)
     eng0.rlc_decode_plan(sp, rp, k, r, nb, ws)
     rec_pk = torch.empty((nb, min(k, r), L), dtype=torch.uint8, device=dev)
-    return dict(src=src, rep=rep, work=work, st=st, rec=rec, ws=ws, rec_pk=rec_pk, k=k, r=r, L=L, nb=nb)
+    return dict(src=src, rep=rep, work=work, st=st, rec=rec, ws=ws, rec_pk=rec_pk, k=k, r=r, L=L, nb=nb,
+                miss=miss.sort(dim=1).values.to(dev))
 
 
 cases = []
@@ -67,6 +70,31 @@ d32 = dec_setup(32, 8, 8, 1200, 1 << 19, 0x5EEDF3C1)
 cases.append(("enc k32r8", lambda e: e.rlc_encode(d32["src"], d32["rep"], 32, 8, 1200)))
 cases.append(("app_pk k32e8", lambda e: e.rlc_decode_apply_packed(d32["work"], d32["rep"], d32["rec_pk"], d32["st"],
                                                                    d32["rec"], 32, 8, 1200, d32["nb"], d32["ws"])))
+if "--check" in sys.argv:
+    for d, e_ in ((d16, 4), (d32, 8)):
+        ref = None
+        for name, _ in variants:
+            e = engines[name]
+            for kn, kv in knobs[name].items():
+                e.set_knob(kn, kv)
+            d["rec_pk"].fill_(0x5A)
+            d["st"].fill_(0xEE)
+            e.rlc_decode_apply_packed(d["work"], d["rep"], d["rec_pk"], d["st"], d["rec"], d["k"], d["r"], d["L"],
+                                      d["nb"], d["ws"])
+            torch.cuda.synchronize()
+            for kn in knobs[name]:
+                e.set_knob(kn, 0)
+            # rows of unknowns whose recovered bit is set (the u-th missing source of the block)
+            bits = ((d["rec"][:, 0:1] >> d["miss"].clamp(max=63)) & 1).bool() & (d["miss"] < 64)
+            got = (d["st"].clone(), d["rec"].clone(), d["rec_pk"][:, :e_][bits].clone())
+            if ref is None:
+                ref = got
+                assert (got[0] == 0).sum().item() > d["nb"] * 0.9
+            else:
+                ok = all(torch.equal(a, b) for a, b in zip(got, ref))
+                print(f"check k{d['k']} e{e_}: {name} {'equal to' if ok else 'DIFFERS from'} {variants[0][0]}", flush=True)
+                if not ok:
+                    sys.exit(1)
 times = {}
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 for cyc in range(cycles):
