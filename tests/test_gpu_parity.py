@@ -514,6 +514,64 @@ def test_full_size_bench_decode_path_k16(eng, oracle):
     torch.cuda.empty_cache()
 
 
+def test_full_size_bench_path_k64_r16_L9000(eng, oracle):
+    """configs[4] at the bench's own size (2^16 blocks of k64 r16, 9000-byte symbols, 16 random source
+    erasures per block: 37.7 GB of sources): the encode and the bench's staged decode (plan, then the
+    packed apply into new rows) on the LDS-ring bodies.  Statuses and recovered masks equal the
+    one-shot decode's, every recovered row of every recovered block equals its original
+    (check_recovered, the bench's gate), the rank-deficient share is the one the bench reports, and a
+    sample of 24 blocks equals the oracle's repair bytes, statuses and recovered bytes."""
+    sys.path.insert(0, ROOT)
+    from bench import check_recovered, make_erasures
+    nb, k, r, e, L = 1 << 16, 64, 16, 16, 9000
+    src = torch.empty((nb, k, L), dtype=torch.uint8, device=DEV)
+    eng.synth_fill(src, src.numel(), 0x64)
+    rep = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
+    eng.rlc_encode(src, rep, k, r, L)
+    sp, miss = make_erasures(torch, nb, k, e, 11, DEV)
+    rp = torch.zeros((nb, 2), dtype=torch.int64, device=DEV)
+    rp[:, 0] = (1 << r) - 1
+    ws = eng.alloc_workspace(nb, k, r)
+    work = src.clone()
+    idx = (torch.arange(nb, device=DEV).unsqueeze(1) * k + miss.to(DEV)).reshape(-1)
+    work.view(nb * k, L)[idx] = 0xA5  # the erased rows hold garbage; the apply must not read them
+    del idx
+    dst = torch.full((nb, e, L), 0x5A, dtype=torch.uint8, device=DEV)
+    st = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    rec = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+    eng.rlc_decode_stages(work, rep, sp, rp, st, rec, k, r, L, nb, ws, dst=dst, packed=True)
+    st1 = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    rec1 = torch.empty((nb, 2), dtype=torch.int64, device=DEV)
+    one = work.clone()
+    eng.rlc_decode(one, rep, sp, rp, st1, rec1, k, r, L)
+    torch.cuda.synchronize()
+    assert torch.equal(st, st1) and torch.equal(rec, rec1)
+    ok = st == 0
+    assert bool(((st == 0) | (st == 2)).all())
+    assert 0.03 < (st == 2).float().mean().item() < 0.09  # the bench's ref_ub share (~5.8 %)
+    check_recovered(torch, dst, src, ok, miss, nb, k, L, "configs[4] packed apply at 2^16 blocks")
+    del one, work
+    torch.cuda.empty_cache()
+    sample = np.sort(np.random.default_rng(4).choice(nb, 24, replace=False))
+    s_src = src[sample].cpu().numpy()
+    s_rep = rep[sample].cpu().numpy()
+    s_sp = sp.cpu().numpy().view(np.uint64)[sample]
+    s_rp = rp.cpu().numpy().view(np.uint64)[sample]
+    msort = miss.sort(dim=1).values.numpy()[sample]
+    got_st = st.cpu().numpy()[sample]
+    got_dst = dst[sample].cpu().numpy()
+    for t, b in enumerate(sample):
+        assert np.array_equal(s_rep[t:t + 1], oracle.rlc_encode_batch(s_src[t:t + 1], r, int(b))), b
+        ref = s_src[t:t + 1].copy()
+        ref[0, msort[t]] = 0
+        stb, recb = oracle.rlc_decode_batch(ref, s_rep[t:t + 1], s_sp[t:t + 1], s_rp[t:t + 1], int(b))
+        assert got_st[t] == stb[0], b
+        if stb[0] == 0:
+            assert np.array_equal(got_dst[t], ref[0, msort[t]]), b
+    del src, rep, dst
+    torch.cuda.empty_cache()
+
+
 def test_host_path_matches_oracle(oracle):
     """Host-resident entry points (pipelined H2D -> kernels -> D2H over 3 streams and
     sub-batches smaller than the batch) give the device results byte for byte."""

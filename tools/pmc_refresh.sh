@@ -8,7 +8,7 @@
 #     rlc_decode_apply_k16_e4=gpurun_out/TAG/k16:k_rlc_recover_bs<4:1048576 \
 #     rlc_encode_k32_r8=gpurun_out/TAG/k32:k_rlc_encode_bs<8:1048576 \
 #     rlc_encode_k64_r16_L9000=gpurun_out/TAG/k64e:k_rlc_encode_bs2<16:32768 \
-#     rlc_decode_apply_k64_e16=gpurun_out/TAG/k64d:k_rlc_recover_bs<16:32768
+#     rlc_decode_apply_k64_e16=gpurun_out/TAG/k64d:k_rlc_recover_bs2<16:32768
 set -o pipefail
 TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
