@@ -112,6 +112,7 @@ struct pquic_fec_batcher {
     pthread_cond_t cv_todo, cv_staged, cv_done;
     job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *post_head, *post_tail, *done_head, *done_tail;
     int inflight, stop, stagers_done;
+    uint32_t pf;                   /* completion prefetch distance in blocks (prefetch_syms; 0: off) */
     int last_slot;                 /* open[] slot of the last submission (caller thread) */
     job_t *completing;             /* finished job whose completions a bounded poll left part-done */
     uint32_t completing_i;         /* its next entry */
@@ -706,6 +707,9 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     if (!b) return NULL;
     b->cfg = *cfg;
     b->stride = fec_pad4(cfg->max_symbol);
+    const char *pfs = getenv("PQUIC_FEC_BATCH_PREFETCH");  /* read once per batcher, like the thread counts */
+    b->pf = pfs && atoi(pfs) >= 0 ? (uint32_t)atoi(pfs) : 8;
+    if (b->pf > 64) b->pf = 64;
     const size_t chunk = (size_t)cfg->batch_blocks * 20 * b->stride / (size_t)cfg->nstreams;
     const char *ne = getenv("PQUIC_FEC_BATCH_ENGINES");
     b->nengines = ne && atoi(ne) > 0 ? atoi(ne) : 2;
@@ -884,6 +888,40 @@ int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_f
     return submit(b, cnx, fb, OP_RECOVER, xor_scheme ? 1 : 0, now_us, done, user);
 }
 
+/* The symbols a completion hands to the framework -- a generate's repairs, a gathered recover's
+ * recovered sources -- are what the framework touches next (it sends their bytes, then frees them; the
+ * plugin allocator reads the slot header just before the data, picoquic/memory.c:123-127).  The kernel
+ * wrote their data over PCIe, so those lines are in no CPU cache.  Entry i + 2P's symbol structs and
+ * entry i + P's data lines are prefetched while entry i completes (P = b->pf, 0: off), so the misses
+ * overlap instead of stalling the caller one block at a time. */
+static void prefetch_syms(const job_t *j, uint32_t i, int data) {
+    if (GENERATES(j->op)) {
+        const entry_t *e = &j->ent[i];
+        pquic_repair_symbol_t *const *reps = j->reps + (size_t)i * j->r;
+        for (int x = 0; x < e->nalloc; x++) {
+            if (!data) {
+                __builtin_prefetch(reps[x], 0);
+            } else {
+                const uint8_t *d = reps[x]->data;
+                __builtin_prefetch(d - 8, 1);
+                __builtin_prefetch(d, 1);
+            }
+        }
+    } else if (j->gather) {
+        pquic_source_symbol_t *const *pre = j->pre + (size_t)i * j->k;
+        for (uint32_t x = 0; x < j->k; x++) {
+            if (!pre[x]) continue;
+            if (!data) {
+                __builtin_prefetch(pre[x], 0);
+            } else {
+                const uint8_t *d = pre[x]->data;
+                __builtin_prefetch(d - 8, 1);
+                __builtin_prefetch(d, 1);
+            }
+        }
+    }
+}
+
 /* Completes finished jobs, at most `budget` blocks (0: all): the finish halves of the protocol
  * operations, then done().  A job left part-done continues at the next call. */
 static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
@@ -921,9 +959,18 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
             if (GENERATES(j->op)) FEC_STAT_ADD(generate_calls, j->n); else FEC_STAT_ADD(recover_calls, j->n);
         }
         const uint32_t end = budget && j->n - i > budget - (uint32_t)n ? i + (budget - (uint32_t)n) : j->n;
+        const uint32_t pf = j->rc ? 0 : b->pf;
+        if (pf && i == 0) {  /* the job's first entries: their structs, then their data */
+            for (uint32_t x = 0; x < 2 * pf && x < j->n; x++) prefetch_syms(j, x, 0);
+            for (uint32_t x = 0; x < pf && x < j->n; x++) prefetch_syms(j, x, 1);
+        }
         for (; i < end; i++) {
             entry_t *e = &j->ent[i];
             if (i + 4 < j->n) __builtin_prefetch(j->ent[i + 4].fb, 1);  /* the blocks were last touched at submission */
+            if (pf) {
+                if (i + 2 * pf < j->n) prefetch_syms(j, i + 2 * pf, 0);
+                if (i + pf < j->n) prefetch_syms(j, i + pf, 1);
+            }
             protoop_arg_t ret;
             pquic_repair_symbol_t **reps = GENERATES(j->op) ? j->reps + (size_t)i * j->r : NULL;
             pquic_source_symbol_t **pre = j->op == OP_RECOVER && j->gather ? j->pre + (size_t)i * j->k : NULL;

@@ -123,9 +123,13 @@ static int present(const uint64_t *m, uint64_t b, uint32_t j) { return (int)((m[
 
 /* one RLC block from row pointers; rows are all L bytes */
 static void enc_rows(uint32_t fbn, uint32_t k, uint32_t r, uint32_t L, const uint8_t *const *s, uint8_t *const *o) {
+#ifdef STUB_NULL_ENGINE  /* host-cost profiling only (tools/sender_cpu_probe.py): the repairs are not computed */
+    (void)fbn; (void)k; (void)r; (void)L; (void)s; (void)o;
+#else
     uint16_t sl[MAXS], rl[MAXS];
     for (uint32_t j = 0; j < k; j++) sl[j] = (uint16_t)L;
     oracle_rlc_encode_block(fbn, (int)k, (int)r, s, sl, o, rl);
+#endif
 }
 /* one RLC decode from row pointers: missing sources' rows receive the recovered bytes */
 static void dec_rows(uint32_t k, uint32_t r, uint32_t L, uint8_t *const *s, const uint8_t *const *p,

@@ -17,6 +17,10 @@
 
 #include <pthread.h>
 #include <sched.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <ucontext.h>
+#include <unistd.h>
 
 #include "fecgpu.h"
 #include "pquic_fec_batch.h"
@@ -118,6 +122,58 @@ static uint64_t now_us(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+/* PC sampler for the sender thread's measured pass (bl_set_sampling; tools/sender_phase_probe.py
+ * --profile): a per-thread timer delivers SIGPROF to the sender thread alone every 1/hz s of wall time,
+ * and the handler records the interrupted instruction address.  Profiling aid only. */
+static int g_sample_hz;
+static uint64_t *g_samples;
+static volatile long g_nsamples;
+static long g_max_samples;
+static timer_t g_timer;
+static void on_sigprof(int sig, siginfo_t *si, void *uc) {
+    (void)sig; (void)si;
+    const long n = g_nsamples;
+    if (n < g_max_samples) {
+        g_samples[n] = (uint64_t)((ucontext_t *)uc)->uc_mcontext.gregs[REG_RIP];
+        g_nsamples = n + 1;
+    }
+}
+void bl_set_sampling(int hz, long max_samples) {
+    g_sample_hz = hz;
+    free(g_samples);
+    g_samples = hz > 0 ? calloc((size_t)max_samples, sizeof *g_samples) : NULL;
+    g_max_samples = g_samples ? max_samples : 0;
+    g_nsamples = 0;
+}
+long bl_samples(uint64_t *out, long max) {
+    const long n = g_nsamples < max ? g_nsamples : max;
+    if (n > 0) memcpy(out, g_samples, sizeof *out * (size_t)n);
+    return n;
+}
+static void sampling_start(void) {
+    if (g_sample_hz <= 0 || !g_samples) return;
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = on_sigprof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGPROF, &sa, NULL);
+    struct sigevent ev;
+    memset(&ev, 0, sizeof ev);
+    ev.sigev_notify = SIGEV_THREAD_ID;
+    ev.sigev_signo = SIGPROF;
+    ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+    if (timer_create(CLOCK_MONOTONIC, &ev, &g_timer)) return;
+    const long ns = 1000000000L / g_sample_hz;
+    struct itimerspec it = {{ns / 1000000000L, ns % 1000000000L}, {ns / 1000000000L, ns % 1000000000L}};
+    timer_settime(g_timer, 0, &it, NULL);
+}
+static void sampling_stop(void) {
+    if (g_sample_hz <= 0 || !g_samples) return;
+    timer_delete(g_timer);
+    signal(SIGPROF, SIG_IGN);
 }
 
 typedef struct {
@@ -390,6 +446,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
             rec0 = g_recovered;
         }
         if (g_sync) pthread_barrier_wait(g_sync), waits++;  /* bl_run_senders: every sender starts each pass together */
+        if (pass) sampling_start();
         t0 = now_us();
         t_wait = t_submit = 0;
         for (long blk = 0; blk < nb; blk++) {
@@ -447,6 +504,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     }
     pquic_fec_batch_drain(b);
     const uint64_t t_end = now_us();
+    sampling_stop();
     const double wall = (t_end - t0) * 1e-6;
     g_span[0] = t0;
     g_span[1] = t_end;
