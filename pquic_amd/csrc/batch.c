@@ -84,6 +84,8 @@ typedef struct job {
                                     * a missing source's entry is the row its recovered bytes go to) */
     pquic_source_symbol_t **pre;   /* recover gather: [cap][k] symbols allocated at submission for the missing
                                     * sources (written in place by the kernel), NULL where none */
+    uint64_t *cpm;                 /* recover gather: [cap][2] missing sources whose recovered row is staged
+                                    * (copied into its symbol at completion), set by the stagers */
     size_t pre_cap;
     uint64_t seq;                  /* flush order: completions are handed out in it */
     size_t srow_cap, rrow_cap;
@@ -217,6 +219,7 @@ static void job_free(job_t *j) {
     fecgpu_host_free(j->srow);
     fecgpu_host_free(j->rrow);
     free(j->pre);
+    free(j->cpm);
     free(j->copy);
     fecgpu_host_free(j->src);
     fecgpu_host_free(j->rep);
@@ -276,6 +279,8 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         j->pre_cap = (j->pre = calloc((size_t)cap * k, sizeof *j->pre)) ? (size_t)cap * k : 0;
         if (!j->pre) j->gather = 0;
     }
+    if (j->gather && op == OP_RECOVER && !j->cpm && !(j->cpm = malloc(sizeof *j->cpm * 2 * (size_t)cap)))
+        j->gather = 0;
     if (j->gather && (j->srow_cap < (size_t)cap * k || j->rrow_cap < (size_t)cap * r || !j->copy)) {
         if (j->srow_cap < (size_t)cap * k) {
             fecgpu_host_free(j->srow);
@@ -426,8 +431,8 @@ static void gather_recover_blocks(pquic_fec_batcher_t *b, job_t *j, uint32_t i0,
         const entry_t *e = &j->ent[i];
         const pquic_fec_block_t *fb = e->fb;
         const int whole = e->maxl == S;
-        uint64_t *sp = j->sp + 2 * (size_t)i, *rp = j->rp + 2 * (size_t)i;
-        sp[0] = sp[1] = rp[0] = rp[1] = 0;
+        uint64_t *sp = j->sp + 2 * (size_t)i, *rp = j->rp + 2 * (size_t)i, *cpm = j->cpm + 2 * (size_t)i;
+        sp[0] = sp[1] = rp[0] = rp[1] = cpm[0] = cpm[1] = 0;
         for (uint32_t x = 0; x < k; x++) {
             const pquic_source_symbol_t *ss = fb->source_symbols[x];
             const size_t o = ((size_t)i * k + x) * S;
@@ -447,6 +452,7 @@ static void gather_recover_blocks(pquic_fec_batcher_t *b, job_t *j, uint32_t i0,
                 const pquic_source_symbol_t *pre = j->pre[(size_t)i * k + x];
                 d = whole && pre ? heap_dev(b, pre->data, S, &hint) : 0;
                 inplace += d != 0;
+                if (!d) cpm[x >> 6] |= 1ull << (x & 63);  /* recovered into the staging row */
             }
             j->srow[(size_t)i * k + x] = d ? d : j->src_dev + o;
         }
@@ -908,6 +914,11 @@ static void prefetch_syms(const job_t *j, uint32_t i, int data) {
             }
         }
     } else if (j->gather) {
+        if (data) {  /* the status and masks the kernel wrote, the stagers' copy masks */
+            __builtin_prefetch(j->st + i, 0);
+            __builtin_prefetch(j->rec + 2 * (size_t)i, 0);
+            __builtin_prefetch(j->cpm + 2 * (size_t)i, 0);
+        }
         pquic_source_symbol_t *const *pre = j->pre + (size_t)i * j->k;
         for (uint32_t x = 0; x < j->k; x++) {
             if (!pre[x]) continue;
@@ -991,12 +1002,8 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
                 ret = fec_generate_attach(e->fb, reps, e->nalloc);
             } else if (pre) {
                 /* rows the kernel wrote into the staging area (no in-place row for them) are copied */
-                uint64_t copy[2] = {0, 0};
-                const uint64_t s0 = j->src_dev + (uint64_t)i * j->k * S;
-                for (uint32_t x = 0; x < j->k; x++)
-                    if (j->srow[(size_t)i * j->k + x] == s0 + (uint64_t)x * S) copy[x >> 6] |= 1ull << (x & 63);
-                ret = fec_recover_finish_pre(e->cnx, e->fb, j->st[i], j->rec + 2 * (size_t)i, pre, copy,
-                                             j->src + (size_t)i * j->k * S, S, e->maxl);
+                ret = fec_recover_finish_pre(e->cnx, e->fb, j->st[i], j->rec + 2 * (size_t)i, pre,
+                                             j->cpm + 2 * (size_t)i, j->src + (size_t)i * j->k * S, S, e->maxl);
             } else {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
                                          j->src + (size_t)i * j->k * S, S, e->maxl);
