@@ -46,8 +46,14 @@ static void mh_set_cnx(picoquic_cnx_t *cnx, access_key_t ak, uint16_t param, pro
 }
 
 static long g_fail_after = -1;  /* allocation-failure injection: the n-th allocation from now fails */
+static long g_fail_count = 1;   /* ... and this many in a row from there */
+static int g_arena_strict;      /* a full arena fails the allocation instead of falling back to the heap */
 
-void mh_fail_alloc_after(long n) { g_fail_after = n; }
+void mh_fail_alloc_after(long n) { g_fail_after = n; g_fail_count = 1; }
+void mh_fail_alloc_range(long n, long count) { g_fail_after = n; g_fail_count = count > 0 ? count : 1; }
+/* mh_arena_strict(1): a plugin without dynamic memory -- my_malloc_block returns NULL once its arena is
+ * full (picoquic/memory.c:72-110) */
+void mh_arena_strict(int on) { g_arena_strict = on; }
 
 /* Plugin-style memory arenas (picoquic_internal.h:576 memory[PLUGIN_MEMORY], carved into 2100-B
  * slots, picoquic/memory.c:181-191): allocations up to 2092 B come from the arena of the connection
@@ -112,7 +118,10 @@ static mh_arena_t *arena_of(picoquic_cnx_t *cnx, const void *p) {
 
 static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
     if (g_fail_after == 0) {
-        g_fail_after = -1;
+        if (--g_fail_count <= 0) {
+            g_fail_after = -1;
+            g_fail_count = 1;
+        }
         return NULL;
     }
     if (g_fail_after > 0) g_fail_after--;
@@ -127,6 +136,7 @@ static void *mh_malloc(picoquic_cnx_t *cnx, unsigned int size) {
             ar->used += MH_SLOT;
         }
         if (p) ar->live++;
+        else if (g_arena_strict) return NULL;
     }
     if (!p) p = malloc(size <= 2092 ? 2100 : size);
     if (p) g_live++;

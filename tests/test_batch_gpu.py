@@ -769,3 +769,48 @@ def test_batch_recover_arena_full_part_way_through_a_block():
     assert st["engine_errors"] == 0
     assert st["rows_in_place"] == 6 + 1 and st["rows_staged"] > 0, st
     bt.close()
+
+
+def test_batch_recover_frees_unrecovered_preallocations_first():
+    """A gathered recover allocates a symbol for every missing source at submission; the reference
+    allocates only for the sources it recovers, after decoding (rlc_fec_scheme_gf256.c:218-236).  The block:
+    k8 r4, sources 2, 3, 5, 6 missing, source 6 all zero, so only source 5 is recovered (the zero rule
+    drops 6 and what depends on it, :98-101).  The plugin arena returns NULL once full (my_malloc_block
+    without dynamic memory, picoquic/memory.c:72-110) and has three slots left after the received symbols:
+    the pre-allocations of 2, 3 and 5 fail (injected), 6's takes two slots.  The completion frees 6's
+    symbol before it allocates 5's anew, so source 5 is recovered, as the reference recovers it;
+    allocating in source order first would have found one free slot and skipped it."""
+    k, r, L = 8, 4, 1200
+    # 40960 B = 19 slots of 2112 B: 8 for the four received sources, 8 for the four repairs, 3 left
+    bt = Batch(1, max_symbol=L, arena=True, arena_bytes=40960)
+    bt.L.mh_arena_strict.argtypes = [C.c_int]
+    bt.L.mh_fail_alloc_range.argtypes = [C.c_long, C.c_long]
+    bt.L.mh_fail_alloc_after.argtypes = [C.c_long]
+    rng = np.random.default_rng(4)
+    o = Oracle()
+    full = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    fbn = int(rng.integers(0, 1 << 24))
+    full[6] = np.zeros(L, np.uint8)
+    reps = o.rlc_encode_block(fbn, full, r)[1]
+    miss = (2, 3, 5, 6)
+    srcs = [None if j in miss else full[j] for j in range(k)]
+    st, want = o.rlc_decode_block(fbn, srcs, list(reps))
+    assert sorted(want) == [5]
+    bt.L.mh_arena_strict(1)
+    try:
+        # allocations 0-15 build the received block; 16-21 are the pre-allocations of sources 2, 3, 5
+        # (symbol, then data, each), 22-23 source 6's
+        bt.L.mh_fail_alloc_range(2 * 4 + 2 * 4, 6)
+        t = bt.recover(False, fbn, srcs, list(reps), [(fbn << 8) | i for i in range(r)])
+        bt.L.mh_batch_drain()
+    finally:
+        bt.L.mh_fail_alloc_after(-1)
+        bt.L.mh_arena_strict(0)
+    ret, calls = bt.status(t)
+    assert calls == 1 and ret == 0
+    got, cur = bt.recovered(t)
+    assert sorted(got) == [5]
+    assert got[5].tobytes() == want[5].tobytes()
+    assert bt.last_fpids[5] == (fbn << 8) + 5
+    assert cur == k - len(miss) + 1
+    bt.close()
