@@ -115,6 +115,10 @@ struct pquic_fec_batcher {
     job_t *todo_head, *todo_tail, *staged_head, *staged_tail, *post_head, *post_tail, *done_head, *done_tail;
     int inflight, stop, stagers_done;
     uint32_t pf;                   /* completion prefetch distance in blocks (prefetch_syms; 0: off) */
+    int done_ready;                /* atomic: the next job in flush order is finished (set under mu), so a
+                                    * poll with nothing to complete takes no lock */
+    uint64_t next_due;             /* caller thread: the oldest first-submission time of the open jobs
+                                    * (UINT64_MAX: none), so a poll scans them only when one may be overdue */
     int last_slot;                 /* open[] slot of the last submission (caller thread) */
     job_t *completing;             /* finished job whose completions a bounded poll left part-done */
     uint32_t completing_i;         /* its next entry */
@@ -577,12 +581,13 @@ static void push(job_t **head, job_t **tail, job_t *j) {
 static void push_done(pquic_fec_batcher_t *b, job_t *j) {
     if (!b->done_tail || b->done_tail->seq < j->seq) {
         push(&b->done_head, &b->done_tail, j);
-        return;
+    } else {
+        job_t **pp = &b->done_head;
+        while (*pp && (*pp)->seq < j->seq) pp = &(*pp)->next;
+        j->next = *pp;
+        *pp = j;
     }
-    job_t **pp = &b->done_head;
-    while (*pp && (*pp)->seq < j->seq) pp = &(*pp)->next;
-    j->next = *pp;
-    *pp = j;
+    __atomic_store_n(&b->done_ready, b->done_head->seq == b->collect_seq, __ATOMIC_RELEASE);
 }
 
 /* Stager threads split every job into work items of STAGE_CHUNK blocks, so several threads copy
@@ -713,6 +718,7 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     if (!b) return NULL;
     b->cfg = *cfg;
     b->stride = fec_pad4(cfg->max_symbol);
+    b->next_due = UINT64_MAX;
     const char *pfs = getenv("PQUIC_FEC_BATCH_PREFETCH");  /* read once per batcher, like the thread counts */
     b->pf = pfs && atoi(pfs) >= 0 ? (uint32_t)atoi(pfs) : 8;
     if (b->pf > 64) b->pf = 64;
@@ -778,6 +784,11 @@ static void flush_job(pquic_fec_batcher_t *b, int slot, uint64_t *counter) {
     job_t *j = b->open[slot];
     b->open[slot] = NULL;
     if (!j) return;
+    if (j->n && j->t_first == b->next_due) {  /* the oldest open job leaves: the next oldest */
+        b->next_due = UINT64_MAX;
+        for (int s = 0; s < MAX_OPEN; s++)
+            if (b->open[s] && b->open[s]->n && b->open[s]->t_first < b->next_due) b->next_due = b->open[s]->t_first;
+    }
     if (!j->n) {  /* nothing queued: back to the free list */
         j->next = b->free_jobs;
         b->free_jobs = j;
@@ -866,7 +877,10 @@ static int submit(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_fec_block_t
         j->ent[i].nalloc = (int16_t)fec_generate_alloc(cnx, fb, maxl, j->reps + (size_t)i * r);
     else if (j->gather)  /* the recovered symbols, so the kernel writes them where they will stay */
         fec_recover_alloc(cnx, fb, maxl, j->pre + (size_t)i * k);
-    if (!i) j->t_first = now_us;
+    if (!i) {
+        j->t_first = now_us;
+        if (now_us < b->next_due) b->next_due = now_us;
+    }
     j->n = i + 1;
     b->stats.submitted++;
     if (j->n == j->cap) flush_job(b, slot, &b->stats.flushed_full);
@@ -937,7 +951,7 @@ static void prefetch_syms(const job_t *j, uint32_t i, int data) {
  * operations, then done().  A job left part-done continues at the next call. */
 static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     job_t *j = b->completing;
-    if (!j || __atomic_load_n(&b->done_head, __ATOMIC_RELAXED)) {  /* and the finished jobs behind it */
+    if (__atomic_load_n(&b->done_ready, __ATOMIC_ACQUIRE)) {  /* the finished jobs that come next */
         pthread_mutex_lock(&b->mu);
         /* the finished jobs that continue the flush order; a later job waits for the ones before it */
         job_t *more = NULL, **tail = &more;
@@ -950,6 +964,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
             b->collect_seq++;
         }
         if (!b->done_head) b->done_tail = NULL;
+        __atomic_store_n(&b->done_ready, b->done_head && b->done_head->seq == b->collect_seq, __ATOMIC_RELAXED);
         pthread_mutex_unlock(&b->mu);
         if (!j) {
             j = more;
@@ -1027,10 +1042,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     }
     b->completing = j;
     b->completing_i = i;
-    const uint64_t dt = mono_us() - t0;
-    pthread_mutex_lock(&b->mu);
-    b->stats.complete_us += dt;
-    pthread_mutex_unlock(&b->mu);
+    b->stats.complete_us += mono_us() - t0;  /* caller-thread field: only the caller reads it */
     return n;
 }
 
@@ -1038,6 +1050,7 @@ int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us) {
     if (!b) return 0;
     for (int s = 0; s < MAX_OPEN; s++) {
         job_t *j = b->open[s];
+        if (b->next_due == UINT64_MAX || now_us - b->next_due < b->cfg.max_delay_us) break;  /* none overdue */
         if (j && j->n && now_us - j->t_first >= b->cfg.max_delay_us) flush_job(b, s, &b->stats.flushed_deadline);
     }
     return collect(b, b->cfg.poll_blocks);

@@ -34,9 +34,18 @@ def built():
     return os.path.join(SAN, "_build")
 
 
+def _sanitizer_logs(tmp_path):
+    """the reports the sanitizer runtimes wrote to their log_path files (one per process)"""
+    return "".join(p.read_text(errors="replace") for p in sorted(tmp_path.glob("san.*")))
+
+
 def _run_suites(lib, preload, extra_env, tmp_path, deselect=()):
     env = dict(os.environ)
     env.update(extra_env)
+    # reports also go to files: a runtime that ends the process can lose what it wrote to a pipe
+    for var in ("ASAN_OPTIONS", "UBSAN_OPTIONS", "TSAN_OPTIONS"):
+        if var in env:
+            env[var] += f":log_path={tmp_path / 'san'}"
     env["LD_PRELOAD"] = preload
     env["PQUIC_TEST_MINIHOST"] = lib
     env["PYTHONMALLOC"] = "malloc"
@@ -45,7 +54,7 @@ def _run_suites(lib, preload, extra_env, tmp_path, deselect=()):
     for d in deselect:
         cmd += ["--deselect", d]
     r = subprocess.run(cmd + SUITES, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1800)
-    out = r.stdout + r.stderr
+    out = r.stdout + r.stderr + _sanitizer_logs(tmp_path)
     (tmp_path / "log.txt").write_text(out)
     assert r.returncode == 0, out[-6000:]
     found = [m for m in REPORTS if m in out]

@@ -10,6 +10,7 @@
 #define _GNU_SOURCE  /* MAP_ANONYMOUS */
 #define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -21,6 +22,7 @@
 #include <sys/syscall.h>
 #include <ucontext.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include "fecgpu.h"
 #include "pquic_fec_batch.h"
@@ -52,6 +54,9 @@ typedef struct bl_arena {
 } bl_arena_t;
 /* per sender thread (bl_run_senders runs several, each a PQUIC process's single thread with its own heap) */
 static __thread bl_arena_t g_thread_arena;
+/* out of line: a thread-local in a dlopen()ed library costs a __tls_get_addr call, which the
+ * per-connection allocations (the bench legs) then never make */
+__attribute__((noinline)) static bl_arena_t *thread_arena(void) { return &g_thread_arena; }
 static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
     if (n > SLOT - 16) {
         uint8_t *p = malloc((size_t)n + 16);
@@ -59,7 +64,8 @@ static void *bl_malloc(picoquic_cnx_t *c, unsigned int n) {
         p[0] = 1;
         return p + 16;
     }
-    bl_arena_t *a = c && c->arena ? c->arena : &g_thread_arena;
+    bl_arena_t *a = c ? c->arena : NULL;
+    if (!a) a = thread_arena();
     slot_u *s = a->free_slots;
     if (s) {
         a->free_slots = s->next;
@@ -79,7 +85,8 @@ static void bl_free(picoquic_cnx_t *c, void *p) {
     if (!p) return;
     uint8_t *b = (uint8_t *)p - 16;
     if (b[0]) { free(b); return; }
-    bl_arena_t *a = c && c->arena ? c->arena : &g_thread_arena;
+    bl_arena_t *a = c ? c->arena : NULL;
+    if (!a) a = thread_arena();
     slot_u *s = (slot_u *)b;
     s->next = a->free_slots;
     a->free_slots = s;
@@ -122,6 +129,41 @@ static uint64_t now_us(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+/* bl_run's per-block stamps (submission, completion, the clock handed to the batcher) read the TSC when
+ * it is invariant and cheaper than the vDSO clock (on the GPU boxes clock_gettime took about a fifth of
+ * the sender thread's time), calibrated against CLOCK_MONOTONIC once; wall times stay on now_us(). */
+static double g_tsc_us;  /* microseconds per tick; 0: stamps use now_us() */
+static uint64_t g_tsc_base, g_tsc_base_us;
+static pthread_once_t g_tsc_once = PTHREAD_ONCE_INIT;
+static void tsc_init(void) {
+    FILE *f = fopen("/proc/cpuinfo", "r");
+    char line[8192];
+    int inv = 0;
+    while (f && fgets(line, sizeof line, f))
+        if (!strncmp(line, "flags", 5)) {
+            inv = strstr(line, " constant_tsc") && strstr(line, " nonstop_tsc");
+            break;
+        }
+    if (f) fclose(f);
+    if (!inv) return;
+    volatile uint64_t sink = 0;
+    const uint64_t c0 = __rdtsc(), u0 = now_us();
+    for (int i = 0; i < 20000; i++) sink += now_us();
+    const uint64_t c1 = __rdtsc();
+    for (int i = 0; i < 20000; i++) sink += __rdtsc();
+    const uint64_t c2 = __rdtsc();
+    if (c2 - c1 >= c1 - c0) return;  /* the TSC is not the cheaper clock here */
+    while (now_us() - u0 < 30000) {}  /* 30 ms or more of calibration */
+    const uint64_t c3 = __rdtsc(), u3 = now_us();
+    g_tsc_base = c3;
+    g_tsc_base_us = u3;
+    g_tsc_us = (double)(u3 - u0) / (double)(c3 - c0);
+}
+static inline uint64_t stamp_us(void) {
+    if (g_tsc_us <= 0) return now_us();
+    return g_tsc_base_us + (uint64_t)((double)(int64_t)(__rdtsc() - g_tsc_base) * g_tsc_us);
 }
 
 /* PC sampler for the sender thread's measured pass (bl_set_sampling; tools/sender_phase_probe.py
@@ -176,15 +218,27 @@ static void sampling_stop(void) {
     signal(SIGPROF, SIG_IGN);
 }
 
+/* a sender's completion tallies; the callbacks reach them through their slot (no thread-local access
+ * per block) */
+typedef struct {
+    uint64_t *lat;
+    long nlat, recovered;
+    const pquic_source_symbol_t *recv_lo, *recv_hi;  /* the received symbols' descriptors (receiver) */
+} bl_tally_t;
+static __thread bl_tally_t g_tally;
+#define g_lat (g_tally.lat)
+#define g_nlat (g_tally.nlat)
+#define g_recovered (g_tally.recovered)
+#define g_recv_lo (g_tally.recv_lo)
+#define g_recv_hi (g_tally.recv_hi)
+
 typedef struct {
     pquic_fec_block_t fb;
     uint64_t t_submit;
     picoquic_cnx_t *cnx;
+    bl_tally_t *tally;
     int busy;
 } slot_t;
-
-static __thread uint64_t *g_lat;
-static __thread long g_nlat;
 static unsigned g_poll_blocks;  /* pquic_fec_batch_cfg_t.poll_blocks of the next runs (0: all) */
 static int g_hugepages;         /* the next runs' arena on transparent huge pages */
 static int g_detail;            /* time every submission (one more clock read per block) */
@@ -217,8 +271,9 @@ static __thread double g_phases[6];  /* the last bl_run's measured pass: engine,
 
 static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     slot_t *s = user;
+    bl_tally_t *t = s->tally;
     (void)ret;
-    g_lat[g_nlat++] = now_us() - s->t_submit;
+    t->lat[t->nlat++] = stamp_us() - s->t_submit;
     for (int i = 0; i < fb->total_repair_symbols; i++) {
         pquic_repair_symbol_t *rs = fb->repair_symbols[i];
         if (rs) { bl_free(s->cnx, rs->data); bl_free(s->cnx, rs); fb->repair_symbols[i] = NULL; }
@@ -227,16 +282,15 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
 }
 
 /* receiver: the framework decodes the recovered symbols' frames and frees them (fec_protoops.h:252-275) */
-static __thread long g_recovered;
-static __thread const pquic_source_symbol_t *g_recv_lo, *g_recv_hi;  /* the received symbols' descriptors */
 static void on_recovered(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     slot_t *s = user;
+    bl_tally_t *t = s->tally;
     (void)ret;
-    g_lat[g_nlat++] = now_us() - s->t_submit;
+    t->lat[t->nlat++] = stamp_us() - s->t_submit;
     for (int j = 0; j < fb->total_source_symbols; j++) {
         pquic_source_symbol_t *ss = fb->source_symbols[j];
-        if (ss && (ss < g_recv_lo || ss >= g_recv_hi)) {  /* inserted by the recover (allocated by the adapter) */
-            g_recovered++;
+        if (ss && (ss < t->recv_lo || ss >= t->recv_hi)) {  /* inserted by the recover (allocated by the adapter) */
+            t->recovered++;
             bl_free(s->cnx, ss->data);
             bl_free(s->cnx, ss);
         }
@@ -430,6 +484,8 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     g_recv_lo = ss;
     g_recv_hi = ss + (size_t)nslots * k;
     if (!ss || !g_lat || (recover_e && !rsy)) return sender_fail(waits);
+    bl_tally_t *const tally = &g_tally;
+    pthread_once(&g_tsc_once, tsc_init);
     const double bytes_per_block = (double)k * L;
     long next_slot = 0;
     /* pass 0 warms up (pinned queue buffers allocated, device buffers grown), pass 1 is measured */
@@ -448,17 +504,18 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
         if (g_sync) pthread_barrier_wait(g_sync), waits++;  /* bl_run_senders: every sender starts each pass together */
         if (pass) sampling_start();
         t0 = now_us();
+        const uint64_t t0s = stamp_us();
         t_wait = t_submit = 0;
         for (long blk = 0; blk < nb; blk++) {
             if (offered_gib_s > 0) {  /* pace: block blk is due at t0 + blk * bytes / rate */
-                const uint64_t due = t0 + (uint64_t)(blk * bytes_per_block / (offered_gib_s * 1073741824.0) * 1e6);
-                while (now_us() < due) pquic_fec_batch_poll(b, now_us());
+                const uint64_t due = t0s + (uint64_t)(blk * bytes_per_block / (offered_gib_s * 1073741824.0) * 1e6);
+                while (stamp_us() < due) pquic_fec_batch_poll(b, stamp_us());
             }
             slot_t *s = &slots[next_slot];
             if (s->busy) {
-                const uint64_t w0 = now_us();
-                while (s->busy) pquic_fec_batch_poll(b, now_us());  /* back-pressure: slot still in flight */
-                t_wait += now_us() - w0;
+                const uint64_t w0 = stamp_us();
+                while (s->busy) pquic_fec_batch_poll(b, stamp_us());  /* back-pressure: slot still in flight */
+                t_wait += stamp_us() - w0;
             }
             const long si = next_slot;
             next_slot = (next_slot + 1) % nslots;
@@ -469,6 +526,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
             const uint32_t fbn = recover_e ? (uint32_t)(c * ppc + q) & 0xffffffu : (uint32_t)(blk / nconn) & 0xffffffu;
             s->fb.fec_block_number = fbn;
             s->cnx = &cnx[c];
+            s->tally = tally;
             const int lost0 = recover_e ? (int)(blk % (k - recover_e + 1)) : k;  /* sources lost0 .. +e-1 */
             for (int j = 0; j < k; j++) {
                 if (j >= lost0 && j < lost0 + recover_e) continue;
@@ -494,12 +552,12 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
                 s->fb.current_repair_symbols = (uint8_t)r;
             }
             s->busy = 1;
-            s->t_submit = now_us();
+            s->t_submit = stamp_us();
             const int rc = recover_e ? pquic_fec_batch_recover(b, &cnx[c], &s->fb, 0, s->t_submit, on_recovered, s)
                                      : pquic_fec_batch_generate(b, &cnx[c], &s->fb, 0, s->t_submit, on_done, s);
             if (rc) return sender_fail(waits);
-            if (g_detail) t_submit += now_us() - s->t_submit;
-            if ((blk & 15) == 0) pquic_fec_batch_poll(b, now_us());
+            if (g_detail) t_submit += stamp_us() - s->t_submit;
+            if ((blk & 15) == 0) pquic_fec_batch_poll(b, stamp_us());
         }
     }
     pquic_fec_batch_drain(b);
@@ -579,6 +637,7 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
         cnx[c].id = c;
         sent[c] = k > step ? k - step : 0;  /* symbols already sent: the first window then ends at k */
     }
+    pthread_once(&g_tsc_once, tsc_init);
     long next_slot = 0;
     uint64_t t0 = 0;
     pquic_fec_batch_stats_t st0;
@@ -593,7 +652,7 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
         t0 = now_us();
         for (long w = 0; w < nw; w++) {
             slot_t *s = &slots[next_slot];
-            while (s->busy) pquic_fec_batch_poll(b, now_us());
+            while (s->busy) pquic_fec_batch_poll(b, stamp_us());
             next_slot = (next_slot + 1) % nslots;
             const int c = (int)(w % nconn);
             pquic_source_symbol_t *rc = rings + (size_t)c * ring;
@@ -610,11 +669,12 @@ int bl_run_window(int device, int k, int r, int L, int step, int nconn, long nwi
             s->fb.total_repair_symbols = (uint8_t)r;
             s->busy = 1;
             s->cnx = NULL;  /* the repairs come from the thread arena */
-            s->t_submit = now_us();
+            s->tally = &g_tally;
+            s->t_submit = stamp_us();
             const int rc2 = window_api ? pquic_fec_batch_generate_window(b, &cnx[c], &s->fb, s->t_submit, on_done, s)
                                        : pquic_fec_batch_generate(b, &cnx[c], &s->fb, 0, s->t_submit, on_done, s);
             if (rc2) return -1;
-            if ((w & 15) == 0) pquic_fec_batch_poll(b, now_us());
+            if ((w & 15) == 0) pquic_fec_batch_poll(b, stamp_us());
         }
     }
     pquic_fec_batch_drain(b);
