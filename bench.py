@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-blocks", type=int, default=0,
                    help="CPU-baseline sample size in blocks (0: about 300 MiB of source payload)")
+    p.add_argument("--host-legs", action="store_true", help=argparse.SUPPRESS)  # the child of host_legs_child()
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / rendezvous check without a GPU: ranks time an empty step on gloo; "
                         "value is 0 and the line says dry_run (tests only)")
@@ -699,8 +700,34 @@ def dry_run_rank(args, world, rank, local, cpu):
         dist.destroy_process_group()
 
 
+def host_legs_child(args, dev_index):
+    """The batching-adapter and synchronous-hook legs in a child process of their own: a PQUIC process
+    holds the FEC library, not torch and the bench's 50 GB of device tensors, and in the bench's own process
+    one sender measured 20 % slower than in a fresh one on the same box (profiles/r05_batch_context_probe.log).
+    The child is a plain `python bench.py --host-legs` (no torch import); its JSON line is merged here."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--host-legs", "--k", str(args.k), "--r", str(args.r),
+           "--symbol", str(args.symbol), "--erasures", str(args.erasures)]
+    env = dict(os.environ)
+    env["PQUIC_BENCH_HOST_DEVICE"] = str(dev_index)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200, env=env)
+    except subprocess.TimeoutExpired:
+        return {"host_legs": {"error": "timeout"}}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode or not lines:
+        return {"host_legs": {"error": r.returncode, "stderr": r.stderr[-2000:]}}
+    return json.loads(lines[-1])
+
+
 def main():
     args = parse()
+    if args.host_legs:  # child of host_legs_child: no torch, the engine library and the load generator only
+        dev_index = int(os.environ.get("PQUIC_BENCH_HOST_DEVICE", "0"))
+        legs = batching_legs(dev_index, args)
+        legs.update(hook_latency_legs(dev_index))
+        print(json.dumps(legs), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))  # parent: starts one child process per GPU, never touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -877,10 +904,6 @@ def main():
     if e:
         del work, ws, rec_rows
     default = args.config == "k16" and (k, r, e, L) == (16, 4, 4, 1200)
-    if default and not args.no_legs and not args.no_pcie and world == 1:
-        legs.update(pcie_legs(torch, args, dev))
-        legs.update(batching_legs(dev.index or 0, args))
-        legs.update(hook_latency_legs(dev.index or 0))
     if default and not args.no_legs and world == 1:
         # §8f row 2: the repair symbols of the whole batch as FEC frames (header + payload) on the device
         fstride = (14 + L + 15) // 16 * 16
@@ -950,6 +973,12 @@ def main():
         legs["rlc_k64_r16_L9000"] = rlc_leg(torch, eng, dev, 64, 16, 9000, 1 << 16, 16)
         # configs[0]'s XOR scheme (k = 4, r = 1) at GPU scale: encode + single-erasure recover
         legs["xor_k4_r1"] = xor_leg(torch, eng, dev, 4, L, 1 << 22)
+    if default and not args.no_legs and not args.no_pcie and world == 1:
+        # the host-path legs last, once the device legs have freed their tensors (they use buffers of their
+        # own: page-locked rows, registered arenas); the batching and hook legs in a process of their own
+        torch.cuda.empty_cache()
+        legs.update(pcie_legs(torch, args, dev))
+        legs.update(host_legs_child(args, dev.index or 0))
 
     if rank == 0:
         if not e or enc_ms >= apply_ms:

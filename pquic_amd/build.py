@@ -65,7 +65,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     inc = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     for src in c:  # host C: the protoop adapters stay C (reference language)
         obj = os.path.join(odir, os.path.basename(src) + ".o")
-        _run(["gcc", "-std=c11", "-O2", "-fPIC", "-Wall", "-Wextra", "-c", src, "-o", obj] + inc)
+        _run(["gcc", "-std=c11", "-O2", "-g", "-fPIC", "-Wall", "-Wextra", "-c", src, "-o", obj] + inc)
         objs.append(obj)
     for src in hip:
         obj = os.path.join(odir, os.path.basename(src) + ".o")

@@ -914,7 +914,20 @@ int pquic_fec_batch_recover(pquic_fec_batcher_t *b, picoquic_cnx_t *cnx, pquic_f
  * wrote their data over PCIe, so those lines are in no CPU cache.  Entry i + 2P's symbol structs and
  * entry i + P's data lines are prefetched while entry i completes (P = b->pf, 0: off), so the misses
  * overlap instead of stalling the caller one block at a time. */
+/* the lines of [p, p + n) */
+static void prefetch_range(const void *p, size_t n) {
+    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)63, e = (uintptr_t)p + n;
+    for (uintptr_t x = a; x < e; x += 64) __builtin_prefetch((const void *)x, 1);
+}
+
 static void prefetch_syms(const job_t *j, uint32_t i, int data) {
+    if (data) {  /* the block's symbol pointers the completion writes (and the framework then reads) */
+        pquic_fec_block_t *fb = j->ent[i].fb;
+        if (GENERATES(j->op))
+            prefetch_range(&fb->repair_symbols[0], sizeof fb->repair_symbols[0] * (j->ent[i].nalloc > 0 ? j->ent[i].nalloc : 1));
+        else
+            prefetch_range(&fb->source_symbols[0], sizeof fb->source_symbols[0] * j->k);
+    }
     if (GENERATES(j->op)) {
         const entry_t *e = &j->ent[i];
         pquic_repair_symbol_t *const *reps = j->reps + (size_t)i * j->r;
@@ -927,12 +940,13 @@ static void prefetch_syms(const job_t *j, uint32_t i, int data) {
                 __builtin_prefetch(d, 1);
             }
         }
-    } else if (j->gather) {
+    } else {
         if (data) {  /* the status and masks the kernel wrote, the stagers' copy masks */
             __builtin_prefetch(j->st + i, 0);
             __builtin_prefetch(j->rec + 2 * (size_t)i, 0);
-            __builtin_prefetch(j->cpm + 2 * (size_t)i, 0);
+            if (j->gather) __builtin_prefetch(j->cpm + 2 * (size_t)i, 0);
         }
+        if (!j->gather) return;
         pquic_source_symbol_t *const *pre = j->pre + (size_t)i * j->k;
         for (uint32_t x = 0; x < j->k; x++) {
             if (!pre[x]) continue;
@@ -977,6 +991,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     if (!j) return 0;
     const uint64_t t0 = mono_us();
     uint32_t i = b->completing_i;
+    uint64_t nrec = 0;  /* recovered symbols, added to the protoop counters once per call */
     int n = 0;
     while (j) {
         const uint32_t S = j->stride;
@@ -1018,10 +1033,11 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
             } else if (pre) {
                 /* rows the kernel wrote into the staging area (no in-place row for them) are copied */
                 ret = fec_recover_finish_pre(e->cnx, e->fb, j->st[i], j->rec + 2 * (size_t)i, pre,
-                                             j->cpm + 2 * (size_t)i, j->src + (size_t)i * j->k * S, S, e->maxl);
+                                             j->cpm + 2 * (size_t)i, j->src + (size_t)i * j->k * S, S, e->maxl,
+                                             &nrec);
             } else {
                 ret = fec_recover_finish(e->cnx, e->fb, j->xor_scheme, j->st[i], j->rec + 2 * (size_t)i,
-                                         j->src + (size_t)i * j->k * S, S, e->maxl);
+                                         j->src + (size_t)i * j->k * S, S, e->maxl, &nrec);
             }
             e->done(e->user, e->fb, ret);
             n++;
@@ -1042,6 +1058,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     }
     b->completing = j;
     b->completing_i = i;
+    if (nrec) FEC_STAT_ADD(recovered_symbols, nrec);
     b->stats.complete_us += mono_us() - t0;  /* caller-thread field: only the caller reads it */
     return n;
 }

@@ -146,11 +146,13 @@ void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t max
 }
 
 protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme, uint8_t status,
-                                 const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl) {
+                                 const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl,
+                                 uint64_t *nrec_acc) {
     const int k = fb->total_source_symbols;
     if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
     if (!xor_scheme) {
         const uint32_t fbn = fb->fec_block_number & 0xffffffu;
+        uint64_t nrec = 0;
         for (int j = 0; j < k && status == FECGPU_BLOCK_RECOVERED; j++) {  /* :218-236 */
             if (!((rec[j >> 6] >> (j & 63)) & 1)) continue;
             pquic_source_symbol_t *ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl);
@@ -158,8 +160,10 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
             fb->source_symbols[j] = ss;
             fb->current_source_symbols++;
-            FEC_STAT_ADD(recovered_symbols, 1);
+            nrec++;
         }
+        if (nrec_acc) *nrec_acc += nrec;
+        else if (nrec) FEC_STAT_ADD(recovered_symbols, nrec);
         return 0;
     }
     protoop_arg_t ret = 1;
@@ -169,7 +173,8 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
         if (!ss) return PQUIC_ERROR_MEMORY;
         memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
         fb->source_symbols[j] = ss;  /* current_source_symbols is NOT incremented (:72) */
-        FEC_STAT_ADD(recovered_symbols, 1);
+        if (nrec_acc) ++*nrec_acc;
+        else FEC_STAT_ADD(recovered_symbols, 1);
         ret = 0;
     }
     return ret;
@@ -187,8 +192,8 @@ int fec_recover_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t
 }
 
 protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, uint8_t status, const uint64_t rec[2],
-                                     pquic_source_symbol_t **pre, const uint64_t copy[2], const uint8_t *src_rows,
-                                     uint32_t stride, uint16_t maxl) {
+                                     pquic_source_symbol_t *const *pre, const uint64_t copy[2], const uint8_t *src_rows,
+                                     uint32_t stride, uint16_t maxl, uint64_t *nrec_acc) {
     const int k = fb->total_source_symbols;
     const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
@@ -200,14 +205,13 @@ protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
         if (!got && pre[j]) {
             g_fec_api.my_free(cnx, pre[j]->data);
             g_fec_api.my_free(cnx, pre[j]);
-            pre[j] = NULL;
         }
     }
+    uint64_t nrec = 0;
     for (int j = 0; j < k; j++) {  /* :218-236, in source order as the reference inserts them */
         const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
+        if (!got) continue;  /* (freed above) */
         pquic_source_symbol_t *ss = pre[j];
-        pre[j] = NULL;
-        if (!got) continue;
         if (!ss) {
             if (!(ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) continue;
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
@@ -216,7 +220,8 @@ protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
         }
         fb->source_symbols[j] = ss;
         fb->current_source_symbols++;
-        FEC_STAT_ADD(recovered_symbols, 1);
+        nrec++;
     }
+    *nrec_acc += nrec;
     return 0;
 }

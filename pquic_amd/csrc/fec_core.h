@@ -66,9 +66,12 @@ void fec_recover_stage(const pquic_fec_block_t *fb, int xor_scheme, uint16_t max
 /* Recover, after the engine: inserts every source the engine marked recovered (maxl bytes
  * from src_rows) with the reference's FPID and counter behaviour (RLC increments
  * current_source_symbols, :230; XOR does not, xor_fec_scheme.c:72).  Returns the
- * operation's value (RLC 0; XOR 0 after an insertion, else 1). */
+ * operation's value (RLC 0; XOR 0 after an insertion, else 1).  The recovered-symbol counter is added to
+ * atomically, or -- nrec_acc non-NULL, the batcher's completions -- into *nrec_acc, which the caller adds
+ * once per poll (a locked add per block waited for the completion's outstanding stores). */
 protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int xor_scheme, uint8_t status,
-                                 const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl);
+                                 const uint64_t rec[2], const uint8_t *src_rows, uint32_t stride, uint16_t maxl,
+                                 uint64_t *nrec_acc);
 
 /* RLC recover with the recovered symbols allocated before the engine (the batching adapter's gather
  * path, batch.c): fec_recover_alloc allocates one source symbol of maxl bytes, FPID (fbn << 8) + j, for
@@ -78,11 +81,13 @@ protoop_arg_t fec_recover_finish(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, int
  * src_rows row j when bit j of `copy` is set: the engine wrote that row into the staging rows), allocates
  * anew for a recovered source without a pre-allocated symbol (skipped when that fails, :222-226), and
  * frees the pre-allocated symbols of sources left unrecovered -- the block ends as fec_recover_finish
- * leaves it.  Returns 0 (rlc_fec_scheme_gf256.c:250). */
+ * leaves it.  pre[] is only read (the caller drops it: every pre[j] is inserted or freed; not writing it
+ * back keeps the array's lines shared with the stager threads that read them).  Returns 0
+ * (rlc_fec_scheme_gf256.c:250).  Recovered symbols are counted into *nrec_acc (see fec_recover_finish). */
 int fec_recover_alloc(picoquic_cnx_t *cnx, const pquic_fec_block_t *fb, uint16_t maxl, pquic_source_symbol_t **pre);
 protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb, uint8_t status, const uint64_t rec[2],
-                                     pquic_source_symbol_t **pre, const uint64_t copy[2], const uint8_t *src_rows,
-                                     uint32_t stride, uint16_t maxl);
+                                     pquic_source_symbol_t *const *pre, const uint64_t copy[2], const uint8_t *src_rows,
+                                     uint32_t stride, uint16_t maxl, uint64_t *nrec_acc);
 
 #pragma GCC visibility pop
 

@@ -251,7 +251,7 @@ static protoop_arg_t recover(picoquic_cnx_t *cnx, int xor_scheme) {
         FEC_STAT_ADD(errors, 1);
         ret = PQUIC_FEC_ERR_UNBOUND;
     } else {
-        ret = fec_recover_finish(cnx, fb, xor_scheme, g_aux->st, g_aux->rec, g_src, L, maxl);
+        ret = fec_recover_finish(cnx, fb, xor_scheme, g_aux->st, g_aux->rec, g_src, L, maxl, NULL);
     }
     pthread_mutex_unlock(&g_mu);
     return ret;

@@ -506,6 +506,8 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
         t0 = now_us();
         const uint64_t t0s = stamp_us();
         t_wait = t_submit = 0;
+        int cur_c = 0, cur_lost = 0;
+        long cur_q = 0, cur_round = 0;
         for (long blk = 0; blk < nb; blk++) {
             if (offered_gib_s > 0) {  /* pace: block blk is due at t0 + blk * bytes / rate */
                 const uint64_t due = t0s + (uint64_t)(blk * bytes_per_block / (offered_gib_s * 1073741824.0) * 1e6);
@@ -518,16 +520,24 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
                 t_wait += stamp_us() - w0;
             }
             const long si = next_slot;
-            next_slot = (next_slot + 1) % nslots;
-            const int c = (int)(blk % nconn);
-            const long q = (blk / nconn) % ppc;  /* the connection's pool block */
+            if (++next_slot == nslots) next_slot = 0;
+            /* block blk: connection c = blk % nconn, round blk / nconn, pool block q = round % ppc, kept as
+             * counters (no divisions per block) */
+            const int c = cur_c;
+            const long q = cur_q;
             const uint8_t *pb = pool[c] + (size_t)q * k * L;
             memset(&s->fb, 0, sizeof s->fb);
-            const uint32_t fbn = recover_e ? (uint32_t)(c * ppc + q) & 0xffffffu : (uint32_t)(blk / nconn) & 0xffffffu;
+            const uint32_t fbn = recover_e ? (uint32_t)(c * ppc + q) & 0xffffffu : (uint32_t)cur_round & 0xffffffu;
+            if (++cur_c == nconn) {
+                cur_c = 0;
+                cur_round++;
+                if (++cur_q == ppc) cur_q = 0;
+            }
             s->fb.fec_block_number = fbn;
             s->cnx = &cnx[c];
             s->tally = tally;
-            const int lost0 = recover_e ? (int)(blk % (k - recover_e + 1)) : k;  /* sources lost0 .. +e-1 */
+            const int lost0 = recover_e ? cur_lost : k;  /* sources lost0 .. +e-1, lost0 = blk % (k - e + 1) */
+            if (recover_e && ++cur_lost == k - recover_e + 1) cur_lost = 0;
             for (int j = 0; j < k; j++) {
                 if (j >= lost0 && j < lost0 + recover_e) continue;
                 pquic_source_symbol_t *sym = &ss[si * k + j];
