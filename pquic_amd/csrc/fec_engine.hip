@@ -100,8 +100,10 @@ static void knobs_default() {
   // context's streams, and a slice held back at most yield_gate_us while a hook request is pending (0:
   // not held).  Beside back-to-back 4096-block zero-copy encodes (profiles/r05_pacer_sweep.log): 2560 KiB,
   // 16, 2 streams -> hooks p99 174 / 184 us (generate / recover; unsliced 1473 / 1486) for bulk calls
-  // 9 % longer (1.725 against 1.582 ms); 2048 KiB -> p99 142-152 us, +12 %; 3072 KiB -> 207-218 us, +7 %
-  g_knob[K_YIELD_SLICE_KB] = 2560;
+  // 9 % longer (1.725 against 1.582 ms); 2048 KiB -> p99 142-152 us, +12 %; 3072 KiB -> 207-218 us, +7 %.
+  // 2304 KiB (profiles/r05_pacer_sweep2.log, one box, twice): p99 158 / 170 us against 2560's 175 / 187 for
+  // bulk calls 0.9 % longer -- the margin under 200 us the bench's runs needed (one read recover p99 202)
+  g_knob[K_YIELD_SLICE_KB] = 2304;
   g_knob[K_YIELD_DEPTH] = 16;
   g_knob[K_YIELD_GATE_US] = 0;
   g_knob[K_YIELD_STREAMS] = 2;

@@ -183,7 +183,7 @@ static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 // defaults and their measurement in fec_engine.hip knobs_default).  Optionally (yield_gate_us) no
 // slice starts while a hook request is pending.  Without hooks nothing changes (one launch).  The
 // hooks still wait for the slices running when they arrive; the slice size trades their p99 against
-// the bulk call's time (about 60-80 us of PCIe transfer per 2.5 MiB slice).
+// the bulk call's time (about 55-80 us of PCIe transfer per 2.25-2.5 MiB slice).
 int fecgpu_svc_hooks_pending(void);                                  // fec_engine.hip (library-internal)
 uint64_t fecgpu_svc_last_request_us(void);                           // fec_engine.hip (library-internal)
 void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us, int *streams, int *always);  // fec_engine.hip

@@ -48,15 +48,18 @@ if pacer:
             eng.set_knob(n, v)
     # the bulk job alone, slices forced (what slicing costs without any hook)
     lib.bl_bulk_rate.argtypes = [C.c_int, C.c_int, C.c_int, D]
-    for kb, streams, depth in ((0, 1, 4), (2048, 2, 16), (2560, 2, 16), (3072, 2, 16), (4096, 2, 16)):
+    for kb, streams, depth in (() if os.environ.get("PACER_SETS") else
+                               ((0, 1, 4), (2048, 2, 16), (2560, 2, 16), (3072, 2, 16), (4096, 2, 16))):
         knobs(kb, depth, 0, streams, 1)
         out = (C.c_double * 2)()
         rc |= lib.bl_bulk_rate(0, 4096, 200, out)
         print(f"bulk alone, slices {kb:5d} KiB on {streams} stream(s), depth {depth}: {out[0]:.3f} ms per 4096-block call "
               f"({out[1]:.1f} GiB/s of sources)", flush=True)
-    for kb, depth, gate, streams in ((0, 4, 0, 1), (2048, 16, 0, 2), (2560, 16, 0, 2), (3072, 16, 0, 2),
-                                     (2048, 12, 0, 2), (4096, 16, 0, 2), (2048, 16, 0, 2), (3072, 16, 0, 2),
-                                     (0, 4, 0, 1)):
+    sets = ((0, 4, 0, 1), (2048, 16, 0, 2), (2560, 16, 0, 2), (3072, 16, 0, 2), (2048, 12, 0, 2), (4096, 16, 0, 2),
+            (2048, 16, 0, 2), (3072, 16, 0, 2), (0, 4, 0, 1))
+    if os.environ.get("PACER_SETS"):  # e.g. "2560:16,2304:16,2560:12" (2 streams, no gate)
+        sets = tuple((int(a), int(b), 0, 2) for a, b in (x.split(":") for x in os.environ["PACER_SETS"].split(",")))
+    for kb, depth, gate, streams in sets:
         knobs(kb, depth, gate, streams, 0)
         s0 = eng.stats()
         lo = (C.c_double * 11)()
