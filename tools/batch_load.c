@@ -163,7 +163,8 @@ static void tsc_init(void) {
 }
 static inline uint64_t stamp_us(void) {
     if (g_tsc_us <= 0) return now_us();
-    return g_tsc_base_us + (uint64_t)((double)(int64_t)(__rdtsc() - g_tsc_base) * g_tsc_us);
+    /* signed: a core whose TSC reads a little behind the calibrating one gives a small negative offset */
+    return (uint64_t)((int64_t)g_tsc_base_us + (int64_t)((double)(int64_t)(__rdtsc() - g_tsc_base) * g_tsc_us));
 }
 
 /* PC sampler for the sender thread's measured pass (bl_set_sampling; tools/sender_phase_probe.py
