@@ -67,7 +67,7 @@ static std::once_flag g_knob_once;
 
 static void knobs_default() {
   g_knob[K_PLAN] = PLAN_AUTO;  // plan kernel by batch size and shape
-  g_knob[K_INTERLEAVE] = 1;    // interleaved block groups
+  g_knob[K_INTERLEAVE] = 1;    // bit 0: interleaved block groups; bit 1: XCD-aware group order (grp_index)
   g_knob[K_GROUP] = 0;         // 0: the measured per-shape group sizes
   g_knob[K_ENC_RT] = 0;        // encode tiles by r (0), one wave per group (enc_tile_waves 0)
   g_knob[K_ENC_W] = 0;
@@ -194,6 +194,18 @@ __device__ uint64_t g_fec_stamps[16];
 static uint32_t grid_for(uint64_t units);
 // The data-pass kernels run one group per workgroup (no grid-stride loop); a batch of more groups
 // than one grid holds (grid_for's cap) is launched in slices, q0 = the slice's first group.
+// The group a workgroup codes.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, workgroup dispatch); with `interleave` bit 1 the order is swizzled so each XCD's
+// workgroups take one contiguous run of groups -- with interleaved groups, one contiguous run of blocks
+// per XCD at a time -- instead of every eighth (bijective for any grid size:
+// cdna_hip_programming.md, XCD swizzle).  Bit 0 (interleaved groups) is read by the kernels themselves.
+__device__ __forceinline__ uint64_t grp_index(int ilv) {
+  const uint32_t orig = blockIdx.x, nwg = gridDim.x;
+  if (!(ilv & 2) || nwg <= 8) return orig;
+  const uint32_t q = nwg / 8, r = nwg % 8, x = orig % 8;
+  return (uint64_t)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8);
+}
+
 #define FEC_LAUNCH_GROUPS(KERNEL, GROUPS, BLOCK, LDS, STREAM, ...)                                  \
   for (uint64_t q0_ = 0; q0_ < (GROUPS); q0_ += grid_for(GROUPS)) {                               \
     const uint64_t n_ = (GROUPS) - q0_ < grid_for(GROUPS) ? (GROUPS) - q0_ : grid_for(GROUPS);   \
@@ -1388,12 +1400,12 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
   // Group q holds G blocks.  Interleaved (ilv): blocks q, q + NG, q + 2 NG, ... so the waves resident
   // at one time stream neighbouring blocks (dense HBM pages); otherwise blocks qG .. qG + G - 1.
   const uint64_t NG = (nblocks + G - 1) / G;
-  const uint64_t bstep = ilv ? NG : 1;
+  const uint64_t bstep = (ilv & 1) ? NG : 1;
   {  // one group per workgroup: no grid-stride loop invariants live across the asm body
-    const uint64_t q = q0 + blockIdx.x;
+    const uint64_t q = q0 + grp_index(ilv);
     if (q >= NG) return;
-    const uint64_t b0 = ilv ? q : q * G;
-    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const uint64_t b0 = (ilv & 1) ? q : q * G;
+    const uint64_t left = (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
     FEC_STAMP_AT(5);
@@ -1498,8 +1510,8 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
   const int lane = threadIdx.x;
   RecoverLds<RT> S(lds, G, k);
   {
-    const uint64_t b0 = ilv ? q : q * G;
-    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const uint64_t b0 = (ilv & 1) ? q : q * G;
+    const uint64_t left = (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     // wsl: the group's workspace records are copied into LDS first, 16 B per lane-piece, so the setup
     // below costs one memory round trip per group instead of a chain of dependent ones (header ->
@@ -1668,11 +1680,11 @@ void k_rlc_recover_bs(uint8_t *__restrict__ src, const uint8_t *__restrict__ rep
                                                        uint8_t *dst, uint32_t wsl_off, int dst_rows, uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t NG = (nblocks + G - 1) / G;  // groups; interleaved as in k_rlc_encode_bs
-  const uint64_t bstep = ilv ? NG : 1;
+  const uint64_t bstep = (ilv & 1) ? NG : 1;
   // one group per workgroup (the launcher splits batches of more groups than one grid holds): no
   // grid-stride loop whose invariants the compiler would keep live across the asm body (they cost
   // the wave-per-SIMD budget, 168 VGPRs for 3 waves)
-  const uint64_t q = q0 + blockIdx.x;
+  const uint64_t q = q0 + grp_index(ilv);
   if (q < NG)
     recover_bs_group<RT, VEC>(q, NG, bstep, src, rep, nblocks, k, r, L, nchunks, chunk_bytes, ws, r0, G, status,
                               recovered, ilv, dst, lds, wsl_off ? lds + wsl_off : nullptr, dst_rows);
@@ -2393,12 +2405,12 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
   if constexpr (!CW) r0 += wave * RT;
   const int rt = r - r0 < RT ? r - r0 : RT;  // <= 0: this wave has no repairs (waits at barriers)
   const uint64_t NG = (nblocks + G - 1) / G;
-  const uint64_t bstep = ilv ? NG : 1;
+  const uint64_t bstep = (ilv & 1) ? NG : 1;
   {  // one group per workgroup: no grid-stride loop invariants live across the asm body
-    const uint64_t q = q0 + blockIdx.x;
+    const uint64_t q = q0 + grp_index(ilv);
     if (q >= NG) return;
-    const uint64_t b0 = ilv ? q : q * G;
-    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const uint64_t b0 = (ilv & 1) ? q : q * G;
+    const uint64_t left = (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
     if ((CW ? (int)threadIdx.x : lane) < G * RT) {  // TinyMT32 rows: lane -> (block g, repair r0 + lane % RT)
@@ -2471,12 +2483,12 @@ void k_rlc_recover_bs2(uint8_t *__restrict__ src, const uint8_t *__restrict__ re
   const uint32_t ring = lds_addr(lds) + (uint32_t)pad16((uint32_t)RecoverLds<RT>::bytes(G, k)) +
                         (uint32_t)wave * Bs2Depth<RT>::dec * slotb;
   const uint64_t NG = (nblocks + G - 1) / G;
-  const uint64_t bstep = ilv ? NG : 1;
+  const uint64_t bstep = (ilv & 1) ? NG : 1;
   {  // one group per workgroup: no grid-stride loop invariants live across the asm body
-    const uint64_t q = q0 + blockIdx.x;
+    const uint64_t q = q0 + grp_index(ilv);
     if (q >= NG) return;
-    const uint64_t b0 = ilv ? q : q * G;
-    const uint64_t left = ilv ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const uint64_t b0 = (ilv & 1) ? q : q * G;
+    const uint64_t left = (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     bool act = false;
     int st = FECGPU_BLOCK_NOTHING, e = 0;
@@ -3023,6 +3035,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_DEPTH: return v >= 1 && v <= 16;
     case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
     case K_YIELD_STREAMS: return v >= 1 && v <= 4;
+    case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs
   }
 }

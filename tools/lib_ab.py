@@ -4,7 +4,9 @@ slots and packed), k32 r8 encode and k32 e8 decode apply (2^19 blocks).  Every b
 buffers; variants alternate over cycles; prints the median and min kernel time per (variant, case).
 --check: before timing, every variant's packed apply (k16 e4, k32 e8) must give the first variant's statuses,
 recovered masks and recovered rows (the rows of unknowns whose bit is set), byte for byte.
-usage: python tools/lib_ab.py name=path.so[:knob=value,...] ... [--cycles=N] [--check]"""
+--k64: configs[4] too (k64 r16 L9000 encode and e16 packed apply, 2^16 blocks).  Knobs a variant sets are
+restored to their values from before it ran (variants of one library share its knobs).
+usage: python tools/lib_ab.py name=path.so[:knob=value,...] ... [--cycles=N] [--check] [--k64]"""
 import ctypes as C
 import os
 import statistics
@@ -70,20 +72,36 @@ d32 = dec_setup(32, 8, 8, 1200, 1 << 19, 0x5EEDF3C1)
 cases.append(("enc k32r8", lambda e: e.rlc_encode(d32["src"], d32["rep"], 32, 8, 1200)))
 cases.append(("app_pk k32e8", lambda e: e.rlc_decode_apply_packed(d32["work"], d32["rep"], d32["rec_pk"], d32["st"],
                                                                    d32["rec"], 32, 8, 1200, d32["nb"], d32["ws"])))
+checks = [(d16, 4), (d32, 8)]
+if "--k64" in sys.argv:
+    d64 = dec_setup(64, 16, 16, 9000, 1 << 16, 0x5EEDF3C2)
+    cases.append(("enc k64r16", lambda e: e.rlc_encode(d64["src"], d64["rep"], 64, 16, 9000)))
+    cases.append(("app_pk k64e16", lambda e: e.rlc_decode_apply_packed(d64["work"], d64["rep"], d64["rec_pk"],
+                                                                        d64["st"], d64["rec"], 64, 16, 9000,
+                                                                        d64["nb"], d64["ws"])))
+    checks.append((d64, 16))
+
+
+def set_knobs(e, kv):
+    """sets a variant's knobs; returns their previous values"""
+    old = {k: e.get_knob(k) for k in kv}
+    for k, v in kv.items():
+        e.set_knob(k, v)
+    return old
+
+
 if "--check" in sys.argv:
-    for d, e_ in ((d16, 4), (d32, 8)):
+    for d, e_ in checks:
         ref = None
         for name, _ in variants:
             e = engines[name]
-            for kn, kv in knobs[name].items():
-                e.set_knob(kn, kv)
+            old = set_knobs(e, knobs[name])
             d["rec_pk"].fill_(0x5A)
             d["st"].fill_(0xEE)
             e.rlc_decode_apply_packed(d["work"], d["rep"], d["rec_pk"], d["st"], d["rec"], d["k"], d["r"], d["L"],
                                       d["nb"], d["ws"])
             torch.cuda.synchronize()
-            for kn in knobs[name]:
-                e.set_knob(kn, 0)
+            set_knobs(e, old)
             # rows of unknowns whose recovered bit is set (the u-th missing source of the block)
             bits = ((d["rec"][:, 0:1] >> d["miss"].clamp(max=63)) & 1).bool() & (d["miss"] < 64)
             got = (d["st"].clone(), d["rec"].clone(), d["rec_pk"][:, :e_][bits].clone())
@@ -100,8 +118,7 @@ ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 for cyc in range(cycles):
     for name, _ in variants:
         e = engines[name]
-        for kn, kv in knobs[name].items():
-            e.set_knob(kn, kv)
+        old = set_knobs(e, knobs[name])
         for cname, fn in cases:
             if cname.startswith("app_pk") and not has_packed(e):
                 continue
@@ -112,8 +129,7 @@ for cyc in range(cycles):
             ev[1].record()
             torch.cuda.synchronize()
             times.setdefault((name, cname), []).append(ev[0].elapsed_time(ev[1]) / 3)
-        for kn in knobs[name]:
-            e.set_knob(kn, 0)
+        set_knobs(e, old)
 print(f"{'variant':10s} " + " ".join(f"{c:>18s}" for c, _ in cases) + "   (median ms; min)")
 for name, _ in variants:
     cells = []

@@ -83,6 +83,7 @@ enc_done.record(main)
 idx = (torch.arange(nb, device=dev).unsqueeze(1) * k + miss.sort(dim=1).values.to(dev))
 for fn in (serial, overlapped, pipelined, pipelined):  # every schedule restores the sources
     dst.fill_(0)
+    torch.cuda.synchronize()  # the side stream's apply must not start before the fill
     fn()
     torch.cuda.synchronize()
     ok = (st == 0).nonzero().squeeze(1)
