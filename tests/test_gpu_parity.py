@@ -251,6 +251,43 @@ def test_decode_ws_lds_vs_oracle(eng, oracle, k, r, L, nb):
     assert (st_ref == DEC_RECOVERED).sum() > nb // 2
 
 
+@pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 12289), (32, 8, 1200, 4100), (64, 16, 9000, 37)])
+def test_group_order_knob_vs_oracle(eng, oracle, k, r, L, nb):
+    """Knob interleave: bit 0 interleaved block groups, bit 1 the XCD-aware order of the groups
+    (grp_index, bijective for grids that are not a multiple of 8).  Every setting gives the oracle's
+    repairs, statuses, masks and recovered bytes, on the register bodies and the LDS-ring ones."""
+    rng = np.random.default_rng(k * 13 + nb)
+    src_h = synth_bytes(nb * k * L, 17 + k).reshape(nb, k, L)
+    fbn_base = int(rng.integers(0, 1 << 24))
+    rep_h = oracle.rlc_encode_batch(src_h, r, fbn_base)
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    full_k, full_r = (1 << k) - 1, (1 << r) - 1
+    for b in range(nb):
+        miss = rng.choice(k, int(rng.integers(0, r + 1)), replace=False)
+        sp[b, 0] = full_k & ~int(sum(1 << int(j) for j in miss))
+        rp[b, 0] = full_r
+    ref = src_h.copy()
+    for b in range(nb):
+        for j in range(k):
+            if not (int(sp[b, 0]) >> j) & 1:
+                ref[b, j] = 0xA5
+    st_ref, rec_ref = oracle.rlc_decode_batch(ref, rep_h, sp, rp, fbn_base)
+    jbit = np.uint64(1) << np.arange(k, dtype=np.uint64)
+    keep = ((rec_ref[:, 0:1] | sp[:, 0:1]) & jbit) != 0
+    src_d = to_dev(src_h)
+    for v in (0, 1, 2, 3):
+        with eng.knob("interleave", v):
+            rep_d = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
+            eng.rlc_encode(src_d, rep_d, k, r, L, fbn_base=fbn_base)
+            torch.cuda.synchronize()
+            assert np.array_equal(rep_d.cpu().numpy(), rep_h), v
+            _, got, st, rec = _run_decode_batch(eng, k, r, L, src_h, rep_h, sp, rp, fbn_base=fbn_base)
+        assert np.array_equal(st, st_ref), v
+        assert np.array_equal(rec, rec_ref), v
+        assert np.array_equal(got[keep], src_h[keep]), v
+
+
 @pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 1), (16, 4, 1200, 64), (32, 8, 1200, 7), (5, 5, 20, 33),
                                       (64, 16, 9000, 3), (20, 16, 2052, 9), (3, 1, 4, 2), (32, 9, 1200, 5),
                                       (1, 1, 16, 3), (31, 8, 100, 17)])
