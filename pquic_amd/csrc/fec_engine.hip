@@ -55,10 +55,11 @@ static std::atomic<uint64_t> g_stats[4];
 // environment variables, so nothing outside the caller's own calls can change which kernels run.
 // ---------------------------------------------------------------------------------------------
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
+              K_ENC_BW,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
               K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
-                                           "zc_read", "ring", "window_sc", "min_groups", "chunk_waves",
+                                           "zc_read", "ring", "window_sc", "min_groups", "enc_block_waves", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
                                            "yield_depth", "yield_gate_us", "yield_streams", "yield_always"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
@@ -71,6 +72,9 @@ static void knobs_default() {
   g_knob[K_GROUP] = 0;         // 0: the measured per-shape group sizes
   g_knob[K_ENC_RT] = 0;        // encode tiles by r (0), one wave per group (enc_tile_waves 0)
   g_knob[K_ENC_W] = 0;
+  // register-prefetch encode: waves per workgroup, each on its own block group (adjacent groups share a CU;
+  // §5.6 probe acol); 1 = one wave per workgroup
+  g_knob[K_ENC_BW] = 1;
   g_knob[K_ZC_READ] = 1;       // page-locked host buffers read by the kernels in place
   // LDS-ring data path (bs2 bodies) for 16-repair / 16-unknown tiles: 2 (default) on, 0 off
   g_knob[K_RING] = 2;
@@ -1389,27 +1393,30 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                        uint64_t nblocks, int k, int r, int L, int nchunks,
                                                        int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
                                                        int r0, int G, uint64_t sbs, uint32_t fbn_step, int ilv,
-                                                       uint64_t q0) {
+                                                       int bw, uint64_t q0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the asm's SGPRs
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);  // per source: RT (>= 4) u16 case offsets
   uint8_t *lds = lds_all + (size_t)wave * G * k * CSB;
-  const int r0w = r0 + wave * RT;
+  // bw > 1: the workgroup's waves code bw adjacent groups (knob enc_block_waves); else its waves split the
+  // group's repairs (W waves, each RT of them)
+  const int r0w = r0 + (bw > 1 ? 0 : wave * RT);
   const int rt = r - r0w < RT ? r - r0w : RT;  // <= 0: this wave has no repairs (waits at barriers)
   // Group q holds G blocks.  Interleaved (ilv): blocks q, q + NG, q + 2 NG, ... so the waves resident
   // at one time stream neighbouring blocks (dense HBM pages); otherwise blocks qG .. qG + G - 1.
   const uint64_t NG = (nblocks + G - 1) / G;
   const uint64_t bstep = (ilv & 1) ? NG : 1;
-  {  // one group per workgroup: no grid-stride loop invariants live across the asm body
-    const uint64_t q = q0 + grp_index(ilv);
-    if (q >= NG) return;
+  {  // one group per wave: no grid-stride loop invariants live across the asm body
+    const uint64_t q = bw > 1 ? (q0 + grp_index(ilv)) * bw + wave : q0 + grp_index(ilv);
+    const bool live = q < NG;  // a wave past the end still meets its workgroup's barriers
+    if (bw == 1 && !live) return;
     const uint64_t b0 = (ilv & 1) ? q : q * G;
-    const uint64_t left = (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
+    const uint64_t left = !live ? 0 : (ilv & 1) ? (nblocks - q + NG - 1) / NG : nblocks - b0;
     const int ng = left < (uint64_t)G ? (int)left : G;
     __syncthreads();
     FEC_STAMP_AT(5);
-    if (lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
+    if (live && lane < G * RT) {  // TinyMT32 rows: lane -> (block g of the group, repair r0w + lane % RT)
       const int g = lane / RT, i = lane % RT;
       const uint64_t b = b0 + g * bstep;
       uint16_t *row0 = reinterpret_cast<uint16_t *>(lds + (size_t)g * k * CSB);
@@ -1434,7 +1441,7 @@ void k_rlc_encode_bs(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
     }
     __syncthreads();
     FEC_STAMP_AT(6);
-    if (rt <= 0) return;
+    if (rt <= 0 || !live) return;
     for (int ch = 0; ch < nchunks; ch++) {
       const int c0 = ch * chunk_bytes;
       const int cb = L - c0 < chunk_bytes ? L - c0 : chunk_bytes;
@@ -2134,10 +2141,14 @@ static void launch_encode_bs(const uint8_t *src, uint8_t *rep, uint64_t nb, int 
                              uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                              hipStream_t s) {
   const int G = sbs == (uint64_t)k * L ? bs_group(RT, k, FEC_BS_COEF_ROW_BYTES(RT), 0, true, c.nchunks, nb) : 1;
-  const size_t lds = (size_t)W * G * k * FEC_BS_COEF_ROW_BYTES(RT);
   const uint64_t groups = (nb + G - 1) / G;
-  FEC_LAUNCH_GROUPS((k_rlc_encode_bs<RT, VEC>), groups, 64 * W, lds, s, src, rep, nb, k, r, L, c.nchunks,
-                    c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups())
+  // knob enc_block_waves: bw waves per workgroup on adjacent groups (only with whole blocks, one wave's repairs)
+  int bw = W == 1 && sbs == (uint64_t)k * L ? knob(K_ENC_BW) : 1;
+  if ((uint64_t)bw > groups) bw = 1;
+  const int wpw = bw > 1 ? bw : W;  // waves per workgroup
+  const size_t lds = (size_t)wpw * G * k * FEC_BS_COEF_ROW_BYTES(RT);
+  FEC_LAUNCH_GROUPS((k_rlc_encode_bs<RT, VEC>), (groups + bw - 1) / bw, 64 * wpw, lds, s, src, rep, nb, k, r, L,
+                    c.nchunks, c.chunk_bytes, fbn_base, fbn, r0, G, sbs, fbn_step, interleave_groups(), bw)
 }
 
 template <int RT, int VEC>
@@ -3027,6 +3038,7 @@ static bool knob_value_ok(int id, int v) {
     case K_PLAN: return v >= PLAN_AUTO && v <= PLAN_WREG;
     case K_ENC_RT: return v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16;
     case K_ENC_W: return v >= 0 && v <= 4;
+    case K_ENC_BW: return v == 1 || v == 2 || v == 4;
     case K_RING: return v == 0 || v == 2 || (v == 4 && FEC_BS2_HAS_RT4);
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;

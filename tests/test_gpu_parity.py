@@ -254,8 +254,9 @@ def test_decode_ws_lds_vs_oracle(eng, oracle, k, r, L, nb):
 @pytest.mark.parametrize("k,r,L,nb", [(16, 4, 1200, 12289), (32, 8, 1200, 4100), (64, 16, 9000, 37)])
 def test_group_order_knob_vs_oracle(eng, oracle, k, r, L, nb):
     """Knob interleave: bit 0 interleaved block groups, bit 1 the XCD-aware order of the groups
-    (grp_index, bijective for grids that are not a multiple of 8).  Every setting gives the oracle's
-    repairs, statuses, masks and recovered bytes, on the register bodies and the LDS-ring ones."""
+    (grp_index, bijective for grids that are not a multiple of 8); knob enc_block_waves: 2 or 4 waves per
+    workgroup on adjacent groups.  Every setting gives the oracle's repairs, statuses, masks and
+    recovered bytes, on the register bodies and the LDS-ring ones."""
     rng = np.random.default_rng(k * 13 + nb)
     src_h = synth_bytes(nb * k * L, 17 + k).reshape(nb, k, L)
     fbn_base = int(rng.integers(0, 1 << 24))
@@ -276,6 +277,12 @@ def test_group_order_knob_vs_oracle(eng, oracle, k, r, L, nb):
     jbit = np.uint64(1) << np.arange(k, dtype=np.uint64)
     keep = ((rec_ref[:, 0:1] | sp[:, 0:1]) & jbit) != 0
     src_d = to_dev(src_h)
+    for bw in (2, 4):  # knob enc_block_waves: a workgroup's waves on adjacent groups (register bodies)
+        with eng.knob("enc_block_waves", bw):
+            rep_d = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
+            eng.rlc_encode(src_d, rep_d, k, r, L, fbn_base=fbn_base)
+            torch.cuda.synchronize()
+            assert np.array_equal(rep_d.cpu().numpy(), rep_h), bw
     for v in (0, 1, 2, 3):
         with eng.knob("interleave", v):
             rep_d = torch.empty((nb, r, L), dtype=torch.uint8, device=DEV)
