@@ -1578,9 +1578,15 @@ __device__ void recover_bs_group(uint64_t q, uint64_t NG, uint64_t bstep, uint8_
         row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD((uint32_t)(0x53 + j + u) & 0xffu, u) : (uint16_t)0;
       const uint32_t sl = j < k - rt ? (uint32_t)(j + rt) : (uint32_t)(0x80 | (j - (k - rt)));
 #else
+#ifdef FEC_PROBE_NOFIELD  // timing probe only (wrong bytes): the records are read, the D bytes are not
+#pragma unroll
+      for (int u = 0; u < NF; u++)
+        row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD((uint32_t)(0x53 + j + u) & 0xffu, u) : (uint16_t)0;
+#else
 #pragma unroll
       for (int u = 0; u < NF; u++)  // case offset of D[u][j]; 0 past the live unknowns ends the chain
         row[FEC_BS_FIELD_SLOT(RT, u)] = (u < rt) ? FEC_BS_FIELD(h[WL.off_D + (r0 + u) * k + j], u) : (uint16_t)0;
+#endif
       const uint32_t sl = h[WL.off_slot + j];
 #endif
       if (dst_rows < 0) {  // row tables: src / rep hold the rows' device addresses ([block][k] / [block][r])
