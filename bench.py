@@ -711,7 +711,7 @@ def host_legs_child(args, dev_index):
     env = dict(os.environ)
     env["PQUIC_BENCH_HOST_DEVICE"] = str(dev_index)
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     except subprocess.TimeoutExpired:
         return {"host_legs": {"error": "timeout"}}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
