@@ -63,6 +63,10 @@ EARLY_CO = os.environ.get("FEC_GEN_EARLY_CO", "0") != "0"
 # register-prefetch bodies compute exec-masked to the lanes that own pieces (vm0: at L = 1200, 38 of
 # 64), as the ring bodies do; idle lanes then neither load nor switch
 EXECMASK = os.environ.get("FEC_GEN_EXECMASK", "0") != "0"
+# TOUCH (decode register bodies, EARLY_PF): after each row's loads, one dword load per lane 32 bytes
+# apart over the row TOUCH - 1 rows beyond it (an L2 warm-up of a row not yet in flight; the data is
+# dropped).  Costs 4 VGPRs above the accumulators and one VMEM per row in the vmcnt budget
+TOUCH = int(os.environ.get("FEC_GEN_TOUCH", "0"))
 
 
 def table_map(B):
@@ -419,7 +423,11 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     NP = 32 // VEC
     DATA_BASE = data_base(mode)
     acc_base = DATA_BASE + 8 * P
-    assert acc_base + 8 * RT <= 256
+    touch = TOUCH if mode == "dec" and EARLY_PF else 0
+    TA = acc_base + 8 * RT  # touch: the row address (pair), the dropped data, the lane offset
+    TD, TOFF = TA + 2, TA + 3
+    assert acc_base + 8 * RT + (4 if touch else 0) <= 256
+    assert not touch or (touch >= 2 and (NP + 1) * (P - 1) + 1 <= 63)
     L = []
     a = L.append
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -456,6 +464,12 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     else:
         a(f"v_mov_b32 v{INPTR}, %[intab]")
         a(f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}")  # source 0's address
+        if touch:  # row touch - 1's address, touched after source 0's loads
+            a(f"ds_read_b64 v[{TA}:{TA + 1}], v{INPTR} offset:{8 * (touch - 1)}")
+            a(f"v_lshlrev_b32 v{TOFF}, {NP.bit_length() - 1}, %[off0]")  # lane * 32 (0 on idle lanes)
+            # S_JL = rows with a touch target (y + touch - 1 < nsrc for the y-th row loaded)
+            a(f"s_sub_u32 s{S_JL}, %[nsrc], {touch - 1}")
+            a(f"s_cselect_b32 s{S_JL}, 0, s{S_JL}")
         a(f"v_add_u32 v{INPTR}, 8, v{INPTR}")
         a(f"v_mov_b32 v{OUTPTR}, %[outtab]")
     # count-down loop counters, tested by the borrow of s_sub_u32 (no compares in the loop):
@@ -477,12 +491,23 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
             out += [f"s_waitcnt lgkmcnt({lgkm})",
                     f"v_readfirstlane_b32 s{S_CUR}, v{NADDR}",
                     f"v_readfirstlane_b32 s{S_CUR + 1}, v{NADDR + 1}",
-                    f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}",
-                    f"v_add_u32 v{INPTR}, 8, v{INPTR}"]
+                    f"ds_read_b64 v[{NADDR}:{NADDR + 1}], v{INPTR}"]
+            if touch:  # the touch target read one row ago, and the next one's address
+                out += [f"v_readfirstlane_b32 s{S_O2}, v{TA}",
+                        f"v_readfirstlane_b32 s{S_O2 + 1}, v{TA + 1}",
+                        f"ds_read_b64 v[{TA}:{TA + 1}], v{INPTR} offset:{8 * (touch - 1)}"]
+            out += [f"v_add_u32 v{INPTR}, 8, v{INPTR}"]
         # no exec switching: a lane's piece past the chunk end has offset 0 (BsLanes), so its load
         # stays inside the row, and its bytes never reach memory (the stores are masked)
         for q in range(NP):
             out.append(f"{ld} {regrange(DATA_BASE + 8 * buf + q * nw, nw)}, %[off{q}], s[{S_CUR}:{S_CUR + 1}]@LDPOL@")
+        if touch:
+            # past the last target the touch re-reads this row (every row's loads are followed by
+            # exactly one touch, which the vmcnt waits count); the selects leave S_O2 SALU-written
+            out += [f"s_sub_u32 s{S_JL}, s{S_JL}, 1",
+                    f"s_cselect_b64 s[{S_O2}:{S_O2 + 1}], s[{S_CUR}:{S_CUR + 1}], s[{S_O2}:{S_O2 + 1}]",
+                    f"s_cselect_b32 s{S_JL}, 0, s{S_JL}",
+                    f"global_load_dword v{TD}, v{TOFF}, s[{S_O2}:{S_O2 + 1}]"]
         if mode == "enc":
             # next row of this block, or -- after its k-th row -- the first row of the group's next
             # block, which starts bstep blocks further on: one 64-bit select between the two steps
@@ -518,7 +543,8 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
             # source s waits in buffer b; P sources are in flight.  Round 0 of the transpose is the
             # buffer's only reader, so source s + P is loaded into it right after (SCC still holds
             # the borrow of the S_T2 decrement: VALU and s_waitcnt leave it alone)
-            a(f"s_waitcnt vmcnt({NP * (P - 1)})")
+            # with touches: each younger row brings NP + 1 loads, and this row's own touch follows it
+            a(f"s_waitcnt vmcnt({(NP + 1) * (P - 1) + 1 if touch else NP * (P - 1)})")
             a(f".Lpf{b}_%=:")
             ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
             tr = transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE))
@@ -660,7 +686,7 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     a("s_waitcnt lgkmcnt(0)")
     a(f"s_mov_b64 exec, s[{S_SAVEEX}:{S_SAVEEX + 1}]")
     a(f"s_mov_b32 m0, s{S_SAVEM0}")
-    return L, acc_base + 8 * RT
+    return L, acc_base + 8 * RT + (4 if touch else 0)
 
 
 def cstring(lines):
@@ -1117,7 +1143,9 @@ def prefetch_depth(mode: str, RT: int, VEC: int = 16) -> int:
     # 2-wave budget for decode: RT=8 needs a larger margin than RT=16 (measured: a 242 budget at
     # RT=8 compiled to 256 VGPRs + 4 AGPRs = 1 wave/SIMD, k32 e8 apply 13 ms -> 7.6 ms at 222)
     budget2 = 256 - margin - (8 if mode == "dec" and RT <= 8 else 0)
-    fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT <= lim and NP * (P - (0 if EARLY_PF else 1)) <= 63
+    tv = 4 if TOUCH and mode == "dec" and EARLY_PF else 0
+    fits = lambda P, lim: data_base(mode) + 8 * P + 8 * RT + tv <= lim and NP * (P - (0 if EARLY_PF else 1)) <= 63 \
+        and (not tv or (NP + 1) * (P - 1) + 1 <= 63)
     # 4-unknown decode tiles take the 2-wave budget: 19 rows in flight at 2 waves/SIMD streamed the k16 e4
     # apply 2.3 % faster than 8 at 3 waves (profiles/r03_ab_dec_occupancy.log); 8-unknown tiles keep 3
     # waves (2 waves: +13-20 %)
