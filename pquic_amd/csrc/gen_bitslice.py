@@ -67,6 +67,9 @@ EXECMASK = os.environ.get("FEC_GEN_EXECMASK", "0") != "0"
 # apart over the row TOUCH - 1 rows beyond it (an L2 warm-up of a row not yet in flight; the data is
 # dropped).  Costs 4 VGPRs above the accumulators and one VMEM per row in the vmcnt budget
 TOUCH = int(os.environ.get("FEC_GEN_TOUCH", "0"))
+# DEC_EPI_PF (decode register bodies): the epilogue reads each output address one row ahead, so no
+# LDS round trip is waited for per recovered row (before: one per row plus one for the row count)
+DEC_EPI_PF = os.environ.get("FEC_GEN_DEC_EPI_PF", "0") != "0"
 
 
 def table_map(B):
@@ -424,6 +427,10 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     DATA_BASE = data_base(mode)
     acc_base = DATA_BASE + 8 * P
     touch = TOUCH if mode == "dec" and EARLY_PF else 0
+    epi_pf = mode == "dec" and DEC_EPI_PF and T64
+    EPI_RT, EPI_AD = PL[0], PL[2]  # v32, v34:35 (planes, dead in the epilogue; clear of t64 scratch)
+    assert not epi_pf or (EPI_AD % 2 == 0 and EPI_AD + 1 == PL[3] and {EPI_RT, EPI_AD, EPI_AD + 1}.isdisjoint(
+        set(sum(t64_scratch(T_BASE), []))))
     TA = acc_base + 8 * RT  # touch: the row address (pair), the dropped data, the lane offset
     TD, TOFF = TA + 2, TA + 3
     assert acc_base + 8 * RT + (4 if touch else 0) <= 256
@@ -639,20 +646,45 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
     if mode == "enc":
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
+    elif epi_pf:
+        # the block's row count and first output address are read now and waited for after row 0's
+        # transpose; each later address is read one row ahead (into plane registers, dead here)
+        a(f"ds_read_b32 v{EPI_RT}, v{OUTPTR} offset:{DEC_REC_RT}")
+        a(f"ds_read_b64 v[{EPI_AD}:{EPI_AD + 1}], v{OUTPTR}")
     else:
         a(f"ds_read_b32 v{TMP[2]}, v{OUTPTR} offset:{DEC_REC_RT}")
         a("s_waitcnt lgkmcnt(0)")
         a(f"v_readfirstlane_b32 s{S_RT}, v{TMP[2]}")
     for i in range(RT):
         accs = [acc_base + 8 * i + w for w in range(8)]
-        a(f"s_cmp_le_u32 s{S_RT}, {i}")
-        a(f"s_cbranch_scc1 .Lepi_done_%=")
+        if not (epi_pf and i == 0):
+            a(f"s_cmp_le_u32 s{S_RT}, {i}")
+            a(f"s_cbranch_scc1 .Lepi_done_%=")
         if T64:
             slots = [accs[SIG[o]] for o in range(8)]  # plane o / word o
             L.extend(transpose64(slots, slots, *t64_scratch(T_BASE)))
         else:
             L.extend(transpose_inplace(accs))
-        if mode == "dec":
+        if epi_pf:
+            a(f"v_or3_b32 v{TMP[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
+            a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[3]}, v{accs[4]}")
+            a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[5]}, v{accs[6]}")
+            a(f"v_or_b32 v{TMP[0]}, v{TMP[0]}, v{accs[7]}")
+            a("s_waitcnt lgkmcnt(0)")  # this row's address (and the last row's flag write)
+            if i == 0:  # a block with no rows: row 0's transpose was harmless, nothing is stored
+                a(f"v_readfirstlane_b32 s{S_RT}, v{EPI_RT}")
+                a(f"s_cmp_le_u32 s{S_RT}, 0")
+                a(f"s_cbranch_scc1 .Lepi_done_%=")
+            a(f"v_readfirstlane_b32 s{S_O2}, v{EPI_AD}")
+            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{EPI_AD + 1}")
+            if i + 1 < RT:
+                a(f"ds_read_b64 v[{EPI_AD}:{EPI_AD + 1}], v{OUTPTR} offset:{8 * (i + 1)}")
+            a(f"v_cmp_ne_u32 vcc, 0, v{TMP[0]}")
+            a(f"v_mov_b32 v{TMP[1]}, 1")
+            a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
+            a(f"ds_write_b8 v{OUTPTR}, v{TMP[1]} offset:{DEC_REC_NZ + i}")  # non-zero flag (LDS)
+            a(f"s_mov_b64 exec, {live}")
+        elif mode == "dec":
             a(f"ds_read_b64 v[{TMP[2]}:{TMP[3]}], v{OUTPTR} offset:{8 * i}")
             a(f"v_or3_b32 v{TMP[0]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
             a(f"v_or3_b32 v{TMP[0]}, v{TMP[0]}, v{accs[3]}, v{accs[4]}")
@@ -1031,9 +1063,16 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
     # the next source's combos (E0:E1 the output address, E2 the record pointer, E3/E4 the flag)
     E = [TLm[3], TLm[5], TLm[6], TLm[7], TLm[9]]
     assert E[0] % 2 == 0 and E[1] == E[0] + 1
+    epi_pf = mode == "dec" and DEC_EPI_PF and T64
+    assert not epi_pf or set(E).isdisjoint(set(sum(t64_scratch(T2_BASE), [])))
     if mode == "enc":
         a(f"s_mov_b64 s[{S_O2}:{S_O2 + 1}], s[{S_OUT}:{S_OUT + 1}]")
         a(f"s_mov_b32 s{S_RT}, %[rt]")
+    elif epi_pf:
+        # as the register bodies: the row count and each output address are read a row ahead
+        a(f"v_mov_b32 v{E[2]}, s{S_OUTPTR}")
+        a(f"ds_read_b32 v{E[3]}, v{E[2]} offset:{DEC_REC_RT}")
+        a(f"ds_read_b64 v[{E[0]}:{E[1]}], v{E[2]}")
     else:
         a(f"v_mov_b32 v{E[2]}, s{S_OUTPTR}")
         a(f"ds_read_b32 v{E[0]}, v{E[2]} offset:{DEC_REC_RT}")
@@ -1041,14 +1080,34 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         a(f"v_readfirstlane_b32 s{S_RT}, v{E[0]}")
     for i in range(RT):
         accs = [acc_base + 8 * (i % NACC) + w for w in range(8)]
-        a(f"s_cmp_le_u32 s{S_RT}, {i}")
-        a(f"s_cbranch_scc1 .Lepi_done_%=")
+        if not (epi_pf and i == 0):
+            a(f"s_cmp_le_u32 s{S_RT}, {i}")
+            a(f"s_cbranch_scc1 .Lepi_done_%=")
         if T64:
             slots = [accs[SIG[o]] for o in range(8)]
             L.extend(transpose64(slots, slots, *t64_scratch(T2_BASE)))
         else:
             L.extend(transpose_inplace(accs, TMPm))
-        if mode == "dec":
+        if epi_pf:
+            a("s_waitcnt lgkmcnt(0)")  # this row's address (and the last row's flag write)
+            if i == 0:  # a block with no rows: row 0's transpose was harmless, nothing is stored
+                a(f"v_readfirstlane_b32 s{S_RT}, v{E[3]}")
+                a(f"s_cmp_le_u32 s{S_RT}, 0")
+                a(f"s_cbranch_scc1 .Lepi_done_%=")
+            a(f"v_readfirstlane_b32 s{S_O2}, v{E[0]}")
+            a(f"v_readfirstlane_b32 s{S_O2 + 1}, v{E[1]}")
+            if i + 1 < RT:
+                a(f"ds_read_b64 v[{E[0]}:{E[1]}], v{E[2]} offset:{8 * (i + 1)}")
+            a(f"v_or3_b32 v{E[3]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
+            a(f"v_or3_b32 v{E[3]}, v{E[3]}, v{accs[3]}, v{accs[4]}")
+            a(f"v_or3_b32 v{E[3]}, v{E[3]}, v{accs[5]}, v{accs[6]}")
+            a(f"v_or_b32 v{E[3]}, v{E[3]}, v{accs[7]}")
+            a(f"v_cmp_ne_u32 vcc, 0, v{E[3]}")
+            a(f"v_mov_b32 v{E[4]}, 1")
+            a("s_and_saveexec_b64 s[{0}:{1}], vcc".format(S_T3, S_T3 + 1))
+            a(f"ds_write_b8 v{E[2]}, v{E[4]} offset:{DEC_REC_NZ + i}")
+            a("s_mov_b64 exec, %[vm0]")  # 10 instructions after the readfirstlanes: no s_nop
+        elif mode == "dec":
             a(f"ds_read_b64 v[{E[0]}:{E[1]}], v{E[2]} offset:{8 * i}")
             a(f"v_or3_b32 v{E[3]}, v{accs[0]}, v{accs[1]}, v{accs[2]}")
             a(f"v_or3_b32 v{E[3]}, v{E[3]}, v{accs[3]}, v{accs[4]}")
