@@ -552,18 +552,22 @@ def batching_legs(dev_index, args):
     legs["batch_paced_2GiBps"] = {"error": rc} if rc else leg(
         out, extra, blocks=100000, connections=64, offered_GiB_s=2.0, max_delay_us=250, batch_blocks=4096)
     # two sender threads, each with its own batcher and 64 connections: a server running one
-    # single-threaded PQUIC process per core on one GPU (one sender alone is bound by its own thread)
+    # single-threaded PQUIC process per core on one GPU (one sender alone is bound by its own thread).
+    # Two batchers share the GPU, so each takes half the batch: the same rate at half the latency
+    # (profiles/r05_senders_sweep.log: 2048 blocks 48.0 GiB/s at p99 5.1-6.9 ms, 1024 46.6 at 2.7-3.1 ms)
+    batch2 = 1024
     res = []
     for _ in range(3):
         out = (C.c_double * 8)()
-        if lib.bl_run_senders(2, dev_index, args.k, args.r, args.symbol, 64, 200000, batch, 2000, 2,
+        if lib.bl_run_senders(2, dev_index, args.k, args.r, args.symbol, 64, 200000, batch2, 2000, 2,
                               REG | PER_CONN, out):
             break
         res.append(list(out))
     if len(res) == 3:
         out = sorted(res, key=lambda o: o[0])[1]
         legs["batch_saturated_2senders"] = leg(
-            out, {"runs_payload_GiB_s": [round(o[0], 2) for o in res]}, senders=2, blocks_per_sender=200000,
+            out, {"runs_payload_GiB_s": [round(o[0], 2) for o in res]}, batch_blocks=batch2, senders=2,
+            blocks_per_sender=200000,
             connections_per_sender=64, arenas="one 16 MiB arena per connection",
             note="both senders start each pass at a barrier; rate = all blocks over first start to last drain; "
                  "latency = the worse sender's percentile")
