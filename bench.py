@@ -574,12 +574,15 @@ def batching_legs(dev_index, args):
     lib.bl_set_inflight(4)
     # the sliding-window sender (window_framework_sender.h:209-260) at the redundancy controllers'
     # shapes: a window of the <= 30 symbols in flight every K new ones, N - K repairs
+    # batches of 1536 windows: the same or a higher rate than 2048 or 4096, at a third of 4096's p99
+    # (profiles/r05_window_batch_sweep.log)
+    wbatch = 1536
     for k, r, step in ((30, 1, 5), (30, 5, 25)):
         leg_w = {"k": k, "r": r, "L": args.symbol, "step": step, "windows": 200000, "connections": 64,
-                 "batch_blocks": 4096, "max_delay_us": 2000}
+                 "batch_blocks": wbatch, "max_delay_us": 2000}
         for api, tag in ((1, "window_api"), (0, "block_api")):
             out = (C.c_double * 8)()
-            rc = lib.bl_run_window(dev_index, k, r, args.symbol, step, 64, 200000, 4096, 2000, 2, api, out)
+            rc = lib.bl_run_window(dev_index, k, r, args.symbol, step, 64, 200000, wbatch, 2000, 2, api, out)
             leg_w[tag] = {"error": rc} if rc else {
                 "stream_GiB_s": round(out[0], 2), "window_GiB_s": round(out[7], 2), "latency_us_p50": out[1],
                 "latency_us_p99": out[2], "batches": int(out[4])}
