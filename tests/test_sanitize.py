@@ -16,7 +16,8 @@ import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 SAN = os.path.join(ROOT, "tests", "sanitize")
-SUITES = ["tests/test_protoops_gpu.py", "tests/test_batch_gpu.py", "tests/test_frames.py", "tests/test_cc.py"]
+SUITES = ["tests/test_protoops_gpu.py", "tests/test_batch_gpu.py", "tests/test_frames.py",
+          "tests/test_frames_differential.py", "tests/test_cc.py"]
 REPORTS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer", "ERROR: LeakSanitizer")
 
 
