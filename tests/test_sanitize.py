@@ -17,7 +17,7 @@ import pytest
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 SAN = os.path.join(ROOT, "tests", "sanitize")
 SUITES = ["tests/test_protoops_gpu.py", "tests/test_batch_gpu.py", "tests/test_frames.py",
-          "tests/test_frames_differential.py", "tests/test_cc.py"]
+          "tests/test_frames_differential.py", "tests/test_cc.py", "tests/test_cc_differential.py"]
 REPORTS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer", "ERROR: LeakSanitizer")
 
 
