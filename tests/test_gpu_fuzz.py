@@ -90,3 +90,62 @@ def test_random_shape_encode_decode(eng, oracle, seed):
         for u, j in enumerate(missing[:em]):
             if j in bits(rec_ref[b], k):
                 assert np.array_equal(pk_h[b, u], src_h[b, j]), (tag, b, j, "packed")
+
+
+@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("window_sc", [0, 2])
+def test_random_window_encode(eng, oracle, seed, window_sc):
+    """Sliding-window encode (window_framework_sender.h:214-250: block number 0, coefficients seeded
+    by the repair index) on random (k, r, step, L, windows): overlapping, adjacent and gapped windows;
+    window_sc 2 forces the shared-coefficient kernel (16-B-aligned L), 0 the block-at-a-time one."""
+    rng = np.random.default_rng(0xF0230000 + seed)
+    k = int(rng.integers(1, 65))
+    r = int(rng.integers(1, 17))
+    step = int(rng.integers(1, k + 8))
+    L = 16 * int(rng.choice([1, 3, 75, 128, int(rng.integers(1, 565))]))
+    nw = max(1, min(int(rng.integers(1, 600)), (8 << 20) // ((step + r) * L)))
+    nsym = (nw - 1) * step + k
+    sym_h = synth_bytes(nsym * L, 0xF1D0 + seed).reshape(nsym, L)
+    rep = torch.empty((nw, r, L), dtype=torch.uint8, device=DEV)
+    old = eng.get_knob("window_sc")
+    try:
+        eng.set_knob("window_sc", window_sc)
+        eng.rlc_window_encode(to_dev(sym_h), rep, nw, step, k, r, L)
+    finally:
+        eng.set_knob("window_sc", old)
+    torch.cuda.synchronize()
+    got = rep.cpu().numpy()
+    tag = f"seed {seed}: k {k} r {r} step {step} L {L} windows {nw} window_sc {window_sc}"
+    for w in range(nw):
+        want = oracle.rlc_encode_block(0, list(sym_h[w * step: w * step + k]), r)[1]
+        for i in range(r):
+            assert np.array_equal(got[w, i], want[i]), (tag, w, i)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_xor(eng, oracle, seed):
+    """XOR encode and single-erasure recover (xor_fec_scheme.c) on random k (the specialised kernels
+    and the runtime-k one), L and block counts, erasures 0..2 per block, the repair sometimes absent."""
+    rng = np.random.default_rng(0xF0240000 + seed)
+    k = int(rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 16, int(rng.integers(1, 129))]))
+    L = 4 * int(rng.choice([1, 4, 300, 304, int(rng.integers(1, 2251))]))
+    nb = max(1, min(int(rng.choice([1, 7, 100, 1000, 5000])), (16 << 20) // ((k + 1) * L)))
+    src_h = synth_bytes(nb * k * L, 0xF2D0 + seed).reshape(nb, k, L)
+    rep = torch.empty((nb, 1, L), dtype=torch.uint8, device=DEV)
+    eng.xor_encode(to_dev(src_h), rep, k, L)
+    torch.cuda.synchronize()
+    rep_h = rep.cpu().numpy()
+    tag = f"seed {seed}: k {k} L {L} nb {nb}"
+    assert np.array_equal(rep_h, oracle.xor_encode_batch(src_h)), tag
+    sp = np.zeros((nb, 2), np.uint64)
+    rp = np.zeros((nb, 2), np.uint64)
+    for b in range(nb):
+        miss = set(rng.choice(k, min(int(rng.integers(0, 3)), k), replace=False).tolist())
+        sp[b] = masks_from_lists(1, k, [[j for j in range(k) if j not in miss]])[0]
+        rp[b] = masks_from_lists(1, 1, [[0]] if rng.random() < 0.8 else [[]])[0]
+    work, got, st, rec = _run_decode_batch(eng, k, 1, L, src_h, rep_h, sp, rp, scheme="xor")
+    ref = work.copy()
+    st_ref, rec_ref = oracle.xor_decode_batch(ref, rep_h, sp, rp)
+    assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref), tag
+    ok = st == 0
+    assert np.array_equal(got[ok], src_h[ok]), tag
