@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from oracle_py import Oracle, synth_bytes
-from test_gpu_parity import DEV, _run_decode_batch, bits, masks_from_lists, to_dev
+from test_gpu_parity import DEV, _run_decode_batch, bits, masks_from_lists, test_decode_rows_vs_oracle, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -149,3 +149,16 @@ def test_random_xor(eng, oracle, seed):
     assert np.array_equal(st, st_ref) and np.array_equal(rec, rec_ref), tag
     ok = st == 0
     assert np.array_equal(got[ok], src_h[ok]), tag
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_decode_rows(eng, oracle, seed):
+    """The receive-side gather (fecgpu_rlc_decode_rows: every row anywhere in a shuffled pool, per-repair
+    seeds, recovered rows written through the table) on random shapes: the parametrized parity test's
+    body, with k, r, L and the block count drawn here."""
+    rng = np.random.default_rng(0xF0250000 + seed)
+    k = int(rng.integers(1, 129))
+    r = int(rng.integers(1, 65))
+    L = 4 * int(rng.choice([1, 5, 300, 304, int(rng.integers(1, 2251))]))
+    nb = max(8, min(int(rng.choice([17, 300, 2000])), (8 << 20) // ((k + r) * L)))  # the body asserts some recovery
+    test_decode_rows_vs_oracle(eng, oracle, k, r, L, nb)
