@@ -212,3 +212,55 @@ def test_oversized_block_rejected_before_the_device(host):
     host.lib.mh_protoop_stats(_p(st1, C.c_uint64))
     assert st1[0] == st0[0] and st1[1] == st0[1]   # no generate / recover reached the engine
     assert st1[4] == st0[4] + 6                     # six errors counted
+
+
+def test_random_blocks_match_oracle(host):
+    """The protocol operations on 150 random blocks beyond the fixtures, both directions, against the
+    oracle (itself pinned to the reference, test_oracle_golden.py / test_oracle_differential.py).
+    - Shapes: k 1-100, r 1-32, equal or variable symbol lengths, all-zero sources.
+    - Inputs: random block numbers, erasures and repair subsets, RLC and XOR.
+    - Patterns that crash the reference (the oracle's DEC_REF_UB) must recover nothing and return 0.
+    Under the sanitizer builds (test_sanitize.py) this drives the adapters' bounds on random shapes."""
+    from oracle_py import DEC_RECOVERED, DEC_REF_UB
+    o = Oracle()
+    rng = np.random.default_rng(0xB10C)
+    for t in range(150):
+        k = int(rng.choice([1, 2, 4, 5, 16, 32, 64, 100, int(rng.integers(1, 101))]))
+        xor = rng.random() < 0.2
+        r = 1 if xor else int(rng.choice([1, 2, 4, 8, 16, int(rng.integers(1, 33))]))
+        L = int(rng.choice([1, 8, 40, 1200, int(rng.integers(1, 1500))]))
+        if rng.random() < 0.3:
+            srcs_full = [rng.integers(0, 256, int(rng.integers(1, L + 1)), dtype=np.uint8) for _ in range(k)]
+        else:
+            srcs_full = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        if rng.random() < 0.15:
+            for j in rng.choice(k, size=int(rng.integers(1, min(k, 3) + 1)), replace=False):
+                srcs_full[j] = np.zeros(len(srcs_full[j]), np.uint8)
+        fbn = int(rng.integers(0, 1 << 24))
+        tag = (t, "xor" if xor else "rlc", k, r, L)
+        ret, reps, fps, _ = host.generate(xor, fbn, srcs_full, r)
+        assert ret == 0, tag
+        if xor:
+            want = [o.xor_encode_block(srcs_full)[1]]
+        else:
+            want = o.rlc_encode_block(fbn, srcs_full, r)[1]
+        assert [x.tobytes() for x in reps] == [x.tobytes() for x in want], tag
+        assert fps == [(fbn << 8) | i for i in range(r)], tag
+        e = int(rng.integers(1, min(k, r + 1) + 1))
+        missing = set(rng.choice(k, size=e, replace=False).tolist())
+        present = set(rng.choice(r, size=int(rng.integers(max(0, e - 1), r + 1)), replace=False).tolist())
+        srcs = [None if j in missing else srcs_full[j] for j in range(k)]
+        reps_in = [reps[i] if i in present else None for i in range(r)]
+        ret, rec, cur = host.recover(xor, fbn, srcs, reps_in, fps)
+        if xor:
+            st, orec = o.xor_decode_block(srcs, reps_in)
+        else:
+            st, orec = o.rlc_decode_block(fbn, srcs, reps_in)
+        if st == DEC_REF_UB:
+            assert ret == 0 and rec == {}, tag
+            continue
+        if xor:  # xor_fec_scheme.c returns non-zero when it recovers nothing; it leaves the count alone (:72)
+            assert (ret == 0) == (st == DEC_RECOVERED) and cur == k - e, tag
+        else:    # the RLC scheme returns 0 and counts what it inserts (rlc_fec_scheme_gf256.c:230)
+            assert ret == 0 and cur == k - e + len(rec), tag
+        assert sorted(rec) == sorted(orec) and all(np.array_equal(rec[j], orec[j]) for j in orec), tag
