@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from oracle_py import Oracle, synth_bytes
-from test_gpu_parity import DEV, _run_decode_batch, bits, masks_from_lists, test_decode_rows_vs_oracle, to_dev
+import test_gpu_parity as parity
+from test_gpu_parity import DEV, _run_decode_batch, bits, masks_from_lists, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -161,4 +162,4 @@ def test_random_decode_rows(eng, oracle, seed):
     r = int(rng.integers(1, 65))
     L = 4 * int(rng.choice([1, 5, 300, 304, int(rng.integers(1, 2251))]))
     nb = max(8, min(int(rng.choice([17, 300, 2000])), (8 << 20) // ((k + r) * L)))  # the body asserts some recovery
-    test_decode_rows_vs_oracle(eng, oracle, k, r, L, nb)
+    parity.test_decode_rows_vs_oracle(eng, oracle, k, r, L, nb)  # through the module: not collected twice
