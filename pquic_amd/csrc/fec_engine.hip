@@ -412,6 +412,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       if (lane == 0) { const int t = perm[i]; perm[i] = perm[mx]; perm[mx] = t; }
       plan_sync<WG>();
     }
+    FEC_STAMP_AT(8);
     // forward elimination without re-pivoting (:54-70): row_pk -= (A[pk][i] / A[pi][i]) row_pi for all
     // kk > i at once; inv(0) = 0 makes every term 0 (the block is then flagged below).  A lane owns a
     // column (of A from i on, then of V) and walks the rows below: the pivot row's entry and its log
@@ -444,6 +445,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
       }
       plan_sync<WG>();
     }
+    FEC_STAMP_AT(9);
     // the reference crashes iff some diagonal entry is zero (candidate walks to -1, :74-77)
     const bool zd = lane < n && A[perm[lane] * empad + lane] == 0;
     bool ub = __any(zd);
@@ -469,6 +471,7 @@ __device__ void plan_wave_block(uint64_t b, int k, int r, uint32_t fbn_base, con
         }
       }
     }
+    FEC_STAMP_AT(10);
     plan_sync<WG>();
     for (int x = lane; x < n * n; x += 64) {
       const int i = x / n, u = x - i * n;
