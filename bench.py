@@ -526,6 +526,10 @@ def batching_legs(dev_index, args):
         d.update(extra)
         return d
 
+    # one short untimed sender run first: the process's one-time costs (the engine's first launches and
+    # host contexts, the allocator's first page faults, thread start-up) land outside the measured legs
+    warm = (C.c_double * 8)()
+    lib.bl_run(dev_index, args.k, args.r, args.symbol, 64, 20000, batch, 2000, 2, 0.0, REG | PER_CONN, warm)
     for name, nconn, reg, runs in (("saturated", 64, REG | PER_CONN, 3), ("saturated_512conn", 512, REG | PER_CONN, 3),
                                    ("saturated_staged", 64, PER_CONN, 3)):
         rc, out, extra = median_of(runs, lambda o: lib.bl_run(dev_index, args.k, args.r, args.symbol, nconn, 200000,
