@@ -856,6 +856,43 @@ def main():
         n_rec = int(ok.sum())
         n_ub = int((status == 2).sum())
 
+    n_enc_checked = 0
+
+    def encode_gate(samples=4096):
+        """Encode-only workloads (configs[3]): the repairs of EVERY pass decode back to the sources.  Per
+        pass, a sample of blocks spread over the pass (its own block numbers, fbn_base_of(g0 + p * nb) + b,
+        stated here independently of the step) loses min(k, r) random sources and is decoded from its
+        repairs; every block the decode recovers must equal the originals, and nearly all must recover (the
+        rest are singular draws or the reference's own crash patterns, flagged per block).  The last pass is
+        checked on the timed step's own repairs first; the earlier passes are re-coded untimed, by the same
+        call on the same resident sources.  The line prints only after every sample matches."""
+        nonlocal n_enc_checked
+        em = min(k, r)
+        g = torch.Generator(device="cpu").manual_seed(0xC0FFEE + rank)
+        rp_s = torch.zeros((samples, 2), dtype=torch.int64, device=dev)
+        rp_s[:, 0] = (1 << r) - 1 if r < 64 else -1
+        for p in reversed(range(passes)):
+            m = min(nb, share - p * nb)
+            fb = fbn_base_of(g0 + p * nb)
+            if p != passes - 1:
+                eng.rlc_encode(src, rep, k, r, L, nblocks=m, fbn_base=fb)
+            n = min(samples, m)
+            idx = torch.randperm(m, generator=g)[:n].sort().values.to(dev)
+            s_src, s_rep = src[idx], rep[idx]
+            fbn = ((idx + fb) & 0xFFFFFF).to(torch.int32)
+            sp_s, miss_s = make_erasures(torch, n, k, em, 0x5A17 + p, dev)
+            w = s_src.clone()
+            rows = (torch.arange(n, device=dev).unsqueeze(1) * k + miss_s.to(dev)).reshape(-1)
+            w.view(n * k, L)[rows] = 0
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            rec = torch.empty((n, 2), dtype=torch.int64, device=dev)
+            eng.rlc_decode(w, s_rep, sp_s, rp_s[:n], st, rec, k, r, L, nblocks=n, fbn=fbn)
+            torch.cuda.synchronize()
+            ok = st == 0
+            assert int(ok.sum()) >= 0.9 * n, f"encode gate, pass {p}: only {int(ok.sum())} of {n} sampled blocks decode"
+            assert bool((w[ok] == s_src[ok]).all()), f"encode gate, pass {p}: decoded sources differ from the originals"
+            n_enc_checked += int(ok.sum())
+
     for _ in range(args.warmup):
         step()
     # the gate reads the last timed step's outputs, after the timed region: run between the warmup and
@@ -880,6 +917,8 @@ def main():
     elapsed = t1 - t0
     if e and not gate_first and args.steps + args.warmup > 0:
         gate()
+    if not e and args.steps + args.warmup > 0:
+        encode_gate()
     # first pass of a step: encode, apply (includes the zero/undetermined rule), plan (its own stream)
     enc_ms, apply_ms = (sum(ev[i].elapsed_time(ev[i + 1]) for ev in evs) / args.steps for i in (0, 2))
     plan_ms = sum(ev[4].elapsed_time(ev[5]) for ev in evs) / args.steps if e else 0.0
@@ -1026,6 +1065,10 @@ def main():
         if e:
             conf["decode_output"] = ("recovered symbols into new rows, packed per block (as fec_recover "
                                      "allocates each recovered symbol anew)")
+        if not e:
+            conf["encode_gate"] = {"passes_checked": passes, "blocks_decoded_back": n_enc_checked,
+                                   "method": "per pass, sampled blocks lose min(k, r) sources and decode back "
+                                             "from the pass's repairs at independently stated block numbers"}
         if passes > 1:
             conf["note"] = (f"a GPU's share ({share} blocks) exceeds HBM: each step codes it in {passes} passes "
                             f"over {nb} resident blocks, block numbers advancing per pass")

@@ -57,11 +57,12 @@ static std::atomic<uint64_t> g_stats[4];
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_ENC_BW,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
-              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_N };
+              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "enc_block_waves", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
-                                           "yield_depth", "yield_gate_us", "yield_streams", "yield_always"};
+                                           "yield_depth", "yield_gate_us", "yield_streams", "yield_always",
+                                           "yield_window_ms"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -112,6 +113,9 @@ static void knobs_default() {
   g_knob[K_YIELD_GATE_US] = 0;
   g_knob[K_YIELD_STREAMS] = 2;
   g_knob[K_YIELD_ALWAYS] = 0;   // A/B: slice even when no hook has run lately
+  // the hooks count as in use for this long after a request (tests lengthen it so that slicing does
+  // not depend on how quickly the call follows the hook)
+  g_knob[K_YIELD_WINDOW_MS] = 100;
 }
 
 static inline int knob(KnobId id) {
@@ -123,8 +127,9 @@ static inline int knob(KnobId id) {
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_window_sc(void) { return knob(K_WINDOW_SC); }
 extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us,
-                                                                        int *streams, int *always) {
+                                                                        int *streams, int *always, int *window_ms) {
   *slice_kb = knob(K_YIELD_SLICE_KB);
+  *window_ms = knob(K_YIELD_WINDOW_MS);
   *depth = knob(K_YIELD_DEPTH);
   *gate_us = knob(K_YIELD_GATE_US);
   *streams = knob(K_YIELD_STREAMS);
@@ -3056,6 +3061,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_DEPTH: return v >= 1 && v <= 16;
     case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
     case K_YIELD_STREAMS: return v >= 1 && v <= 4;
+    case K_YIELD_WINDOW_MS: return v >= 0 && v <= 600000;
     case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs
   }
@@ -3695,7 +3701,10 @@ fecgpu_block_svc_t *fecgpu_block_svc_create(int device) {
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
   bool ok = hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
             hipEventCreateWithFlags(&v->ev, hipEventDisableTiming) == hipSuccess &&
-            hipHostMalloc((void **)&v->mb, sizeof(BlockSvcMailbox), hipHostMallocDefault) == hipSuccess;
+            // fine-grained (coherent) explicitly: the host's compare-and-swap on req.seq (svc_unpost) and
+            // the worker's system-scope claim must be atomic against each other over PCIe
+            hipHostMalloc((void **)&v->mb, sizeof(BlockSvcMailbox), hipHostMallocMapped | hipHostMallocCoherent) ==
+                hipSuccess;
   if (ok) {
     memset(v->mb, 0, sizeof(BlockSvcMailbox));
     ok = hipHostGetDevicePointer((void **)&v->mb_dev, v->mb, 0) == hipSuccess &&

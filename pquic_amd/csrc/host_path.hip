@@ -177,7 +177,7 @@ static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 // 256 blocks (1.58 / 0.47 / 0.30 / 0.17 ms each) the hooks' p99 was 1471 / 417 / 271 / 138 us
 // (profiles/r05_hook_sweep.log; rocprofv3 trace in profiles/r05_hook_trace_summary.txt: the slow calls
 // spend no time in HIP calls and involve no worker launch -- the resident worker's reads wait).  So
-// while the block service is in use (a hook request within the last kYieldWindowUs), a zero-copy launch
+// while the block service is in use (a hook request within the last yield_window_ms, 100 ms), a zero-copy launch
 // is cut into slices of about yield_slice_kb of payload, alternating over yield_streams of the context's
 // streams (consecutive slices overlap, so the cut costs less), at most yield_depth in flight (knobs;
 // defaults and their measurement in fec_engine.hip knobs_default).  Optionally (yield_gate_us) no
@@ -186,9 +186,9 @@ static bool zc_read() { return fecgpu_knob_zc_read() != 0; }
 // the bulk call's time (about 55-80 us of PCIe transfer per 2.25-2.5 MiB slice).
 int fecgpu_svc_hooks_pending(void);                                  // fec_engine.hip (library-internal)
 uint64_t fecgpu_svc_last_request_us(void);                           // fec_engine.hip (library-internal)
-void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us, int *streams, int *always);  // fec_engine.hip
+void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us, int *streams, int *always,
+                       int *window_ms);  // fec_engine.hip
 namespace {
-constexpr uint64_t kYieldWindowUs = 100000;
 std::atomic<uint64_t> g_yield_slices{0}, g_yield_waits{0};
 
 uint64_t mono_us() {
@@ -203,10 +203,10 @@ struct Pacer {
   int n = 0;           // slices launched
   int depth = 4, gate_us = 0, streams = 1;
   Pacer(fecgpu_host_ctx_t *c_, uint64_t nblocks, size_t bytes_per_block) : c(c_) {
-    int kb = 0, always = 0;
-    fecgpu_knob_yield(&kb, &depth, &gate_us, &streams, &always);
+    int kb = 0, always = 0, window_ms = 100;
+    fecgpu_knob_yield(&kb, &depth, &gate_us, &streams, &always, &window_ms);
     const uint64_t last = fecgpu_svc_last_request_us();
-    if (!always && (!last || mono_us() - last > kYieldWindowUs)) return;
+    if (!always && (!last || mono_us() - last > (uint64_t)window_ms * 1000u)) return;
     if (streams > c->ns) streams = c->ns;
     if (!kb || depth > kMaxYieldDepth) return;
     uint64_t per = ((uint64_t)kb << 10) / (bytes_per_block ? bytes_per_block : 1);
@@ -355,8 +355,9 @@ int fecgpu_rlc_encode_rows_host(fecgpu_host_ctx_t *c, const uint64_t *src_rows, 
     for (uint64_t b0 = 0, step = pc.slice ? pc.slice : nblocks; b0 < nblocks; b0 += step) {
       const uint64_t m = nblocks - b0 < step ? nblocks - b0 : step;
       LCHK(pc.before());
-      if ((rc = fecgpu_rlc_encode_rows(ds + b0 * k, dr + b0 * r, m, k, r, L, 0, df ? df + b0 : nullptr,
-                                       pc.stream(s.st))))
+      // without fbn[] block b is block number b (fecgpu.h:21): slice b0 starts at b0, not 0
+      if ((rc = fecgpu_rlc_encode_rows(ds + b0 * k, dr + b0 * r, m, k, r, L, df ? 0u : (uint32_t)(b0 & 0xffffffu),
+                                       df ? df + b0 : nullptr, pc.stream(s.st))))
         break;
       LCHK(pc.after());
     }

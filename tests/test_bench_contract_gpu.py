@@ -65,3 +65,7 @@ def test_bench_line_k32r8():
     _check_common(d, 1, 1, scaling="strong")
     assert d["cpu_baseline"] is None
     assert "k32" in d["roofline"]["kernel"] or "<8," in d["roofline"]["kernel"]
+    # the line printed only after the byte gate: every pass's sampled repairs decoded back to the sources
+    g = d["config"]["encode_gate"]
+    assert g["passes_checked"] == d["config"]["passes_per_step"] >= 1
+    assert g["blocks_decoded_back"] >= 0.9 * 4096 * g["passes_checked"]
