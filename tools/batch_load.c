@@ -161,10 +161,21 @@ static void tsc_init(void) {
     g_tsc_base_us = u3;
     g_tsc_us = (double)(u3 - u0) / (double)(c3 - c0);
 }
+static __thread uint64_t t_stamp_last;  /* per thread: stamps never go back */
 static inline uint64_t stamp_us(void) {
     if (g_tsc_us <= 0) return now_us();
-    /* signed: a core whose TSC reads a little behind the calibrating one gives a small negative offset */
-    return (uint64_t)((int64_t)g_tsc_base_us + (int64_t)((double)(int64_t)(__rdtsc() - g_tsc_base) * g_tsc_us));
+    /* signed: a core whose TSC reads a little behind the calibrating one gives a small negative offset.
+     * A thread that migrates onto such a core would see its stamps go back a little: held at the last
+     * stamp, so a latency (stamp - t_submit) never wraps and the batcher never sees a poll time earlier
+     * than a submit time */
+    uint64_t t = (uint64_t)((int64_t)g_tsc_base_us + (int64_t)((double)(int64_t)(__rdtsc() - g_tsc_base) * g_tsc_us));
+    if (t < t_stamp_last) t = t_stamp_last;
+    t_stamp_last = t;
+    return t;
+}
+static inline uint64_t since_us(uint64_t t0) {
+    const uint64_t t = stamp_us();
+    return t > t0 ? t - t0 : 0;  /* a stamp taken on another thread may lie a little ahead */
 }
 
 /* PC sampler for the sender thread's measured pass (bl_set_sampling; tools/sender_phase_probe.py
@@ -274,7 +285,7 @@ static void on_done(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     slot_t *s = user;
     bl_tally_t *t = s->tally;
     (void)ret;
-    t->lat[t->nlat++] = stamp_us() - s->t_submit;
+    t->lat[t->nlat++] = since_us(s->t_submit);
     for (int i = 0; i < fb->total_repair_symbols; i++) {
         pquic_repair_symbol_t *rs = fb->repair_symbols[i];
         if (rs) { bl_free(s->cnx, rs->data); bl_free(s->cnx, rs); fb->repair_symbols[i] = NULL; }
@@ -287,7 +298,7 @@ static void on_recovered(void *user, pquic_fec_block_t *fb, protoop_arg_t ret) {
     slot_t *s = user;
     bl_tally_t *t = s->tally;
     (void)ret;
-    t->lat[t->nlat++] = stamp_us() - s->t_submit;
+    t->lat[t->nlat++] = since_us(s->t_submit);
     for (int j = 0; j < fb->total_source_symbols; j++) {
         pquic_source_symbol_t *ss = fb->source_symbols[j];
         if (ss && (ss < t->recv_lo || ss >= t->recv_hi)) {  /* inserted by the recover (allocated by the adapter) */
