@@ -197,23 +197,28 @@ protoop_arg_t fec_recover_finish_pre(picoquic_cnx_t *cnx, pquic_fec_block_t *fb,
     const int k = fb->total_source_symbols;
     const uint32_t fbn = fb->fec_block_number & 0xffffffu;
     if (status == FECGPU_BLOCK_REF_UB) FEC_STAT_ADD(ref_ub_blocks, 1);
-    /* one pass in source order, as the reference's :219-236: an unrecovered source's pre-allocation goes
-     * back to the arena when its index is reached, and a recovered source whose pre-allocation had failed
-     * retries its allocation only after every source before it has been handled -- the sources after it
-     * still hold theirs, as the reference's unknowns[] after j are still live at its malloc (:222) */
-    uint64_t nrec = 0;
+    /* first the symbols allocated for sources the reference leaves unrecovered go back to the arena, so
+     * an allocation retried below for a recovered one (its pre-allocation had failed) finds their room,
+     * as the reference's allocations after decoding would (it allocates only what it recovers).  The
+     * reference's own loop (:219-236) frees unknowns[] in source order, so at its malloc for source j
+     * the unknowns after j are still live -- but those are its elimination scratch, which here lives on
+     * the device, not in the plugin arena; a pre-allocation for an unrecovered source has no counterpart
+     * in the reference at all, so it must not take room from a recovered one
+     * (test_batch_recover_frees_unrecovered_preallocations_first: recovered 5 before unrecovered 6) */
     for (int j = 0; j < k; j++) {
         const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
-        if (!got) {
-            if (pre[j]) {
-                g_fec_api.my_free(cnx, pre[j]->data);
-                g_fec_api.my_free(cnx, pre[j]);
-            }
-            continue;
+        if (!got && pre[j]) {
+            g_fec_api.my_free(cnx, pre[j]->data);
+            g_fec_api.my_free(cnx, pre[j]);
         }
+    }
+    uint64_t nrec = 0;
+    for (int j = 0; j < k; j++) {  /* :218-236, in source order as the reference inserts them */
+        const int got = status == FECGPU_BLOCK_RECOVERED && ((rec[j >> 6] >> (j & 63)) & 1);
+        if (!got) continue;  /* (freed above) */
         pquic_source_symbol_t *ss = pre[j];
         if (!ss) {
-            if (!(ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) continue;  /* skipped (:223-226) */
+            if (!(ss = new_source(cnx, (fbn << 8) + (uint8_t)j, maxl))) continue;
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
         } else if ((copy[j >> 6] >> (j & 63)) & 1) {
             memcpy(ss->data, src_rows + (size_t)j * stride, maxl);
