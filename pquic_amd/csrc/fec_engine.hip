@@ -57,12 +57,12 @@ static std::atomic<uint64_t> g_stats[4];
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_ENC_BW,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
-              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_N };
+              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_SVC_RESERVE_CUS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "enc_block_waves", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
                                            "yield_depth", "yield_gate_us", "yield_streams", "yield_always",
-                                           "yield_window_ms"};
+                                           "yield_window_ms", "svc_reserve_cus"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -116,6 +116,10 @@ static void knobs_default() {
   // the hooks count as in use for this long after a request (tests lengthen it so that slicing does
   // not depend on how quickly the call follows the hook)
   g_knob[K_YIELD_WINDOW_MS] = 100;
+  // CUs kept for the block service's worker (0: none): its stream runs on the last n CUs only and the
+  // host-path contexts' streams (the zero-copy bulk calls) on the others; read when a service or a
+  // context is created
+  g_knob[K_SVC_RESERVE_CUS] = 0;
 }
 
 static inline int knob(KnobId id) {
@@ -134,6 +138,22 @@ extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *sli
   *gate_us = knob(K_YIELD_GATE_US);
   *streams = knob(K_YIELD_STREAMS);
   *always = knob(K_YIELD_ALWAYS);
+}
+
+// CU masks of the block-service reservation (knob svc_reserve_cus = n): worker = 1 gives the last n CUs,
+// worker = 0 every other CU.  Returns the mask's words (0: no reservation; the caller makes a plain stream).
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_svc_cu_mask(int device, int worker, uint32_t *mask,
+                                                                        int max_words) {
+  const int n = knob(K_SVC_RESERVE_CUS);
+  int cus = 0;
+  if (n <= 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= n || (cus + 31) / 32 > max_words)
+    return 0;
+  const int words = (cus + 31) / 32;
+  for (int w = 0; w < words; w++) mask[w] = 0;
+  for (int c = 0; c < cus; c++)
+    if ((c >= cus - n) == (worker != 0)) mask[c >> 5] |= 1u << (c & 31);
+  return words;
 }
 
 static int set_err(int code, const char *fmt, const char *what) {
@@ -3062,6 +3082,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
     case K_YIELD_STREAMS: return v >= 1 && v <= 4;
     case K_YIELD_WINDOW_MS: return v >= 0 && v <= 600000;
+    case K_SVC_RESERVE_CUS: return v >= 0 && v <= 128;
     case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs
   }
@@ -3699,7 +3720,10 @@ fecgpu_block_svc_t *fecgpu_block_svc_create(int device) {
   v->device = device;
   int prio_least = 0, prio_greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-  bool ok = hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
+  uint32_t cu_mask[16];
+  const int mw = fecgpu_svc_cu_mask(device, 1, cu_mask, 16);
+  bool ok = (mw ? hipExtStreamCreateWithCUMask(&v->stream, (uint32_t)mw, cu_mask)
+                : hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest)) == hipSuccess &&
             hipEventCreateWithFlags(&v->ev, hipEventDisableTiming) == hipSuccess &&
             // fine-grained (coherent) explicitly: the host's compare-and-swap on req.seq (svc_unpost) and
             // the worker's system-scope claim must be atomic against each other over PCIe

@@ -197,6 +197,35 @@ def v(n):
     return f"v{n}"
 
 
+def inline_cases(RT, tl, th, acc_base, c):
+    """FEC_GEN_INLINE_CASES=c (timing probes only, results are garbage): RT case bodies of the fixed
+    coefficient c inline, no jump.  FEC_GEN_INLINE_MODE: 'plain' (absolute accumulators), 'salu' (plus the
+    three SALU of a chain tail per case, on dead SGPRs), 'idx' (GPR-index mode on, M0 advanced per case,
+    as the chains run): what the dispatch's jumps, tail SALU and index mode each cost."""
+    mode = os.environ.get("FEC_GEN_INLINE_MODE", "plain")
+    out = []
+    if mode == "idx":
+        out.append(f"s_set_gpr_idx_on {acc_base}, gpr_idx(SRC0,DST)")
+    for i in range(RT):
+        for o, (nl, nh) in enumerate(case_rows(c)):
+            s = SIG[o] if mode == "idx" else acc_base + 8 * i + SIG[o]
+            if nl and nh:
+                out.append(f"v_bitop3_b32 v{s}, v{s}, {v(tl[nl])}, {v(th[nh])} bitop3:0x96")
+            elif nl:
+                out.append(f"v_xor_b32 v{s}, v{s}, {v(tl[nl])}")
+            elif nh:
+                out.append(f"v_xor_b32 v{s}, v{s}, {v(th[nh])}")
+        if mode == "idx":
+            out.append("s_add_u32 m0, m0, 8")
+        elif mode == "salu":
+            out += [f"s_add_u32 s{S_TGT + 1}, s{S_TGT + 1}, 8",
+                    f"s_lshr_b64 s[{S_CQ}:{S_CQ + 1}], s[{S_CQ}:{S_CQ + 1}], 16",
+                    f"s_pack_ll_b32_b16 s{S_TGT}, s{S_CQ}, s{S_TABHI}"]
+    if mode == "idx":
+        out.append("s_set_gpr_idx_off")
+    return out
+
+
 def emit_table(sym="fec_bs_case_table", tl=None, th=None):
     tl = tl or TL
     th = th or TH
@@ -555,6 +584,8 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
             a(f".Lpf{b}_%=:")
             ool += [f".Lnopf{b}_%=:", f"s_mov_b32 s{S_T2}, 0", "s_waitcnt vmcnt(0)", f"s_branch .Lpf{b}_%="]
             tr = transpose64([DATA_BASE + 8 * b + SIG[w] for w in range(8)], PL, *t64_scratch(T_BASE))
+            if os.environ.get("FEC_GEN_PROBE_NOTRANS"):  # timing probe only (garbage): no forward transpose
+                tr = []
             if early_co:  # the coefficient fields (into CO = TMP, untouched by transpose64) go out first
                 a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
                 a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
@@ -588,7 +619,8 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
             a(f"{dsr} {regrange(CO[0], ndw)}, v{COPTR}")
             if csb <= 16:
                 a(f"v_add_u32 v{COPTR}, {csb}, v{COPTR}")
-        L.extend(combos())
+        if not os.environ.get("FEC_GEN_PROBE_NOCOMBO"):  # timing probe only (garbage) when set: no combos
+            L.extend(combos())
         if AB:
             # QA = s[S_C0:S_C1], QB = s[S_C2:S_C3] (rows of 4 fields: one dword each, the high
             # dwords stay 0); one chain per 8 fields, entered at QA's first field
@@ -618,7 +650,13 @@ def body(mode: str, RT: int, VEC: int, P: int, sc: bool = False):
         if csb == 32 and not constco and not AB:  # second half of the offsets lands while the first two chains run
             a(f"ds_read_b128 {regrange(CO[0], 4)}, v{COPTR} offset:16")
             a(f"v_add_u32 v{COPTR}, 32, v{COPTR}")
-        for ch in range(0 if AB else nch):
+        # FEC_GEN_INLINE_CASES=c (timing probe only, results are garbage): every chain replaced by the
+        # case bodies of the fixed coefficient c, inline on absolute accumulator registers -- no jump,
+        # no chain tail, no GPR-index mode: what the case dispatch itself costs
+        inline_c = os.environ.get("FEC_GEN_INLINE_CASES")
+        if inline_c and not AB:
+            L.extend(inline_cases(RT, TL, TH, acc_base, int(inline_c, 0)))
+        for ch in range(0 if AB or inline_c else nch):
             if ch == 2:  # RT = 16: offsets 8..15 (no VALU may run in GPR-index mode)
                 a("s_set_gpr_idx_off")
                 if not constco:
@@ -975,7 +1013,13 @@ def body2(mode: str, RT: int, D: int, NDMA: int):
         else:
             L.extend(transpose_inplace(PL, XT))
         L.extend(combos(TLm, THm))
-        if NT >= 4:
+        inline2 = os.environ.get("FEC_GEN_INLINE_CASES")  # timing probe only (body(): no dispatch at all)
+        if inline2:
+            a("s_waitcnt lgkmcnt(0)")
+            L.extend(inline_cases(RT, TLm, THm, acc_base, int(inline2, 0)))
+            if NT < 4 and not const2:
+                a(f"s_add_u32 s{S_COPTR}, s{S_COPTR}, {csb}")
+        elif NT >= 4:
             CO = TMPm[:ndw]
             a("s_waitcnt lgkmcnt(0)")
             for w in range(ndw):

@@ -56,6 +56,8 @@ struct fecgpu_host_ctx {
 
 extern "C" {
 
+int fecgpu_svc_cu_mask(int device, int worker, uint32_t *mask, int max_words);  // fec_engine.hip (internal)
+
 fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk_bytes) {
   if (fecgpu_init(device) != FECGPU_OK) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -63,8 +65,11 @@ fecgpu_host_ctx_t *fecgpu_host_ctx_create(int device, int nstreams, size_t chunk
   c->device = device;
   c->ns = nstreams < 1 ? 1 : (nstreams > kMaxStreams ? kMaxStreams : nstreams);
   c->chunk_bytes = chunk_bytes ? chunk_bytes : (64u << 20);
+  uint32_t cu_mask[16];
+  const int mw = fecgpu_svc_cu_mask(device, 0, cu_mask, 16);  // off the block service's CUs (if reserved)
   for (int i = 0; i < c->ns; i++) {
-    if (hipStreamCreateWithFlags(&c->slot[i].st, hipStreamNonBlocking) != hipSuccess) {
+    if ((mw ? hipExtStreamCreateWithCUMask(&c->slot[i].st, (uint32_t)mw, cu_mask)
+            : hipStreamCreateWithFlags(&c->slot[i].st, hipStreamNonBlocking)) != hipSuccess) {
       fecgpu_host_ctx_destroy(c);
       return nullptr;
     }
