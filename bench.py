@@ -497,6 +497,8 @@ def batching_legs(dev_index, args):
     lib.bl_run_senders.argtypes = [C.c_int] + lib.bl_run.argtypes[:9] + [C.c_int, D]
     lib.bl_set_inflight.argtypes = [C.c_int]
     lib.bl_last_rows.argtypes = [D]
+    lib.bl_last_latency.argtypes = [D]
+    lib.bl_last_jobs.argtypes = [D]
     REG, PER_CONN = 1, 2
     batch, inflight = 2048, 3
     lib.bl_set_inflight(inflight)
@@ -506,16 +508,20 @@ def batching_legs(dev_index, args):
         """host-side rates on a shared CPU slice vary from run to run: the run with the median rate"""
         res = []
         for _ in range(runs):
-            out, rows = (C.c_double * 8)(), (C.c_double * 2)()
+            out, rows, q, jb = (C.c_double * 8)(), (C.c_double * 2)(), (C.c_double * 8)(), (C.c_double * 2)()
             rc = fn(out)
             if rc:
                 return rc, None, None
             lib.bl_last_rows(rows)
-            res.append((list(out), list(rows)))
+            lib.bl_last_latency(q)
+            lib.bl_last_jobs(jb)
+            res.append((list(out), list(rows), list(q), list(jb)))
         res.sort(key=lambda x: x[0][0])
-        out, rows = res[len(res) // 2]
-        return 0, out, {"runs_payload_GiB_s": [round(o[0][0], 2) for o in res], "rows_in_place": int(rows[0]),
-                        "rows_staged": int(rows[1])}
+        out, rows, q, jb = res[len(res) // 2]
+        return 0, out, {"runs_payload_GiB_s": [round(o[0][0], 2) for o in res],
+                        "runs_latency_us_p99": [o[0][2] for o in res], "rows_in_place": int(rows[0]),
+                        "rows_staged": int(rows[1]), "latency_us_p90": q[1], "latency_us_p99_9": q[4],
+                        "jobs_allocated_on_sender_thread": int(jb[0])}
 
     def leg(out, extra, **kw):
         d = {"k": args.k, "r": args.r, "L": args.symbol, "batch_blocks": batch, "batches_in_flight": inflight,

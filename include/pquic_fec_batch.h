@@ -60,6 +60,8 @@ typedef struct {
     uint64_t complete_us;           /* caller-thread time in completions (poll / drain) */
     uint64_t rows_in_place;         /* symbol rows the kernels read or wrote where they lie (registered arenas) */
     uint64_t rows_staged;           /* symbol rows copied through the page-locked staging rows instead */
+    uint64_t jobs_allocated;        /* batch jobs (page-locked queue buffers) allocated on the caller's thread */
+    uint64_t job_alloc_us;          /* caller-thread time in those allocations */
 } pquic_fec_batch_stats_t;
 
 /* NULL on failure (bad configuration, no device, out of pinned memory). */

@@ -123,6 +123,13 @@ struct pquic_fec_batcher {
     job_t *completing;             /* finished job whose completions a bounded poll left part-done */
     uint32_t completing_i;         /* its next entry */
     pquic_fec_batch_stats_t stats;
+    /* the provisioner (prov_main): one request at a time, under mu; the spares it made, under mu */
+    pthread_t prov;
+    int prov_started, prov_want, prov_op, prov_xor;
+    uint32_t prov_k, prov_r;
+    pthread_cond_t cv_prov;
+    job_t *spares;
+    uint64_t stats_spares;         /* spares made (under mu) */
     uint64_t next_seq;             /* caller thread: sequence number of the next flushed job */
     uint64_t collect_seq;          /* caller thread: the job whose completions come next */
     /* registered arenas, sorted by base and disjoint; stagers look rows up under the read lock (one
@@ -236,44 +243,41 @@ static void job_free(job_t *j) {
     free(j);
 }
 
-/* A job for (op, scheme, k, r), from the free list when one is big enough. */
+static uint64_t mono_us(void);
 static uint32_t window_stride(const pquic_fec_batcher_t *b) { return (b->stride + 15u) & ~15u; }
 
-static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
+/* A job's page-locked queue buffers for `cap` blocks of sb / rb bytes of rows (NULL on failure). */
+static job_t *job_alloc(uint32_t cap, size_t sb, size_t rb) {
+    job_t *j = calloc(1, sizeof *j);
+    if (!j) return NULL;
+    j->src_bytes = sb;
+    j->rep_bytes = rb;
+    j->src = fecgpu_host_alloc(sb);
+    j->rep = fecgpu_host_alloc(rb ? rb : 4);
+    j->st = fecgpu_host_alloc(cap);
+    j->fbn = fecgpu_host_alloc((size_t)cap * 4);
+    j->sp = fecgpu_host_alloc((size_t)cap * 48);  /* sp | rp | rec, 2 words each per block */
+    j->ent = calloc(cap, sizeof *j->ent);
+    if (!j->src || !j->rep || !j->st || !j->fbn || !j->sp || !j->ent) {
+        job_free(j);
+        return NULL;
+    }
+    return j;
+}
+
+/* Grows what a job needs for (op, scheme, k, r) beyond its row buffers -- seeds, gather tables, window tables,
+ * repair pointers -- and sets it up for that use.  Touches nothing of the batcher but its configuration and
+ * the heap count, so the provisioner thread may run it on a job no one else sees.  Returns 0, or -1 when an
+ * allocation failed (the job stays valid for another use). */
+static int job_prepare(pquic_fec_batcher_t *b, job_t *j, int op, int xor_scheme, uint32_t k, uint32_t r) {
     const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
     const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
-    job_t **pp = &b->free_jobs;
-    for (; *pp; pp = &(*pp)->next)
-        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb) break;
-    job_t *j = *pp;
-    if (j) {
-        *pp = j->next;
-    } else {
-        j = calloc(1, sizeof *j);
-        if (!j) return NULL;
-        j->src_bytes = sb;
-        j->rep_bytes = rb;
-        j->src = fecgpu_host_alloc(sb);
-        j->rep = fecgpu_host_alloc(rb ? rb : 4);
-        j->st = fecgpu_host_alloc(cap);
-        j->fbn = fecgpu_host_alloc((size_t)cap * 4);
-        j->sp = fecgpu_host_alloc((size_t)cap * 48);  /* sp | rp | rec, 2 words each per block */
-        j->ent = calloc(cap, sizeof *j->ent);
-        if (!j->src || !j->rep || !j->st || !j->fbn || !j->sp || !j->ent) {
-            job_free(j);
-            return NULL;
-        }
-    }
     /* recover only: the repairs' FPID seeds, [cap][r] (grown on reuse like the repair table) */
     const size_t eb = (size_t)cap * (r ? r : 1) * 4;
     if (op == OP_RECOVER && j->seed_bytes < eb) {
         fecgpu_host_free(j->seeds);
         j->seed_bytes = 0;
-        if (!(j->seeds = fecgpu_host_alloc(eb))) {
-            j->next = b->free_jobs;
-            b->free_jobs = j;
-            return NULL;
-        }
+        if (!(j->seeds = fecgpu_host_alloc(eb))) return -1;
         j->seed_bytes = eb;
     }
     /* gather tables (RLC generate or recover with a registered heap): grown on reuse like the repair table */
@@ -311,20 +315,12 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
                 j->rowsym_cap = (size_t)cap * k;
             }
         }
-        if (!j->wrow || !j->order || j->rowsym_cap < (size_t)cap * k) {
-            j->next = b->free_jobs;
-            b->free_jobs = j;
-            return NULL;
-        }
+        if (!j->wrow || !j->order || j->rowsym_cap < (size_t)cap * k) return -1;
     }
     j->nrows = 0;
     if (GENERATES(op) && j->reps_cap < (size_t)cap * r) {
         pquic_repair_symbol_t **nr = realloc(j->reps, sizeof *nr * (size_t)cap * r);
-        if (!nr) {
-            j->next = b->free_jobs;
-            b->free_jobs = j;
-            return NULL;
-        }
+        if (!nr) return -1;
         j->reps = nr;
         j->reps_cap = (size_t)cap * r;
     }
@@ -341,6 +337,93 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
     j->rc = 0;
     j->post = 0;
     j->next_chunk = j->chunks_done = 0;
+    return 0;
+}
+
+/* Unlinks and returns the first job of *pp with rows for at least sb / rb bytes, or NULL. */
+static job_t *take_fit(job_t **pp, size_t sb, size_t rb) {
+    for (; *pp; pp = &(*pp)->next)
+        if ((*pp)->src_bytes >= sb && (*pp)->rep_bytes >= rb) {
+            job_t *j = *pp;
+            *pp = j->next;
+            j->next = NULL;
+            return j;
+        }
+    return NULL;
+}
+
+static int has_fit(const job_t *j, size_t sb, size_t rb) {
+    for (; j; j = j->next)
+        if (j->src_bytes >= sb && j->rep_bytes >= rb) return 1;
+    return 0;
+}
+
+/* Spare jobs.  Allocating a job's page-locked buffers takes milliseconds (6.3 ms for a 2048-block k16 r4 job,
+ * profiles/r06_conn512_probe.log), and on the caller's thread it stalls every block queued meanwhile: the run
+ * whose pipeline went one job deeper than ever before had its p99 at 8.7 ms against 2.3-3.8 in the others.  So
+ * whenever the caller takes the last job that fits a shape, the provisioner thread allocates the next one
+ * (same shape, prepared for the same use) and leaves it in b->spares, where job_get finds it. */
+static void *prov_main(void *arg) {
+    pquic_fec_batcher_t *b = arg;
+    pthread_mutex_lock(&b->mu);
+    for (;;) {
+        while (!b->stop && !b->prov_want) pthread_cond_wait(&b->cv_prov, &b->mu);
+        if (b->stop) break;
+        const int op = b->prov_op, xs = b->prov_xor;
+        const uint32_t k = b->prov_k, r = b->prov_r;
+        pthread_mutex_unlock(&b->mu);
+        const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
+        job_t *j = job_alloc(cap, (size_t)cap * k * S, (size_t)cap * r * S);
+        if (j && job_prepare(b, j, op, xs, k, r)) {
+            job_free(j);
+            j = NULL;
+        }
+        pthread_mutex_lock(&b->mu);
+        if (j) {
+            j->next = b->spares;
+            b->spares = j;
+            b->stats_spares++;
+        }
+        b->prov_want = 0;
+    }
+    pthread_mutex_unlock(&b->mu);
+    return NULL;
+}
+
+/* A job for (op, scheme, k, r): from the free list, else a spare, else allocated here (counted). */
+static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
+    const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
+    const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
+    job_t *j = take_fit(&b->free_jobs, sb, rb);
+    if (!j && b->prov_started) {
+        pthread_mutex_lock(&b->mu);
+        j = take_fit(&b->spares, sb, rb);
+        pthread_mutex_unlock(&b->mu);
+    }
+    if (!j) {
+        const uint64_t t_alloc = mono_us();
+        if (!(j = job_alloc(cap, sb, rb))) return NULL;
+        b->stats.jobs_allocated++;
+        b->stats.job_alloc_us += mono_us() - t_alloc;
+    }
+    if (job_prepare(b, j, op, xor_scheme, k, r)) {
+        j->next = b->free_jobs;
+        b->free_jobs = j;
+        return NULL;
+    }
+    /* the last job of this shape is in use: have the next one made off this thread */
+    if (b->prov_started && !has_fit(b->free_jobs, sb, rb)) {
+        pthread_mutex_lock(&b->mu);
+        if (!b->prov_want && !has_fit(b->spares, sb, rb)) {
+            b->prov_want = 1;
+            b->prov_op = op;
+            b->prov_xor = xor_scheme;
+            b->prov_k = k;
+            b->prov_r = r;
+            pthread_cond_signal(&b->cv_prov);
+        }
+        pthread_mutex_unlock(&b->mu);
+    }
     return j;
 }
 
@@ -739,6 +822,7 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
     pthread_cond_init(&b->cv_todo, NULL);
     pthread_cond_init(&b->cv_staged, NULL);
     pthread_cond_init(&b->cv_done, NULL);
+    pthread_cond_init(&b->cv_prov, NULL);
     /* copy threads: half the CPUs of the process's share (the caller and the engine thread keep the
      * rest), at least 2; PQUIC_FEC_BATCH_STAGERS overrides, read once per batcher */
     const char *ns = getenv("PQUIC_FEC_BATCH_STAGERS");
@@ -771,12 +855,15 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
         pthread_cond_destroy(&b->cv_todo);
         pthread_cond_destroy(&b->cv_staged);
         pthread_cond_destroy(&b->cv_done);
+        pthread_cond_destroy(&b->cv_prov);
         pthread_mutex_destroy(&b->mu);
         pthread_rwlock_destroy(&b->heaps_mu);
         for (int e = 0; e < b->nengines; e++) fecgpu_host_ctx_destroy(b->ctx[e]);
         free(b);
         return NULL;
     }
+    /* the provisioner (spare jobs); without it every job is allocated on the caller's thread */
+    b->prov_started = pthread_create(&b->prov, NULL, prov_main, b) == 0;
     return b;
 }
 
@@ -1098,11 +1185,18 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
     b->stop = 1;
     pthread_cond_broadcast(&b->cv_todo);
     pthread_mutex_unlock(&b->mu);
+    pthread_cond_broadcast(&b->cv_prov);
     for (int i = 0; i < b->nstagers; i++) pthread_join(b->stager[i], NULL);
     for (int e = 0; e < b->nengines; e++) pthread_join(b->worker[e], NULL);
+    if (b->prov_started) pthread_join(b->prov, NULL);
     while (b->free_jobs) {
         job_t *j = b->free_jobs;
         b->free_jobs = j->next;
+        job_free(j);
+    }
+    while (b->spares) {
+        job_t *j = b->spares;
+        b->spares = j->next;
         job_free(j);
     }
     for (int i = 0; i < b->nheaps; i++) fecgpu_host_unregister((void *)b->heaps[i].base);
@@ -1113,5 +1207,6 @@ void pquic_fec_batcher_destroy(pquic_fec_batcher_t *b) {
     pthread_cond_destroy(&b->cv_todo);
     pthread_cond_destroy(&b->cv_staged);
     pthread_cond_destroy(&b->cv_done);
+    pthread_cond_destroy(&b->cv_prov);
     free(b);
 }

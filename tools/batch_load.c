@@ -277,6 +277,8 @@ double bl_clock_cost(void) {
 
 static pthread_barrier_t *g_sync;  /* bl_run_senders: the senders' pass barrier */
 static __thread uint64_t g_span[2];  /* the last measured pass: start, end (us) */
+static __thread double g_jobs[2];   /* the last measured pass: batch jobs allocated, caller us in those allocations */
+static __thread double g_lat_q[8];  /* the last measured pass's latency: p50 p90 p95 p99 p99.9 max mean, count */
 static __thread double g_rows[2];   /* the last bl_run's measured pass: rows in place, rows staged */
 static __thread double g_phases[6];  /* the last bl_run's measured pass: engine, stager, completion thread-us; wall us;
                              * caller us waiting for a free slot; caller us inside pquic_fec_batch_generate */
@@ -592,6 +594,15 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     pquic_fec_batch_get_stats(b, &st);
     pquic_fec_batcher_destroy(b);  /* unregisters the arenas */
     qsort(g_lat, g_nlat, sizeof *g_lat, cmp_u64);
+    {
+        static const double qs[6] = {0.5, 0.9, 0.95, 0.99, 0.999, 1.0};
+        for (int i = 0; i < 6; i++)
+            g_lat_q[i] = g_nlat ? (double)g_lat[qs[i] >= 1.0 ? g_nlat - 1 : (long)(g_nlat * qs[i])] : 0;
+        double sum = 0;
+        for (long i = 0; i < g_nlat; i++) sum += (double)g_lat[i];
+        g_lat_q[6] = g_nlat ? sum / g_nlat : 0;
+        g_lat_q[7] = (double)g_nlat;
+    }
     out[0] = nblocks * bytes_per_block / wall / 1073741824.0;
     out[1] = g_nlat ? (double)g_lat[g_nlat / 2] : 0;
     out[2] = g_nlat ? (double)g_lat[(long)(g_nlat * 0.99)] : 0;
@@ -608,6 +619,8 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     g_phases[5] = (double)t_submit;
     g_rows[0] = (double)(st.rows_in_place - st0.rows_in_place);
     g_rows[1] = (double)(st.rows_staged - st0.rows_staged);
+    g_jobs[0] = (double)(st.jobs_allocated - st0.jobs_allocated);
+    g_jobs[1] = (double)(st.job_alloc_us - st0.job_alloc_us);
     free(slots); free(ss); free(rsy); free(g_lat); free(cnx); free(pool);
     g_lat = NULL;
     if (pinned) sched_setaffinity(0, sizeof saved, &saved);
@@ -885,6 +898,17 @@ int bl_hook_latency_loaded(int device, int bulk_blocks, long ncalls, double out[
  * us waiting for a free block slot (completions inside it included), [5] caller us in submissions. */
 void bl_last_phases(double out[6]) {
     for (int i = 0; i < 6; i++) out[i] = g_phases[i];
+}
+
+/* The last bl_run's measured pass: batch jobs the batcher allocated on the sender's thread, and the us spent. */
+void bl_last_jobs(double out[2]) {
+    out[0] = g_jobs[0];
+    out[1] = g_jobs[1];
+}
+
+/* The last bl_run's measured pass, block latency (us): p50, p90, p95, p99, p99.9, max, mean; [7] blocks. */
+void bl_last_latency(double out[8]) {
+    for (int i = 0; i < 8; i++) out[i] = g_lat_q[i];
 }
 
 /* Rows the last bl_run's measured pass coded where they lie ([0]) and through the staging rows ([1]). */
