@@ -862,8 +862,10 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
         free(b);
         return NULL;
     }
-    /* the provisioner (spare jobs); without it every job is allocated on the caller's thread */
-    b->prov_started = pthread_create(&b->prov, NULL, prov_main, b) == 0;
+    /* the provisioner (spare jobs); without it every job is allocated on the caller's thread.
+     * PQUIC_FEC_BATCH_SPARES=0 turns it off (A/B), read once per batcher like the thread counts */
+    const char *sp = getenv("PQUIC_FEC_BATCH_SPARES");
+    b->prov_started = !(sp && atoi(sp) == 0) && pthread_create(&b->prov, NULL, prov_main, b) == 0;
     return b;
 }
 
