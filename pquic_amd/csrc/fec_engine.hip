@@ -57,12 +57,12 @@ static std::atomic<uint64_t> g_stats[4];
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_ENC_BW,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
-              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_SVC_RESERVE_CUS, K_N };
+              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_SVC_RESERVE_CUS, K_HOST_ALLOC, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "enc_block_waves", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
                                            "yield_depth", "yield_gate_us", "yield_streams", "yield_always",
-                                           "yield_window_ms", "svc_reserve_cus"};
+                                           "yield_window_ms", "svc_reserve_cus", "host_alloc"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -120,6 +120,9 @@ static void knobs_default() {
   // host-path contexts' streams (the zero-copy bulk calls) on the others; read when a service or a
   // context is created
   g_knob[K_SVC_RESERVE_CUS] = 0;
+  // fecgpu_host_alloc's page-locked memory: 0 the runtime's default, 1 fine-grained (coherent), 2
+  // coarse-grained (non-coherent), mapped either way (A/B of how zero-copy kernels' host lines sit in L2)
+  g_knob[K_HOST_ALLOC] = 0;
 }
 
 static inline int knob(KnobId id) {
@@ -130,6 +133,7 @@ static inline int knob(KnobId id) {
 // host_path.hip reads the zero-copy knob through this (library-internal)
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_zc_read(void) { return knob(K_ZC_READ); }
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_window_sc(void) { return knob(K_WINDOW_SC); }
+extern "C" __attribute__((visibility("hidden"))) int fecgpu_knob_host_alloc(void) { return knob(K_HOST_ALLOC); }
 extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *slice_kb, int *depth, int *gate_us,
                                                                         int *streams, int *always, int *window_ms) {
   *slice_kb = knob(K_YIELD_SLICE_KB);
@@ -3083,6 +3087,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_STREAMS: return v >= 1 && v <= 4;
     case K_YIELD_WINDOW_MS: return v >= 0 && v <= 600000;
     case K_SVC_RESERVE_CUS: return v >= 0 && v <= 128;
+    case K_HOST_ALLOC: return v >= 0 && v <= 2;
     case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs
   }

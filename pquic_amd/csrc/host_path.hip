@@ -614,9 +614,14 @@ int fecgpu_xor_decode_host(fecgpu_host_ctx_t *c, void *src, const void *rep, uin
 }  // extern "C"
 
 extern "C" {
+int fecgpu_knob_host_alloc(void);  // fec_engine.hip (library-internal)
+
 void *fecgpu_host_alloc(size_t bytes) {
   void *p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  const int mode = fecgpu_knob_host_alloc();
+  const unsigned flags = mode == 1 ? hipHostMallocMapped | hipHostMallocCoherent
+                       : mode == 2 ? hipHostMallocMapped | hipHostMallocNonCoherent : hipHostMallocDefault;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, flags) != hipSuccess) return nullptr;
   hipPointerAttribute_t pa;
   if (hipPointerGetAttributes(&pa, p) == hipSuccess && pa.devicePointer)
     pinned_add((uintptr_t)p, bytes ? bytes : 1, (uint8_t *)pa.devicePointer, false);
