@@ -2348,6 +2348,13 @@ template <> struct Bs2Depth<4> { static constexpr int enc = FEC_BS2_D(ENC, 4), d
 #else
 #define FEC_BS2_HAS_RT4 0
 #endif
+// 8-repair ring encode bodies (FEC_GEN2_TILES=8,16 builds; knob ring = 8; A/B experiments)
+#ifdef FEC_BS2_D_ENC_RT8
+#define FEC_BS2_HAS_RT8 1
+template <> struct Bs2Depth<8> { static constexpr int enc = FEC_BS2_D(ENC, 8), dec = FEC_BS2_D(DEC, 8); };
+#else
+#define FEC_BS2_HAS_RT8 0
+#endif
 using Bs2Depth16 = Bs2Depth<16>;
 
 // Lane geometry of one chunk of cb bytes (cb >= 16) as 16-B pieces, the last pulled back to end at cb.
@@ -2399,9 +2406,16 @@ __device__ __forceinline__ int lane_fresh() {
 #define BS2_CALL_DEC(RT, ND) \
   bs2_dec_r##RT##_d##ND(ia, oa, nsrc, (uint32_t)k, ca, ring, BS2_LANE_ARGS)
 
+template <int RT>
 __device__ __forceinline__ void bs2_enc_call(bool two, uint64_t sp, uint64_t rpp, int L, uint32_t rslo, uint32_t rshi,
                                              uint64_t sdl, uint64_t ll, int rt, uint32_t nsrc, int k, uint32_t ca,
                                              uint32_t ring, const Bs2Lanes &ln) {
+#if FEC_BS2_HAS_RT8
+  if constexpr (RT == 8) {
+    if (two) BS2_CALL_ENC(8, 2); else BS2_CALL_ENC(8, 1);
+    return;
+  }
+#endif
   if (two) BS2_CALL_ENC(16, 2); else BS2_CALL_ENC(16, 1);
 }
 
@@ -2436,7 +2450,8 @@ template <int RT, bool CW>
 #ifndef FEC_BS2_RT16_WAVES
 #define FEC_BS2_RT16_WAVES 3
 #endif
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? FEC_BS2_RT16_WAVES : 1)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT == 16 && FEC_BS2_BASE <= 8 ? FEC_BS2_RT16_WAVES
+                                                                    : RT == 8 ? 4 : 1)))
 void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep,
                                                         uint64_t nblocks, int k, int r, int L, int nchunks,
                                                         int chunk_bytes, uint32_t fbn_base, const uint32_t *fbn,
@@ -2446,7 +2461,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int CSB = FEC_BS_COEF_ROW_BYTES(RT);
-  constexpr int D = Bs2Depth16::enc;
+  constexpr int D = Bs2Depth<RT>::enc;
   const uint32_t coef_bytes = pad16((uint32_t)(G * k * CSB));
   // CW: one set of coefficient rows for the group, then a ring per wave; otherwise rows + ring per wave
   uint8_t *lds = CW ? lds_all : lds_all + (size_t)wave * (coef_bytes + D * slotb);
@@ -2493,7 +2508,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
         const uint64_t b = b0 + g * bstep;
         const uint64_t sp = (uint64_t)(uintptr_t)(src + b * sbs + c0);
         const uint64_t rpp = (uint64_t)(uintptr_t)(rep + (b * (uint64_t)r + r0) * (uint64_t)L + c0);
-        bs2_enc_call(ln.npieces > 64, sp, rpp, L, 0u, 0u, (uint64_t)L, (uint64_t)L, rt, (uint32_t)k, k,
+        bs2_enc_call<RT>(ln.npieces > 64, sp, rpp, L, 0u, 0u, (uint64_t)L, (uint64_t)L, rt, (uint32_t)k, k,
                      lds_addr(lds + (size_t)g * k * CSB), ring, ln);
       }
     } else {
@@ -2507,7 +2522,7 @@ void k_rlc_encode_bs2(const uint8_t *__restrict__ src, uint8_t *__restrict__ rep
         const uint64_t sdelta = bstep * sbs - (uint64_t)k * L;
         const uint32_t rslo = (uint32_t)rstep, rshi = (uint32_t)(rstep >> 32);
         const uint64_t sdl = sdelta + L, ll = (uint64_t)L;
-        bs2_enc_call(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
+        bs2_enc_call<RT>(ln.npieces > 64, sp, rpp, L, rslo, rshi, sdl, ll, rt, (uint32_t)(ng * k), k, lds_addr(lds), ring,
                      ln);
       }
     }
@@ -2690,7 +2705,7 @@ static void launch_encode_bs2(const uint8_t *src, uint8_t *rep, uint64_t nb, int
                               uint32_t fbn_base, const uint32_t *fbn, int r0, int W, uint64_t sbs, uint32_t fbn_step,
                               hipStream_t s) {
   const uint32_t slotb = bs2_slot_bytes(c.chunk_bytes);
-  const size_t ring_bytes = (size_t)Bs2Depth16::enc * slotb;
+  const size_t ring_bytes = (size_t)Bs2Depth<RT>::enc * slotb;
   const int CSB = FEC_BS_COEF_ROW_BYTES(RT);
   if (int G = (W == 1 && c.nchunks > 1) ? cw_group(RT, k, CSB, 0, ring_bytes, nb) : 0) {
     if (sbs != (uint64_t)k * L) G = 1;  // overlapping blocks (windows): one per group
@@ -2733,6 +2748,9 @@ static void launch_recover_bs2(uint8_t *src, const uint8_t *rep, uint64_t nb, in
 static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
   if (knob(K_RING) == 0 || cfg.vec != 16) return false;
   if (rt == 16) return (int)k >= (enc ? Bs2Depth16::enc : Bs2Depth16::dec);
+#if FEC_BS2_HAS_RT8
+  if (rt == 8 && enc && knob(K_RING) == 8) return (int)k >= Bs2Depth<8>::enc;
+#endif
 #if FEC_BS2_HAS_RT4
   if (rt == 4 && !enc && knob(K_RING) == 4) return (int)k >= Bs2Depth<4>::dec;
 #endif
@@ -2745,7 +2763,12 @@ static bool use_ring(int rt, uint32_t k, const BsCfg &cfg, bool enc) {
 #else
 #define FEC_BS2_DISPATCH_DEC(FN, ...) FN<16>(__VA_ARGS__);
 #endif
+#if FEC_BS2_HAS_RT8
+#define FEC_BS2_DISPATCH(FN, ...) \
+  if (rt == 8) FN<8>(__VA_ARGS__); else FN<16>(__VA_ARGS__);
+#else
 #define FEC_BS2_DISPATCH(FN, ...) FN<16>(__VA_ARGS__);
+#endif
 
 #define FEC_BS_DISPATCH(FN, ...)                                                   \
   switch (rt * 100 + cfg.vec) {                                                    \
@@ -3077,7 +3100,7 @@ static bool knob_value_ok(int id, int v) {
     case K_ENC_RT: return v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16;
     case K_ENC_W: return v >= 0 && v <= 4;
     case K_ENC_BW: return v == 1 || v == 2 || v == 4;
-    case K_RING: return v == 0 || v == 2 || (v == 4 && FEC_BS2_HAS_RT4);
+    case K_RING: return v == 0 || v == 2 || (v == 4 && FEC_BS2_HAS_RT4) || (v == 8 && FEC_BS2_HAS_RT8);
     case K_WINDOW_SC: return v >= 0 && v <= 2;
     case K_GROUP: case K_MIN_GROUPS: return v >= 0;
     case K_DEC_WAVES: return v >= 0 && v <= 8;
