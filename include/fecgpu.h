@@ -266,6 +266,11 @@ uint64_t fecgpu_block_svc_launches(const fecgpu_block_svc_t *svc);
 int fecgpu_block_svc_set_deadline(fecgpu_block_svc_t *svc, uint64_t deadline_us);
 /* requests withdrawn at the deadline so far */
 uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *svc);
+/* Diagnostics: the phases of the last served request.  out[0..3]: the worker's clock (s_memrealtime,
+ * 100 MHz ticks) when it claimed the request, when the request was in LDS, when its rows were coded, and
+ * just before it published `done`; out[4], out[5]: the host's clock (CLOCK_MONOTONIC, us) when the request
+ * was posted and when the call saw it done.  Returns FECGPU_OK, or FECGPU_ERR_INVALID for NULL. */
+int fecgpu_block_svc_last_stamps(fecgpu_block_svc_t *svc, uint64_t out[6]);
 
 /* FEC frames for a batch of repair symbols, ready for packet buffers (the block framework's
  * get_repair_payload_from_queue + write_fec_frame, block_framework_sender.h:100-133,

@@ -2080,6 +2080,7 @@ struct alignas(64) BlockSvcMailbox {
   uint32_t status, pad0;
   uint64_t quit;                    // host: 1 = end the worker
   uint64_t launches;                // device: worker generations started (diagnostics)
+  uint64_t stamp[4];                // device: claim, request in LDS, rows coded, before done (s_memrealtime)
 };
 
 __device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
@@ -2108,6 +2109,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, 
                                                  __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) {
           done = s;  // the number this pass serves
           g = 1;
+          __hip_atomic_store(&mb->stamp[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -2128,6 +2131,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, 
           __builtin_nontemporal_load(reinterpret_cast<const v4u *>(&mb->req) + threadIdx.x);
     }
     __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&mb->stamp[1], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int k = (int)R.k, r = (int)R.r, L = (int)R.L;
     const uint32_t em = (uint32_t)(k < r ? k : r);
     if (R.op == 1) {
@@ -2145,9 +2150,12 @@ __global__ __launch_bounds__(kLdsThreads) void k_block_svc(BlockSvcMailbox *mb, 
       else if (em <= 8) decode_block_lds<8>(lds, 0, src, rep, dst, k, r, L, 0, nullptr, R.seeds, R.sp, R.rp, st, rec, R.wreg);
       else decode_block_lds<16>(lds, 0, src, rep, dst, k, r, L, 0, nullptr, R.seeds, R.sp, R.rp, st, rec, R.wreg);
     }
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&mb->stamp[2], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave's outputs reach host memory first
     __syncthreads();
     if (threadIdx.x == 0) {
+      __hip_atomic_store(&mb->stamp[3], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&mb->done, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       t_last = __builtin_amdgcn_s_memrealtime();
     }
@@ -3710,6 +3718,7 @@ struct fecgpu_block_svc {
   uint64_t misses = 0;              // requests withdrawn at the deadline
   uint64_t t_launch_us = 0;         // the running worker's launch, host clock
   uint64_t t_done_us = 0;           // the last request it finished, host clock
+  uint64_t t_post_us = 0, t_seen_us = 0;  // the last served request: posted / seen done (diagnostics)
   std::mutex mu;
 };
 
@@ -3876,8 +3885,13 @@ static int svc_run_posted(fecgpu_block_svc_t *v, uint64_t t0) {
   const uint64_t seq = v->seq + 1;
   v->seq = seq;
   __atomic_store_n(&v->mb->req.seq, seq, __ATOMIC_RELEASE);
+  const uint64_t t_post = svc_now_us();
   for (uint64_t spin = 1;; spin++) {
-    if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) return FECGPU_OK;
+    if (__atomic_load_n(&v->mb->done, __ATOMIC_ACQUIRE) == seq) {
+      v->t_post_us = t_post;
+      v->t_seen_us = svc_now_us();
+      return FECGPU_OK;
+    }
     __builtin_ia32_pause();
     if ((spin & 255) == 0 && svc_now_us() - t0 > v->deadline_us) return svc_withdraw(v, seq);
     if ((spin & 1023) == 0) {
@@ -3970,6 +3984,15 @@ int fecgpu_block_svc_set_deadline(fecgpu_block_svc_t *v, uint64_t deadline_us) {
   std::lock_guard<std::mutex> g(v->mu);
   v->deadline_us = deadline_us;
   v->backoff_until = 0;
+  return FECGPU_OK;
+}
+
+int fecgpu_block_svc_last_stamps(fecgpu_block_svc_t *v, uint64_t out[6]) {
+  if (!v || !out || !v->mb) return FECGPU_ERR_INVALID;
+  std::lock_guard<std::mutex> g(v->mu);
+  for (int i = 0; i < 4; i++) out[i] = __atomic_load_n(&v->mb->stamp[i], __ATOMIC_ACQUIRE);
+  out[4] = v->t_post_us;
+  out[5] = v->t_seen_us;
   return FECGPU_OK;
 }
 
