@@ -148,15 +148,19 @@ extern "C" __attribute__((visibility("hidden"))) void fecgpu_knob_yield(int *sli
 // worker = 0 every other CU.  Returns the mask's words (0: no reservation; the caller makes a plain stream).
 extern "C" __attribute__((visibility("hidden"))) int fecgpu_svc_cu_mask(int device, int worker, uint32_t *mask,
                                                                         int max_words) {
+  // n > 0: the last n CU indices; n < 0: every (-n)-th CU index counted from the last (-8: the indices
+  // c % 8 == 7, one XCD's CUs where the queue's CU numbering interleaves the eight XCDs)
   const int n = knob(K_SVC_RESERVE_CUS);
   int cus = 0;
-  if (n <= 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-      cus <= n || (cus + 31) / 32 > max_words)
+  if (n == 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= (n > 0 ? n : -n) || (cus + 31) / 32 > max_words)
     return 0;
   const int words = (cus + 31) / 32;
   for (int w = 0; w < words; w++) mask[w] = 0;
-  for (int c = 0; c < cus; c++)
-    if ((c >= cus - n) == (worker != 0)) mask[c >> 5] |= 1u << (c & 31);
+  for (int c = 0; c < cus; c++) {
+    const bool reserved = n > 0 ? c >= cus - n : (c % -n) == (-n - 1);
+    if (reserved == (worker != 0)) mask[c >> 5] |= 1u << (c & 31);
+  }
   return words;
 }
 
@@ -3117,7 +3121,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_GATE_US: return v >= 0 && v <= 10000;
     case K_YIELD_STREAMS: return v >= 1 && v <= 4;
     case K_YIELD_WINDOW_MS: return v >= 0 && v <= 600000;
-    case K_SVC_RESERVE_CUS: return v >= 0 && v <= 128;
+    case K_SVC_RESERVE_CUS: return v >= -64 && v <= 128;
     case K_HOST_ALLOC: return v >= 0 && v <= 2;
     case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs

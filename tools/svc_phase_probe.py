@@ -6,7 +6,7 @@ coded / before `done`, and the host's post and done-seen times.  The device cloc
 with the median offset of the fast calls, so each slow call splits into: posted -> claimed (the worker had
 not seen it), claimed -> coded (reading the request and the rows over PCIe, computing, writing), coded ->
 done published (the release fence), published -> seen by the host.
-usage (GPU box): python tools/svc_phase_probe.py [calls] [slice_kb]"""
+usage (GPU box): python tools/svc_phase_probe.py [calls] [slice_kb] [svc_reserve_cus]"""
 import ctypes as C
 import os
 import statistics
@@ -20,9 +20,12 @@ from pquic_amd import load_library  # noqa: E402
 
 ncalls = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
 slice_kb = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+reserve = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # knob svc_reserve_cus (before the streams exist)
 lib = load_library()
 lib.fecgpu_set_knob.argtypes = [C.c_char_p, C.c_int]
 assert lib.fecgpu_set_knob(b"yield_slice_kb", slice_kb) == 0
+assert lib.fecgpu_set_knob(b"svc_reserve_cus", reserve) == 0
+print(f"slices {slice_kb} KiB, svc_reserve_cus {reserve}", flush=True)
 lib.fecgpu_host_alloc.restype = C.c_void_p
 lib.fecgpu_host_alloc.argtypes = [C.c_size_t]
 lib.fecgpu_host_ctx_create.restype = C.c_void_p
