@@ -57,12 +57,12 @@ static std::atomic<uint64_t> g_stats[4];
 enum KnobId { K_PLAN, K_INTERLEAVE, K_GROUP, K_ENC_RT, K_ENC_W, K_ZC_READ, K_RING, K_WINDOW_SC, K_MIN_GROUPS,
               K_ENC_BW,
               K_CHUNK_WAVES, K_SMALL_LDS, K_BLOCK_SVC, K_WS_LDS, K_DEC_WAVES, K_YIELD_SLICE_KB, K_YIELD_DEPTH,
-              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_SVC_RESERVE_CUS, K_HOST_ALLOC, K_N };
+              K_YIELD_GATE_US, K_YIELD_STREAMS, K_YIELD_ALWAYS, K_YIELD_WINDOW_MS, K_SVC_RESERVE_CUS, K_HOST_ALLOC, K_ZC_CUS, K_N };
 static const char *const kKnobName[K_N] = {"plan", "interleave", "group", "enc_tile_rt", "enc_tile_waves",
                                            "zc_read", "ring", "window_sc", "min_groups", "enc_block_waves", "chunk_waves",
                                            "small_lds", "block_svc", "ws_lds", "dec_waves", "yield_slice_kb",
                                            "yield_depth", "yield_gate_us", "yield_streams", "yield_always",
-                                           "yield_window_ms", "svc_reserve_cus", "host_alloc"};
+                                           "yield_window_ms", "svc_reserve_cus", "host_alloc", "zc_cus"};
 enum { PLAN_AUTO = 0, PLAN_WAVE = 1, PLAN_LANE = 2, PLAN_REG = 3, PLAN_TILE = 4, PLAN_WREG = 5 };
 static std::atomic<int> g_knob[K_N];
 static std::once_flag g_knob_once;
@@ -123,6 +123,9 @@ static void knobs_default() {
   // fecgpu_host_alloc's page-locked memory: 0 the runtime's default, 1 fine-grained (coherent), 2
   // coarse-grained (non-coherent), mapped either way (A/B of how zero-copy kernels' host lines sit in L2)
   g_knob[K_HOST_ALLOC] = 0;
+  // host-path context streams on only n CUs spread over the chip (0: all): caps how many waves a zero-copy
+  // bulk call keeps reading host memory at once (A/B of the hooks' wait behind it)
+  g_knob[K_ZC_CUS] = 0;
 }
 
 static inline int knob(KnobId id) {
@@ -150,13 +153,20 @@ extern "C" __attribute__((visibility("hidden"))) int fecgpu_svc_cu_mask(int devi
                                                                         int max_words) {
   // n > 0: the last n CU indices; n < 0: every (-n)-th CU index counted from the last (-8: the indices
   // c % 8 == 7, one XCD's CUs where the queue's CU numbering interleaves the eight XCDs)
-  const int n = knob(K_SVC_RESERVE_CUS);
+  const int n = knob(K_SVC_RESERVE_CUS), zc = knob(K_ZC_CUS);
   int cus = 0;
-  if (n == 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+  if ((n == 0 && (zc == 0 || worker)) ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       cus <= (n > 0 ? n : -n) || (cus + 31) / 32 > max_words)
     return 0;
   const int words = (cus + 31) / 32;
   for (int w = 0; w < words; w++) mask[w] = 0;
+  if (!worker && zc > 0 && zc < cus) {  // zc_cus: the host-path streams on zc CUs, every (cus / zc)-th index
+    const int step = cus / zc;
+    for (int c = 0, m = 0; c < cus && m < zc; c += step, m++) mask[c >> 5] |= 1u << (c & 31);
+    return words;
+  }
+  if (n == 0) return 0;
   for (int c = 0; c < cus; c++) {
     const bool reserved = n > 0 ? c >= cus - n : (c % -n) == (-n - 1);
     if (reserved == (worker != 0)) mask[c >> 5] |= 1u << (c & 31);
@@ -3123,6 +3133,7 @@ static bool knob_value_ok(int id, int v) {
     case K_YIELD_WINDOW_MS: return v >= 0 && v <= 600000;
     case K_SVC_RESERVE_CUS: return v >= -64 && v <= 128;
     case K_HOST_ALLOC: return v >= 0 && v <= 2;
+    case K_ZC_CUS: return v >= 0 && v <= 256;
     case K_INTERLEAVE: return v >= 0 && v <= 3;
     default: return v == 0 || v == 1;  // on / off knobs
   }
