@@ -271,6 +271,10 @@ uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *svc);
  * just before it published `done`; out[4], out[5]: the host's clock (CLOCK_MONOTONIC, us) when the request
  * was posted and when the call saw it done.  Returns FECGPU_OK, or FECGPU_ERR_INVALID for NULL. */
 int fecgpu_block_svc_last_stamps(fecgpu_block_svc_t *svc, uint64_t out[6]);
+/* Whether a worker is running now (it ends by itself after 20 ms without a request, 50 ms in all):
+ * 1 running, 0 not (or never launched), FECGPU_ERR_HIP if the last one ended in an error,
+ * FECGPU_ERR_INVALID for NULL.  Lets a caller (a test) wait for the idle state instead of a time. */
+int fecgpu_block_svc_worker_running(fecgpu_block_svc_t *svc);
 
 /* FEC frames for a batch of repair symbols, ready for packet buffers (the block framework's
  * get_repair_payload_from_queue + write_fec_frame, block_framework_sender.h:100-133,

@@ -4017,6 +4017,15 @@ uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *v) {
   return v->misses;
 }
 
+int fecgpu_block_svc_worker_running(fecgpu_block_svc_t *v) {
+  if (!v) return FECGPU_ERR_INVALID;
+  std::lock_guard<std::mutex> g(v->mu);
+  if (!v->launched) return 0;
+  const hipError_t q = hipEventQuery(v->ev);
+  if (q == hipErrorNotReady) return 1;
+  return q == hipSuccess ? 0 : set_err(FECGPU_ERR_HIP, "block service: worker ended with %s", hipGetErrorString(q));
+}
+
 int fecgpu_synth_fill(void *dst, uint64_t nbytes, uint64_t seed, uint64_t offset, void *stream) {
   if (!dst) return set_err(FECGPU_ERR_INVALID, "%s", "NULL dst");
   if (!nbytes) return FECGPU_OK;

@@ -90,6 +90,8 @@ def load_library(path: str = LIB_PATH, private: bool = False):
         L.fecgpu_block_svc_deadline_misses.restype = u64
     if hasattr(L, "fecgpu_block_svc_last_stamps"):
         L.fecgpu_block_svc_last_stamps.argtypes = [v, C.POINTER(u64)]
+    if hasattr(L, "fecgpu_block_svc_worker_running"):
+        L.fecgpu_block_svc_worker_running.argtypes = [v]
     if hasattr(L, "fecgpu_rlc_decode_rows"):
         L.fecgpu_rlc_decode_rows.argtypes = [v, v, u64, u32, u32, u32, v, v, v, v, v, v, sz, v]
         L.fecgpu_rlc_decode_rows_host.argtypes = [v, v, v, u64, u32, u32, u32, v, v, v, v, v]

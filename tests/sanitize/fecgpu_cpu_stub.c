@@ -112,6 +112,7 @@ int fecgpu_block_svc_rlc_decode_seeded(fecgpu_block_svc_t *svc, const void *src,
     return FECGPU_ERR_INVALID;
 }
 uint64_t fecgpu_block_svc_deadline_misses(fecgpu_block_svc_t *svc) { (void)svc; return 0; }
+int fecgpu_block_svc_worker_running(fecgpu_block_svc_t *svc) { return svc ? 0 : FECGPU_ERR_INVALID; }
 int fecgpu_block_svc_last_stamps(fecgpu_block_svc_t *svc, uint64_t out[6]) {
     (void)svc;
     for (int i = 0; i < 6; i++) out[i] = 0;

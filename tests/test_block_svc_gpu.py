@@ -116,9 +116,13 @@ def test_svc_encode_decode_vs_oracle(lib, svc, k, r, L):
 
 
 def _launches_after_idle(lib, svc):
-    """Waits until any worker of an earlier call has ended on its idle limit (20 ms without a request,
-    worker clock) and returns the launch count."""
-    time.sleep(0.1)
+    """Waits (for the state, bounded) until any worker of an earlier call has ended on its idle limit
+    (20 ms without a request, worker clock) and returns the launch count."""
+    t0 = time.perf_counter()
+    while (st := lib.fecgpu_block_svc_worker_running(svc)) == 1:
+        assert time.perf_counter() - t0 < 5.0, "the worker did not end on its idle limit"
+        time.sleep(0.002)
+    assert st == 0
     return lib.fecgpu_block_svc_launches(svc)
 
 
