@@ -508,7 +508,7 @@ def batching_legs(dev_index, args):
         """host-side rates on a shared CPU slice vary from run to run: the run with the median rate"""
         res = []
         for _ in range(runs):
-            out, rows, q, jb = (C.c_double * 8)(), (C.c_double * 2)(), (C.c_double * 8)(), (C.c_double * 2)()
+            out, rows, q, jb = (C.c_double * 8)(), (C.c_double * 2)(), (C.c_double * 8)(), (C.c_double * 3)()
             rc = fn(out)
             if rc:
                 return rc, None, None
@@ -521,7 +521,9 @@ def batching_legs(dev_index, args):
         return 0, out, {"runs_payload_GiB_s": [round(o[0][0], 2) for o in res],
                         "runs_latency_us_p99": [o[0][2] for o in res], "rows_in_place": int(rows[0]),
                         "rows_staged": int(rows[1]), "latency_us_p90": q[1], "latency_us_p99_9": q[4],
-                        "jobs_allocated_on_sender_thread": int(jb[0])}
+                        "jobs_allocated_on_sender_thread": int(jb[0]),
+                        "job_alloc_ms_on_sender_thread": round(jb[1] / 1000.0, 2),
+                        "polls_holding_for_a_job": int(jb[2])}
 
     def leg(out, extra, **kw):
         d = {"k": args.k, "r": args.r, "L": args.symbol, "batch_blocks": batch, "batches_in_flight": inflight,

@@ -62,6 +62,8 @@ typedef struct {
     uint64_t rows_staged;           /* symbol rows copied through the page-locked staging rows instead */
     uint64_t jobs_allocated;        /* batch jobs (page-locked queue buffers) allocated on the caller's thread */
     uint64_t job_alloc_us;          /* caller-thread time in those allocations */
+    uint64_t deadline_holds;        /* polls that kept an overdue queue open: no idle job for its successor while
+                                     * two or more were in flight (flushed at the first poll with one back) */
 } pquic_fec_batch_stats_t;
 
 /* NULL on failure (bad configuration, no device, out of pinned memory). */

@@ -66,6 +66,7 @@ typedef struct job {
     struct job *next;
     int op, xor_scheme;
     uint32_t k, r, n, cap, stride;
+    uint32_t cap_alloc;            /* blocks its per-block buffers hold: batch_blocks, or small_cap (job_get) */
     size_t src_bytes, rep_bytes;   /* allocated pinned sizes */
     uint8_t *src, *rep, *st;       /* pinned */
     uint32_t *fbn;                 /* pinned: block numbers (generate) */
@@ -130,8 +131,12 @@ struct pquic_fec_batcher {
     pthread_cond_t cv_prov;
     job_t *spares;
     uint64_t stats_spares;         /* spares made (under mu) */
+    int reserve;                   /* idle jobs of a shape to keep, free + spare (PQUIC_FEC_BATCH_RESERVE, default 1) */
+    uint32_t small_cap;            /* blocks of a job the caller allocates itself (0: full size; job_get) */
+    int hold;                      /* deadline_hold on (PQUIC_FEC_BATCH_HOLD=0 turns it off, A/B) */
     uint64_t next_seq;             /* caller thread: sequence number of the next flushed job */
     uint64_t collect_seq;          /* caller thread: the job whose completions come next */
+    uint64_t jobs_back;            /* caller thread: flushed jobs completed and back in free_jobs */
     /* registered arenas, sorted by base and disjoint; stagers look rows up under the read lock (one
      * lock per work item), registration takes the write lock, so connections may come and go while
      * batches run */
@@ -250,6 +255,7 @@ static uint32_t window_stride(const pquic_fec_batcher_t *b) { return (b->stride 
 static job_t *job_alloc(uint32_t cap, size_t sb, size_t rb) {
     job_t *j = calloc(1, sizeof *j);
     if (!j) return NULL;
+    j->cap_alloc = cap;
     j->src_bytes = sb;
     j->rep_bytes = rb;
     j->src = fecgpu_host_alloc(sb);
@@ -270,7 +276,7 @@ static job_t *job_alloc(uint32_t cap, size_t sb, size_t rb) {
  * the heap count, so the provisioner thread may run it on a job no one else sees.  Returns 0, or -1 when an
  * allocation failed (the job stays valid for another use). */
 static int job_prepare(pquic_fec_batcher_t *b, job_t *j, int op, int xor_scheme, uint32_t k, uint32_t r) {
-    const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
+    const uint32_t cap = j->cap_alloc, S = op == OP_WINDOW ? window_stride(b) : b->stride;
     const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
     /* recover only: the repairs' FPID seeds, [cap][r] (grown on reuse like the repair table) */
     const size_t eb = (size_t)cap * (r ? r : 1) * 4;
@@ -352,17 +358,22 @@ static job_t *take_fit(job_t **pp, size_t sb, size_t rb) {
     return NULL;
 }
 
-static int has_fit(const job_t *j, size_t sb, size_t rb) {
+static int count_fit(const job_t *j, size_t sb, size_t rb) {
+    int n = 0;
     for (; j; j = j->next)
-        if (j->src_bytes >= sb && j->rep_bytes >= rb) return 1;
-    return 0;
+        if (j->src_bytes >= sb && j->rep_bytes >= rb) n++;
+    return n;
 }
 
 /* Spare jobs.  Allocating a job's page-locked buffers takes milliseconds (6.3 ms for a 2048-block k16 r4 job,
  * profiles/r06_conn512_probe.log), and on the caller's thread it stalls every block queued meanwhile: the run
  * whose pipeline went one job deeper than ever before had its p99 at 8.7 ms against 2.3-3.8 in the others.  So
  * whenever the caller takes the last job that fits a shape, the provisioner thread allocates the next one
- * (same shape, prepared for the same use) and leaves it in b->spares, where job_get finds it. */
+ * (same shape, prepared for the same use) and leaves it in b->spares, where job_get finds it.  One spare
+ * covers one job more in flight per allocation time (about 20 ms for a 4096-block k16 r4 job); a stall that
+ * deepens the pipeline faster (the paced leg under a kernel trace: 1-2 caller allocations of 20-45 ms in 3 of
+ * 12 runs, profiles/r06_paced_probe.log) makes the caller allocate.  That allocation is a small job (job_get);
+ * PQUIC_FEC_BATCH_RESERVE > 1 has the provisioner keep more idle full-size jobs of the shape (free or spare). */
 static void *prov_main(void *arg) {
     pquic_fec_batcher_t *b = arg;
     pthread_mutex_lock(&b->mu);
@@ -390,7 +401,11 @@ static void *prov_main(void *arg) {
     return NULL;
 }
 
-/* A job for (op, scheme, k, r): from the free list, else a spare, else allocated here (counted). */
+/* A job for (op, scheme, k, r): from the free list, else a spare, else a small job from the free list, else
+ * allocated here (counted).  What the caller allocates itself is small (b->small_cap blocks, a sixteenth of
+ * batch_blocks when that is at least 1024, window jobs excepted): page-locking a full 4096-block k16 r4 job
+ * takes about 20 ms, a 256-block one about 1, and a small job only flushes sooner (at its own capacity).
+ * The provisioner makes the full-size ones. */
 static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k, uint32_t r) {
     const uint32_t cap = b->cfg.batch_blocks, S = op == OP_WINDOW ? window_stride(b) : b->stride;
     const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
@@ -400,9 +415,12 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         j = take_fit(&b->spares, sb, rb);
         pthread_mutex_unlock(&b->mu);
     }
+    const uint32_t small = b->prov_started && op != OP_WINDOW ? b->small_cap : 0;
+    if (!j && small) j = take_fit(&b->free_jobs, (size_t)small * k * S, (size_t)small * r * S);
     if (!j) {
+        const uint32_t c = small ? small : cap;
         const uint64_t t_alloc = mono_us();
-        if (!(j = job_alloc(cap, sb, rb))) return NULL;
+        if (!(j = job_alloc(c, (size_t)c * k * S, (size_t)c * r * S))) return NULL;
         b->stats.jobs_allocated++;
         b->stats.job_alloc_us += mono_us() - t_alloc;
     }
@@ -411,10 +429,11 @@ static job_t *job_get(pquic_fec_batcher_t *b, int op, int xor_scheme, uint32_t k
         b->free_jobs = j;
         return NULL;
     }
-    /* the last job of this shape is in use: have the next one made off this thread */
-    if (b->prov_started && !has_fit(b->free_jobs, sb, rb)) {
+    /* fewer idle jobs of this shape than the reserve: have the next one made off this thread */
+    const int idle = count_fit(b->free_jobs, sb, rb);
+    if (b->prov_started && idle < b->reserve) {
         pthread_mutex_lock(&b->mu);
-        if (!b->prov_want && !has_fit(b->spares, sb, rb)) {
+        if (!b->prov_want && idle + count_fit(b->spares, sb, rb) < b->reserve) {
             b->prov_want = 1;
             b->prov_op = op;
             b->prov_xor = xor_scheme;
@@ -866,6 +885,12 @@ pquic_fec_batcher_t *pquic_fec_batcher_create(const pquic_fec_batch_cfg_t *cfg) 
      * PQUIC_FEC_BATCH_SPARES=0 turns it off (A/B), read once per batcher like the thread counts */
     const char *sp = getenv("PQUIC_FEC_BATCH_SPARES");
     b->prov_started = !(sp && atoi(sp) == 0) && pthread_create(&b->prov, NULL, prov_main, b) == 0;
+    const char *rs = getenv("PQUIC_FEC_BATCH_RESERVE");  /* idle jobs per shape the provisioner keeps (A/B) */
+    b->reserve = rs && atoi(rs) > 0 ? (atoi(rs) < 8 ? atoi(rs) : 8) : 1;
+    const char *sm = getenv("PQUIC_FEC_BATCH_SMALL");  /* 0: the caller allocates full-size jobs (A/B) */
+    b->small_cap = cfg->batch_blocks >= 1024 && !(sm && atoi(sm) == 0) ? cfg->batch_blocks / 16 : 0;
+    const char *ho = getenv("PQUIC_FEC_BATCH_HOLD");
+    b->hold = !(ho && atoi(ho) == 0);
     return b;
 }
 
@@ -1141,6 +1166,7 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
         j->n = 0;
         j->next = b->free_jobs;
         b->free_jobs = j;
+        b->jobs_back++;
         j = next;
         i = 0;
         if (budget && (uint32_t)n >= budget) break;
@@ -1152,14 +1178,52 @@ static int collect(pquic_fec_batcher_t *b, uint32_t budget) {
     return n;
 }
 
-int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us) {
-    if (!b) return 0;
+/* Whether an overdue queue stays open for now: its successor would find no idle job (none free, no spare)
+ * while at least two jobs are in flight, so the next submission would page-lock a new one on the caller's
+ * thread -- and under a GPU stall that allocation waits out the stall itself (17-48 ms beside a 10-30 ms one,
+ * profiles/r06_paced_stall.log) while a batch flushed every deadline needs a new job each time.  The queue
+ * keeps filling instead, up to its capacity, and is flushed at the first poll that has a job back; the
+ * provisioner is asked for one meanwhile. */
+static int deadline_hold(pquic_fec_batcher_t *b, const job_t *j) {
+    if (!b->hold || !b->prov_started || b->next_seq - b->jobs_back < 2) return 0;
+    const uint32_t cap = b->cfg.batch_blocks, S = j->op == OP_WINDOW ? window_stride(b) : b->stride;
+    const size_t sb = (size_t)cap * j->k * S, rb = (size_t)cap * j->r * S;
+    const uint32_t sm = j->op == OP_WINDOW ? 0 : b->small_cap;
+    if (count_fit(b->free_jobs, sm ? (size_t)sm * j->k * S : sb, sm ? (size_t)sm * j->r * S : rb)) return 0;
+    pthread_mutex_lock(&b->mu);
+    const int hold = !count_fit(b->spares, sb, rb);
+    if (hold && !b->prov_want) {
+        b->prov_want = 1;
+        b->prov_op = j->op;
+        b->prov_xor = j->xor_scheme;
+        b->prov_k = j->k;
+        b->prov_r = j->r;
+        pthread_cond_signal(&b->cv_prov);
+    }
+    pthread_mutex_unlock(&b->mu);
+    return hold;
+}
+
+/* Flushes the overdue queues (deadline_hold aside); returns 1 if one was held. */
+static int deadline_pass(pquic_fec_batcher_t *b, uint64_t now_us) {
+    int held = 0;
     for (int s = 0; s < MAX_OPEN; s++) {
         job_t *j = b->open[s];
         if (b->next_due == UINT64_MAX || now_us - b->next_due < b->cfg.max_delay_us) break;  /* none overdue */
-        if (j && j->n && now_us - j->t_first >= b->cfg.max_delay_us) flush_job(b, s, &b->stats.flushed_deadline);
+        if (!j || !j->n || now_us - j->t_first < b->cfg.max_delay_us) continue;
+        if (deadline_hold(b, j)) held = 1;
+        else flush_job(b, s, &b->stats.flushed_deadline);
     }
-    return collect(b, b->cfg.poll_blocks);
+    b->stats.deadline_holds += (uint64_t)held;
+    return held;
+}
+
+int pquic_fec_batch_poll(pquic_fec_batcher_t *b, uint64_t now_us) {
+    if (!b) return 0;
+    const int held = deadline_pass(b, now_us);
+    const int n = collect(b, b->cfg.poll_blocks);
+    if (held && n) deadline_pass(b, now_us);  /* a job came back: the held queue goes now */
+    return n;
 }
 
 int pquic_fec_batch_drain(pquic_fec_batcher_t *b) {

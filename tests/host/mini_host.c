@@ -589,12 +589,13 @@ void mh_batch_recovered(long t, uint8_t *out, uint16_t *out_len, uint8_t *recove
     *cur_ss = tk->fb->current_source_symbols;
 }
 
-void mh_batch_get_stats(uint64_t out[12]) {
+void mh_batch_get_stats(uint64_t out[15]) {
     pquic_fec_batch_stats_t s;
     pquic_fec_batch_get_stats(g_batcher, &s);
     out[0] = s.submitted; out[1] = s.completed; out[2] = s.batches; out[3] = s.flushed_full;
     out[4] = s.flushed_deadline; out[5] = s.flushed_drain; out[6] = s.immediate; out[7] = s.engine_errors;
     out[8] = s.windows; out[9] = s.window_rows; out[10] = s.rows_in_place; out[11] = s.rows_staged;
+    out[12] = s.jobs_allocated; out[13] = s.job_alloc_us; out[14] = s.deadline_holds;
 }
 
 /* frees every ticket's block and the batcher */

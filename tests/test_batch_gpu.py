@@ -149,10 +149,11 @@ class Batch:
         return {j: out[j, : ol[j]].copy() for j in range(k) if rec[j]}, cur.value
 
     def stats(self):
-        s = (C.c_uint64 * 12)()
+        s = (C.c_uint64 * 15)()
         self.L.mh_batch_get_stats(s)
         keys = ["submitted", "completed", "batches", "flushed_full", "flushed_deadline", "flushed_drain",
-                "immediate", "engine_errors", "windows", "window_rows", "rows_in_place", "rows_staged"]
+                "immediate", "engine_errors", "windows", "window_rows", "rows_in_place", "rows_staged",
+                "jobs_allocated", "job_alloc_us", "deadline_holds"]
         return dict(zip(keys, list(s)))
 
     def close(self):
@@ -258,6 +259,107 @@ def test_batch_generate_gathers_from_registered_arena(batch_blocks, max_symbol):
         _check_generate(bt, t, j)
     st = bt.stats()
     assert st["engine_errors"] == 0
+    bt.close()
+
+
+@pytest.mark.parametrize("conns", [0, 2])
+def test_batch_small_jobs_keep_the_bytes(conns):
+    """batch_blocks >= 1024: a job the caller has to allocate itself (no idle one, no spare from the
+    provisioner) is a small one, batch_blocks / 16 blocks (batch.c job_get), flushed at its own capacity.
+    A fresh batcher's first job is always one.  600 k16 r4 blocks generated back to back (fewer than
+    batch_blocks, so any full flush is a small job's), then recovered with 4 erasures each: repairs and
+    recovered rows equal the oracle's, staged (conns 0) and in place (conns 2)."""
+    o = Oracle()
+    k, r, L, n = 16, 4, 1200, 600
+    rng = np.random.default_rng(77 + conns)
+    src = rng.integers(0, 256, (n, k, L), dtype=np.uint8)
+    fbn0 = int(rng.integers(0, 1 << 24))
+    want = o.rlc_encode_batch(src, r, fbn0)
+    bt = Batch(1024, max_symbol=L, connections=conns, conn_bytes=16 << 20)
+    tickets = []
+    for b in range(n):
+        if conns:
+            bt.use(b % conns)
+        tickets.append(bt.generate(False, (fbn0 + b) & 0xFFFFFF, list(src[b]), r, now=b))
+    bt.L.mh_batch_drain()
+    st = bt.stats()
+    assert st["engine_errors"] == 0 and st["completed"] == n
+    assert st["flushed_full"] >= 1, "no job was flushed below batch_blocks: no small job ran"
+    for b, t in enumerate(tickets):
+        assert bt.status(t) == (0, 1)
+        reps, fps = bt.repairs(t)
+        assert np.array_equal(np.stack(reps), want[b]), b
+        assert fps == [(((fbn0 + b) & 0xFFFFFF) << 8) | i for i in range(r)]
+    miss = [rng.choice(k, 4, replace=False) for _ in range(n)]
+    tickets = []
+    for b in range(n):
+        fbn = (fbn0 + b) & 0xFFFFFF
+        srcs = [None if j in miss[b] else src[b, j] for j in range(k)]
+        tickets.append(_recover_on(bt, conns, b, False, fbn, srcs, list(want[b]),
+                                   [(fbn << 8) | i for i in range(r)], now=n + b))
+    bt.L.mh_batch_drain()
+    assert bt.stats()["engine_errors"] == 0
+    nrec = 0
+    for b, t in enumerate(tickets):
+        ret, calls = bt.status(t)
+        assert calls == 1 and ret == 0
+        rec, _ = bt.recovered(t)
+        fbn = (fbn0 + b) & 0xFFFFFF
+        _, out = o.rlc_decode_block(fbn, [None if j in miss[b] else src[b, j] for j in range(k)], list(want[b]))
+        assert sorted(rec) == sorted(out), b  # none where the reference would crash (about 1 %)
+        for j, row in rec.items():
+            assert np.array_equal(row, src[b, j]) and np.array_equal(row, out[j]), (b, j)
+        nrec += len(rec)
+    assert nrec >= 0.95 * 4 * n
+    bt.close()
+
+
+@pytest.mark.skipif(bool(os.environ.get("PQUIC_TEST_MINIHOST")), reason="stalls the GPU (no GPU under the CPU stand-in)")
+def test_batch_deadline_holds_behind_a_stalled_gpu():
+    """While the GPU is stalled (a kernel holds every CU, tests/host/libgpuhog.so), blocks keep arriving
+    and every poll finds their queue overdue.  With two jobs in flight and none idle, the overdue queue
+    stays open and keeps filling (pquic_fec_batch_stats_t deadline_holds) instead of being flushed into a
+    batch whose successor the caller would have to page-lock on its own thread, which waits out the stall.
+    Asserted: at most one job allocated by the caller during the stall; some polls held the queue (and
+    fewer batches than blocks were flushed), unless the provisioner had a job ready for every flush; every
+    block's repairs equal the oracle's once the GPU is released."""
+    hog = C.CDLL(os.path.join(ROOT, "tests", "host", "libgpuhog.so"))
+    o = Oracle()
+    k, r, L, n = 16, 4, 1200, 40
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, (n + 1, k, L), dtype=np.uint8)
+    want = o.rlc_encode_batch(src, r, 1000)
+    bt = Batch(64, max_delay_us=100, max_symbol=L)
+    tickets = [bt.generate(False, 1000, list(src[0]), r, now=0)]  # warm-up: one job, completed
+    bt.L.mh_batch_drain()
+    s0 = bt.stats()
+    try:
+        assert hog.gpu_hog_launch(5000) == 0
+        t0 = time.perf_counter()
+        while hog.gpu_hog_resident() < hog.gpu_hog_workgroups():
+            assert hog.gpu_hog_running() and time.perf_counter() - t0 < 4.0
+            time.sleep(0.0005)
+        now = 10_000
+        for b in range(1, n + 1):
+            tickets.append(bt.generate(False, 1000 + b, list(src[b]), r, now=now))
+            now += 1000  # every poll finds the queue overdue
+            bt.L.mh_batch_poll(now)
+        s1 = bt.stats()
+    finally:
+        assert hog.gpu_hog_release() == 0
+    bt.L.mh_batch_drain()
+    st = bt.stats()
+    assert st["completed"] == n + 1 and st["engine_errors"] == 0
+    assert s1["jobs_allocated"] - s0["jobs_allocated"] <= 1, (s0, s1)
+    held = s1["deadline_holds"] - s0["deadline_holds"]
+    flushed = s1["flushed_deadline"] - s0["flushed_deadline"]
+    assert held > 0 or flushed == n, (s0, s1)  # held, or the provisioner kept a job ready for every flush
+    if held:
+        assert flushed < n
+    for b, t in enumerate(tickets):
+        assert bt.status(t) == (0, 1)
+        reps, _ = bt.repairs(t)
+        assert np.array_equal(np.stack(reps), want[b]), b
     bt.close()
 
 

@@ -277,7 +277,8 @@ double bl_clock_cost(void) {
 
 static pthread_barrier_t *g_sync;  /* bl_run_senders: the senders' pass barrier */
 static __thread uint64_t g_span[2];  /* the last measured pass: start, end (us) */
-static __thread double g_jobs[2];   /* the last measured pass: batch jobs allocated, caller us in those allocations */
+static __thread double g_jobs[3];   /* the last measured pass: batch jobs allocated, caller us in those allocations,
+                                     * polls that held an overdue queue (no idle job) */
 static __thread double g_lat_q[8];  /* the last measured pass's latency: p50 p90 p95 p99 p99.9 max mean, count */
 static __thread double g_rows[2];   /* the last bl_run's measured pass: rows in place, rows staged */
 static __thread double g_phases[6];  /* the last bl_run's measured pass: engine, stager, completion thread-us; wall us;
@@ -621,6 +622,7 @@ static int run_sender(int device, int k, int r, int L, int nconn, long nblocks, 
     g_rows[1] = (double)(st.rows_staged - st0.rows_staged);
     g_jobs[0] = (double)(st.jobs_allocated - st0.jobs_allocated);
     g_jobs[1] = (double)(st.job_alloc_us - st0.job_alloc_us);
+    g_jobs[2] = (double)(st.deadline_holds - st0.deadline_holds);
     free(slots); free(ss); free(rsy); free(g_lat); free(cnx); free(pool);
     g_lat = NULL;
     if (pinned) sched_setaffinity(0, sizeof saved, &saved);
@@ -900,10 +902,12 @@ void bl_last_phases(double out[6]) {
     for (int i = 0; i < 6; i++) out[i] = g_phases[i];
 }
 
-/* The last bl_run's measured pass: batch jobs the batcher allocated on the sender's thread, and the us spent. */
-void bl_last_jobs(double out[2]) {
+/* The last bl_run's measured pass: batch jobs the batcher allocated on the sender's thread, the us spent, and
+ * the polls that held an overdue queue for want of an idle job (pquic_fec_batch_stats_t deadline_holds). */
+void bl_last_jobs(double out[3]) {
     out[0] = g_jobs[0];
     out[1] = g_jobs[1];
+    out[2] = g_jobs[2];
 }
 
 /* The last bl_run's measured pass, block latency (us): p50, p90, p95, p99, p99.9, max, mean; [7] blocks. */

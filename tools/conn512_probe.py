@@ -51,7 +51,7 @@ for nconn, batch, infl, huge in sets:
                f"{(c1.get('throttled_usec', 0) - c0.get('throttled_usec', 0)) / 1e3:.1f} ms") if c0 else ""
         lib.bl_last_latency(q)
         lib.bl_last_phases(ph)
-        jb = (C.c_double * 2)()
+        jb = (C.c_double * 3)()
         lib.bl_last_jobs(jb)
         print(f"{nconn:3d} conn batch {batch} inflight {infl} hugepages {huge} run {i}: {out[0]:6.2f} GiB/s, "
               f"latency us p50 {q[0]:6.0f} p90 {q[1]:6.0f} p95 {q[2]:6.0f} p99 {q[3]:6.0f} p99.9 {q[4]:6.0f} "

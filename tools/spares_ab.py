@@ -29,7 +29,7 @@ for i in range(runs):
                                                                   REG | PER_CONN, o)),
                          ("2 senders 64 conn ", lambda o: lib.bl_run_senders(2, 0, 16, 4, 1200, 64, 200000, 1024, 2000,
                                                                           2, REG | PER_CONN, o))):
-            out, jb = (C.c_double * 8)(), (C.c_double * 2)()
+            out, jb = (C.c_double * 8)(), (C.c_double * 3)()
             rc |= fn(out)
             lib.bl_last_jobs(jb)
             jobs = f", jobs allocated on the sender {jb[0]:.0f} ({jb[1] / 1e3:.1f} ms)" if "1 sender" in name else ""
