@@ -32,6 +32,9 @@ struct Lay {
 // Random-erasure decode (round 3): MODE 1 = the R erased sources of block b are a random R-subset
 // (one of 64 fixed masks, picked by a hash of b), read in slot order as the recover pass does;
 // MODE 2 = the same, the recovered rows written packed (out[b][i]) instead of at their slots.
+// Combined layout (round 6, COMB_ONLY): each block's k sources and r repairs contiguous, blk[b][k + r][L].
+// MODE 3 = random erasures read from it in slot order, recovered rows packed to out[b][i]; MODE 4 = the
+// same written into the erased slots; MODE 5 = encode: sources read, repairs written to the block's tail.
 __constant__ uint32_t kEras[64];
 __device__ __forceinline__ int nth_bit(uint32_t m, int n) {
   for (int i = 0; i < n; i++) m &= m - 1;
@@ -59,8 +62,11 @@ __global__ __launch_bounds__(64) void pattern(const uint8_t *__restrict__ src, c
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
           const int j = j0 + jj;
-          const uint8_t *p = src + ly.row(b, j, K);
-          if (MODE) {
+          const uint8_t *p = MODE >= 3 ? src + (b * (K + R) + j) * (uint64_t)L : src + ly.row(b, j, K);
+          if (MODE >= 3 && MODE <= 4) {
+            const uint32_t m = kEras[(b * 0x9E3779B1u >> 7) & 63];
+            if ((m >> j) & 1) p = src + (b * (K + R) + K + __popc(m & ((1u << j) - 1))) * (uint64_t)L;
+          } else if (MODE == 1 || MODE == 2) {
             const uint32_t m = kEras[(b * 0x9E3779B1u >> 7) & 63];
             if ((m >> j) & 1) p = rep + ly.row(b, __popc(m & ((1u << j) - 1)), R);
           } else if (DEC && j >= e0 && j < e0 + R) {
@@ -76,7 +82,9 @@ __global__ __launch_bounds__(64) void pattern(const uint8_t *__restrict__ src, c
       for (int i = 0; i < R; i++) {
         uint8_t *p = DEC ? out + ly.row(b, e0 + i, K) : out + ly.row(b, i, R);
         if (MODE == 1) p = out + ly.row(b, nth_bit(kEras[(b * 0x9E3779B1u >> 7) & 63], i), K);
-        if (MODE == 2) p = out + ly.row(b, i, R);
+        if (MODE == 2 || MODE == 3) p = out + ly.row(b, i, R);
+        if (MODE == 4) p = out + (b * (K + R) + nth_bit(kEras[(b * 0x9E3779B1u >> 7) & 63], i)) * (uint64_t)L;
+        if (MODE == 5) p = out + (b * (K + R) + K + i) * (uint64_t)L;
         __builtin_nontemporal_store(x0 + (uint32_t)i, (u32x4 *)(p + o0));
         if (ok1) __builtin_nontemporal_store(x1 + (uint32_t)i, (u32x4 *)(p + o1));
       }
@@ -132,13 +140,13 @@ int main() {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const uint64_t nb = (uint64_t)(1 << 20) * 16 / K;
   uint8_t *src, *rep, *dst;
-  CK(hipMalloc(&src, nb * K * L)); CK(hipMalloc(&rep, nb * R * L)); CK(hipMalloc(&dst, nb * K * L));
-  CK(hipMemset(src, 3, nb * K * L)); CK(hipMemset(rep, 5, nb * R * L)); CK(hipMemset(dst, 0, nb * K * L));
-  auto run = [&](const char *name, size_t lds, auto kern, uint64_t groups, int sm, bool dec) {
+  CK(hipMalloc(&src, nb * (K + R) * L)); CK(hipMalloc(&rep, nb * R * L)); CK(hipMalloc(&dst, nb * (K + R) * L));
+  CK(hipMemset(src, 3, nb * (K + R) * L)); CK(hipMemset(rep, 5, nb * R * L)); CK(hipMemset(dst, 0, nb * (K + R) * L));
+  auto run = [&](const char *name, size_t lds, auto kern, uint64_t groups, int sm, bool dec, uint8_t *outp = nullptr) {
     float best = 1e9;
     for (int it = 0; it < 6; it++) {
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(kern, dim3((uint32_t)groups), dim3(64), lds, 0, src, rep, dec ? dst : rep, nb, sm);
+      hipLaunchKernelGGL(kern, dim3((uint32_t)groups), dim3(64), lds, 0, src, rep, outp ? outp : dec ? dst : rep, nb, sm);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (it) best = std::min(best, ms);
     }
@@ -168,6 +176,23 @@ int main() {
       em[i] = m;
     }
     CK(hipMemcpyToSymbol(HIP_SYMBOL(kEras), em, sizeof em));
+  }
+  if (getenv("COMB_ONLY")) {  // two arrays (src, rep) against one combined block-major array, alternating
+    for (int it = 0; it < 3; it++)
+      for (size_t lds : {(size_t)13 << 10, (size_t)10 << 10}) {
+        const int wps = lds == ((size_t)13 << 10) ? 3 : 4;
+        char nm[96];
+#define RUNC(G_, M_, D_, NAME_)                                                                     \
+        snprintf(nm, sizeof nm, "%s G%-2d %d waves/SIMD", NAME_, G_, wps);                          \
+        run(nm, lds, pattern<G_, D_, M_>, (nb + G_ - 1) / G_, 0, true, M_ >= 4 ? src : nullptr);
+        RUNC(1, 2, true, "decode two arrays, packed out  ") RUNC(1, 3, true, "decode combined,   packed out  ")
+        RUNC(1, 4, true, "decode combined,   in place    ") RUNC(2, 2, true, "decode two arrays, packed out  ")
+        RUNC(2, 3, true, "decode combined,   packed out  ")
+        snprintf(nm, sizeof nm, "encode two arrays               G1  %d waves/SIMD", wps);
+        run(nm, lds, pattern<1, false>, nb, 0, false);
+        RUNC(1, 5, false, "encode combined (repairs in tail)")
+      }
+    return 0;
   }
   if (getenv("DEC_ONLY")) {  // decode patterns: contiguous erased run / random erasures / random + packed output
     for (size_t lds : {(size_t)13 << 10, (size_t)10 << 10}) {
