@@ -276,7 +276,13 @@ static job_t *job_alloc(uint32_t cap, size_t sb, size_t rb) {
  * the heap count, so the provisioner thread may run it on a job no one else sees.  Returns 0, or -1 when an
  * allocation failed (the job stays valid for another use). */
 static int job_prepare(pquic_fec_batcher_t *b, job_t *j, int op, int xor_scheme, uint32_t k, uint32_t r) {
-    const uint32_t cap = j->cap_alloc, S = op == OP_WINDOW ? window_stride(b) : b->stride;
+    const uint32_t S = op == OP_WINDOW ? window_stride(b) : b->stride;
+    /* the blocks of this shape its row buffers hold: a job allocated for a narrower shape (or a small one,
+     * job_get) may hold fewer than its per-block arrays */
+    uint32_t cap = j->cap_alloc;
+    if (k && j->src_bytes / ((size_t)k * S) < cap) cap = (uint32_t)(j->src_bytes / ((size_t)k * S));
+    if (r && j->rep_bytes / ((size_t)r * S) < cap) cap = (uint32_t)(j->rep_bytes / ((size_t)r * S));
+    if (!cap) return -1;
     const size_t sb = (size_t)cap * k * S, rb = (size_t)cap * r * S;
     /* recover only: the repairs' FPID seeds, [cap][r] (grown on reuse like the repair table) */
     const size_t eb = (size_t)cap * (r ? r : 1) * 4;

@@ -314,6 +314,40 @@ def test_batch_small_jobs_keep_the_bytes(conns):
     bt.close()
 
 
+def test_batch_small_jobs_across_shapes():
+    """Jobs reused across block shapes (batch_blocks >= 1024, where job_get also takes a job that only holds
+    a small one's worth of a shape): a job's capacity for a shape is what its row buffers hold (batch.c
+    job_prepare).  First 2100 k4 r1 blocks (full-size k4 jobs, idle after the drain), then 600 k32 r8 blocks
+    (a full k4 job holds 128 of them, not 1024), then the shapes interleaved block by block; repairs equal
+    the oracle's (and under ASan, test_sanitize.py, no row lands past a buffer)."""
+    o = Oracle()
+    L = 1200
+    rng = np.random.default_rng(11)
+    shapes = [(4, 1), (32, 8), (16, 4), (8, 2)]
+    bt = Batch(1024, max_symbol=L)
+    tickets = []
+    order = [(4, 1)] * 2100 + [None] + [(32, 8)] * 600 + [None] + \
+        [shapes[(b * 7 + b // 5) % len(shapes)] for b in range(480)]
+    for b, shape in enumerate(order):
+        if shape is None:
+            bt.L.mh_batch_drain()
+            continue
+        k, r = shape
+        src = rng.integers(0, 256, (1, k, L), dtype=np.uint8)
+        fbn = int(rng.integers(0, 1 << 24))
+        tickets.append((bt.generate(False, fbn, list(src[0]), r, now=b), o.rlc_encode_batch(src, r, fbn)[0]))
+        if b > 2702 and b % 40 == 39:  # deadline flushes in the interleaved part only
+            bt.L.mh_batch_poll(10 ** 9)
+    bt.L.mh_batch_drain()
+    st = bt.stats()
+    assert st["engine_errors"] == 0 and st["completed"] == len(tickets)
+    for t, want in tickets:
+        assert bt.status(t) == (0, 1)
+        reps, _ = bt.repairs(t)
+        assert np.array_equal(np.stack(reps), want)
+    bt.close()
+
+
 @pytest.mark.skipif(bool(os.environ.get("PQUIC_TEST_MINIHOST")), reason="stalls the GPU (no GPU under the CPU stand-in)")
 def test_batch_deadline_holds_behind_a_stalled_gpu():
     """While the GPU is stalled (a kernel holds every CU, tests/host/libgpuhog.so), blocks keep arriving
