@@ -625,6 +625,9 @@ def hook_latency_legs(dev_index):
     # the batching adapter's kind of kernel) occupies the GPU; the resident service withdraws a request
     # it could not serve within 2 ms and the call takes the launch path
     lib.bl_hook_latency_loaded.argtypes = [C.c_int, C.c_int, C.c_long, C.POINTER(C.c_double)]
+    lib.bl_bulk_rate.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    alone = (C.c_double * 2)()
+    rc_alone = lib.bl_bulk_rate(dev_index, 4096, 200, alone)  # the bulk call with no hooks, same run
     lo = (C.c_double * 11)()
     rc = lib.bl_hook_latency_loaded(dev_index, 4096, 2000, lo)
     leg["under_bulk_load"] = {"error": rc} if rc else {
@@ -632,6 +635,23 @@ def hook_latency_legs(dev_index):
         "generate_us_p50": lo[0], "generate_us_p99": lo[1], "recover_us_p50": lo[3], "recover_us_p99": lo[4],
         "bulk_calls_meanwhile": int(lo[7]), "bulk_ms_per_call_mean": round(lo[9], 3),
         "bulk_ms_per_call_max": round(lo[10], 3), "requests_withdrawn_at_deadline": int(lo[8])}
+    if not rc and not rc_alone:
+        leg["under_bulk_load"]["bulk_alone_ms_per_call"] = round(alone[0], 3)
+        leg["under_bulk_load"]["bulk_beside_hooks_over_alone"] = round(lo[9] / alone[0], 3)
+        # the same without slicing (knob yield_slice_kb 0): what the slices buy, and what they cost
+        eng = C.CDLL(os.path.join(ROOT, "pquic_amd", "lib", "libpquic_fec.so"))
+        eng.fecgpu_set_knob.argtypes = [C.c_char_p, C.c_int]
+        eng.fecgpu_get_knob.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
+        kb = C.c_int(0)
+        un = (C.c_double * 11)()
+        if eng.fecgpu_get_knob(b"yield_slice_kb", C.byref(kb)) == 0 and eng.fecgpu_set_knob(b"yield_slice_kb", 0) == 0:
+            try:
+                if lib.bl_hook_latency_loaded(dev_index, 4096, 2000, un) == 0:
+                    leg["under_bulk_load"]["unsliced"] = {
+                        "generate_us_p99": un[1], "recover_us_p99": un[4], "bulk_ms_per_call_mean": round(un[9], 3),
+                        "bulk_beside_hooks_over_alone": round(un[9] / alone[0], 3)}
+            finally:
+                eng.fecgpu_set_knob(b"yield_slice_kb", kb.value)
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libfecref.so")
     if os.path.exists(ref_path):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
