@@ -379,10 +379,10 @@ def gpu_device_fds():
 
 def launch_ranks(args):
     """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment): this process never touches
-    the GPU.  It counts the GPUs in a throw-away child (visible_gpu_count), measures cpu_baseline (its
-    workers are fork()ed), then starts N child processes of this script, one per GPU (RANK = LOCAL_RANK
-    = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), hands them the baseline through a file, waits for all
-    of them and exits with the first failure's code.  Rank 0 prints the JSON line.  No exec: the
+    the GPU.  It counts the GPUs in a throw-away child (visible_gpu_count), then starts N child processes
+    of this script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), waits for
+    all of them and exits with the first failure's code.  cpu_baseline is an N = 1 figure (measured by
+    rank 0 of a one-GPU run only), so an N > 1 line carries none.  Rank 0 prints the JSON line.  No exec: the
     children are started as new processes, and the launcher checks it holds no GPU device open first."""
     import signal
     import subprocess
@@ -401,7 +401,7 @@ def launch_ranks(args):
     cfg = workload_cfg(args)
     env = dict(os.environ)
     tmp = None
-    if not args.no_cpu:
+    if not args.no_cpu and n == 1:  # never, here (n > 1): kept for a launcher of one rank
         cpu = measure_cpu_baseline(args, cfg)
         fd, tmp = tempfile.mkstemp(prefix="pquic_bench_cpu_", suffix=".json")
         with os.fdopen(fd, "w") as f:
@@ -778,7 +778,7 @@ def main():
     cfg = workload_cfg(args)
     k, r, e, L = cfg["k"], cfg["r"], cfg["e"], cfg["L"]
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu and world == 1:  # the CPU baseline is timed at N = 1 only
         path = os.environ.get("PQUIC_BENCH_CPU_JSON")
         if path:  # measured by the launcher before it started the ranks
             with open(path) as f:

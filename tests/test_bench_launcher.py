@@ -1,10 +1,10 @@
 """bench.py's multi-GPU launch paths, without a GPU (CPU suite).
 
 `python bench.py --gpus N` with no WORLD_SIZE in the environment must drive N ranks itself: the
-parent measures cpu_baseline (the reference pluglets on the host cores) and starts N child
-processes, never touching a GPU; rank 0's line carries n_gpus == N, the baseline and every rank's
-step time.  --dry-run swaps the device work for an empty timed region on gloo, so the launcher,
-rendezvous, max-over-ranks reduction and baseline hand-off run here.  A WORLD_SIZE that disagrees
+parent starts N child processes, never touching a GPU; rank 0's line carries n_gpus == N and every
+rank's step time.  cpu_baseline is an N = 1 figure (the reference pluglets on the host cores, rank 0 of
+a one-GPU run), so an N > 1 line carries none.  --dry-run swaps the device work for an empty timed
+region on gloo, so the launcher, rendezvous and max-over-ranks reduction run here.  A WORLD_SIZE that disagrees
 with --gpus is refused."""
 import json
 import os
@@ -40,6 +40,16 @@ def test_spawn_path_two_ranks(config):
     d = _line(p.stdout)
     assert d["n_gpus"] == 2 and d["dry_run"] is True
     assert len(d["per_rank_ms_per_step"]) == 2
+    assert d["cpu_baseline"] is None  # timed at N = 1 only
+
+
+@pytest.mark.skipif(not os.path.exists(ORACLE), reason="oracle not built (make -C oracle)")
+@pytest.mark.parametrize("config", ["k16", "k32r8"])
+def test_single_rank_carries_the_cpu_baseline(config):
+    p = _run(["--gpus", "1", "--config", config, "--dry-run", "--steps", "2", "--warmup", "1",
+              "--cpu-blocks", "64", "--cpu-seconds", "0.5"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
     cpu = d["cpu_baseline"]
     assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
     if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libfecref.so")):
